@@ -1,0 +1,32 @@
+"""Builds the MI355X codec library in-tree (hipcc, gfx950):
+capnproto-java_amd/lib/libcapnp_packed_hip.so.  Used by __graft_entry__.build()."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+SRC = PKG / "csrc" / "packed_codec.hip"
+HDR = PKG.parent / "include" / "capnp_packed.h"
+LIB = PKG / "lib" / "libcapnp_packed_hip.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("CPK_OFFLOAD_ARCH", "gfx950")
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    if (not force and LIB.exists()
+            and LIB.stat().st_mtime >= max(SRC.stat().st_mtime, HDR.stat().st_mtime)):
+        return LIB
+    LIB.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-value", "-Wno-unused-result", "-o", str(LIB), str(SRC)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,211 @@
+"""Host-side binding of the MI355X packed codec (C ABI: include/capnp_packed.h).
+
+Mirrors capnproto-java's packed API for the hot path:
+  * encode_batch / decode_batch -- n independent pieces, device-resident
+    (each piece = one PackedOutputStream.write / PackedInputStream.read,
+    runtime/src/main/java/org/capnproto/PackedOutputStream.java:35-205,
+    PackedInputStream.java:35-140).
+  * PackedOutputStream / PackedInputStream / SerializePacked in
+    capnp_packed.stream -- the reference's stream classes, same names and
+    error behaviour, routed through the batch kernels.
+
+torch is used only for device memory and streams.  There is no CPU fallback:
+if the HIP library cannot be loaded every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+import numpy as np
+
+_PKG = Path(__file__).resolve().parents[1]
+LIB_PATH = _PKG / "lib" / "libcapnp_packed_hip.so"
+
+OK, EINVAL, ETRUNC, EOVERRUN, ETRAILING, ENOMEM, EDEVICE, EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6, -8
+TILE_WORDS = 8192  # largest piece this build encodes/decodes
+
+EXPORTS = [
+    "cpk_abi_version", "cpk_status_string", "cpk_packed_bound", "cpk_batch_packed_capacity",
+    "cpk_ctx_create", "cpk_ctx_destroy", "cpk_ctx_device", "cpk_encode_batch",
+    "cpk_decode_batch", "cpk_encode_host", "cpk_decode_host", "cpk_generate",
+    "cpk_count_mismatch",
+]
+
+
+class CodecError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"{what}: {status_string(status)} ({status})" if what else status_string(status))
+
+
+class DecodeException(CodecError):
+    """org.capnproto.DecodeException (runtime/.../DecodeException.java:24-27)."""
+
+
+class GenParams(ctypes.Structure):
+    _fields_ = [("t_zero0", ctypes.c_uint64), ("t_z2n", ctypes.c_uint64),
+                ("t_n2z", ctypes.c_uint64), ("t_qbyte", ctypes.c_uint64),
+                ("cfg", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def load(path: Path | None = None) -> ctypes.CDLL:
+    """Load the HIP codec library; raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path or LIB_PATH)
+    if not p.exists():
+        raise ImportError(f"capnp_packed: HIP library {p} not built "
+                          "(run python capnproto-java_amd/build_native.py)")
+    L = ctypes.CDLL(str(p))
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "cpk_abi_version": ([], i32),
+        "cpk_status_string": ([i32], ctypes.c_char_p),
+        "cpk_packed_bound": ([u64], u64),
+        "cpk_batch_packed_capacity": ([vp, u32], u64),
+        "cpk_ctx_create": ([i32, ctypes.POINTER(vp)], i32),
+        "cpk_ctx_destroy": ([vp], None),
+        "cpk_ctx_device": ([vp], i32),
+        "cpk_encode_batch": ([vp, vp, vp, u32, u64, vp, vp, vp], i32),
+        "cpk_decode_batch": ([vp, vp, vp, vp, u32, vp, vp, vp], i32),
+        "cpk_encode_host": ([vp, vp, vp, u32, vp, u64, vp], i32),
+        "cpk_decode_host": ([vp, vp, vp, vp, u32, vp, vp], i32),
+        "cpk_generate": ([vp, ctypes.POINTER(GenParams), vp, u32, vp, vp], i32),
+        "cpk_count_mismatch": ([vp, vp, vp, u64, vp, vp], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def status_string(s: int) -> str:
+    try:
+        return load().cpk_status_string(int(s)).decode()
+    except ImportError:
+        return f"status {s}"
+
+
+def packed_bound(words: int) -> int:
+    return 8 * words + 2 * ((words + 1) // 2)
+
+
+def batch_capacity(seg_word_off: np.ndarray) -> int:
+    w = np.diff(np.asarray(seg_word_off, dtype=np.int64))
+    return int(8 * w.sum() + 2 * ((w + 1) // 2).sum() + 16)
+
+
+def _check(rc: int, what: str):
+    if rc != OK:
+        raise CodecError(rc, what)
+
+
+class Context:
+    """One HIP device + its look-back workspace (cpk_ctx_create)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load()
+        h = ctypes.c_void_p()
+        _check(self._lib.cpk_ctx_create(device, ctypes.byref(h)), "cpk_ctx_create")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.cpk_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- device-resident batch API (torch tensors) -----------------------
+    @staticmethod
+    def _stream(stream):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def encode_batch(self, d_in, d_seg_word_off, max_seg_words: int, d_out, d_out_off,
+                     stream=None):
+        n = d_seg_word_off.numel() - 1
+        rc = self._lib.cpk_encode_batch(self.handle, d_in.data_ptr(), d_seg_word_off.data_ptr(), n,
+                                        int(max_seg_words), d_out.data_ptr(), d_out_off.data_ptr(),
+                                        self._stream(stream))
+        _check(rc, "cpk_encode_batch")
+
+    def decode_batch(self, d_packed, d_in_off, d_seg_word_off, d_out, d_status, stream=None):
+        n = d_seg_word_off.numel() - 1
+        rc = self._lib.cpk_decode_batch(self.handle, d_packed.data_ptr(), d_in_off.data_ptr(),
+                                        d_seg_word_off.data_ptr(), n, d_out.data_ptr(),
+                                        d_status.data_ptr(), self._stream(stream))
+        _check(rc, "cpk_decode_batch")
+
+    def generate(self, params: GenParams, d_seg_word_off, d_out, stream=None):
+        n = d_seg_word_off.numel() - 1
+        _check(self._lib.cpk_generate(self.handle, ctypes.byref(params), d_seg_word_off.data_ptr(),
+                                      n, d_out.data_ptr(), self._stream(stream)), "cpk_generate")
+
+    def count_mismatch(self, d_a, d_b, words: int, d_cnt, stream=None):
+        _check(self._lib.cpk_count_mismatch(self.handle, d_a.data_ptr(), d_b.data_ptr(), int(words),
+                                            d_cnt.data_ptr(), self._stream(stream)),
+               "cpk_count_mismatch")
+
+    # ---- host-memory forms (numpy) -----------------------------------------
+    def encode_host(self, data: np.ndarray, seg_word_off: np.ndarray):
+        """-> (packed bytes as uint8 array, out_off uint64[n+1])."""
+        swo = np.ascontiguousarray(seg_word_off, dtype=np.uint64)
+        n = len(swo) - 1
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        cap = batch_capacity(swo)
+        out = np.zeros(cap, dtype=np.uint8)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        rc = self._lib.cpk_encode_host(self.handle, data.ctypes.data if data.size else None,
+                                       swo.ctypes.data, n, out.ctypes.data, cap, off.ctypes.data)
+        _check(rc, "cpk_encode_host")
+        return out[: int(off[-1])], off
+
+    def decode_host(self, packed: np.ndarray, in_off: np.ndarray, seg_word_off: np.ndarray):
+        """-> (decoded uint8 array, status int32[n]).  Never raises on bad data."""
+        swo = np.ascontiguousarray(seg_word_off, dtype=np.uint64)
+        io = np.ascontiguousarray(in_off, dtype=np.uint64)
+        n = len(swo) - 1
+        pk = np.ascontiguousarray(packed, dtype=np.uint8)
+        out = np.zeros(int(8 * swo[-1]) + 8, dtype=np.uint8)
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        rc = self._lib.cpk_decode_host(self.handle, pk.ctypes.data if pk.size else None,
+                                       io.ctypes.data, swo.ctypes.data, n, out.ctypes.data,
+                                       st.ctypes.data)
+        if rc not in (OK, ETRUNC, EOVERRUN, ETRAILING, EUNSUPPORTED, EINVAL):
+            _check(rc, "cpk_decode_host")
+        return out[: int(8 * swo[-1])], st[:n]
+
+
+def gen_params(cfg: int, z: float, lz: float, q: float) -> GenParams:
+    """Thresholds (out of 2^32) of the synthetic 2-state Markov generator."""
+    def thr(p):
+        return int(min(max(p, 0.0), 1.0) * (1 << 32))
+    a = 1.0 / lz
+    b = 1.0 if z >= 1.0 else a * z / (1.0 - z)
+    return GenParams(thr(z), thr(a), thr(b), thr(q), cfg, 0)
+
+
+CONFIGS = {
+    2: dict(z=0.5, lz=4.0, q=0.25),
+    3: dict(z=0.05, lz=1.5, q=1 / 256),
+    4: dict(z=0.9, lz=64.0, q=0.25),
+}
+
+
+def preset(cfg: int) -> GenParams:
+    c = CONFIGS[cfg]
+    return gen_params(cfg, c["z"], c["lz"], c["q"])

@@ -1,0 +1,141 @@
+/*
+ * capnp_packed.h -- C ABI of the MI355X (gfx950) packed-stream codec.
+ *
+ * Drop-in boundary for capnproto-java's packed encoding
+ * (runtime/src/main/java/org/capnproto/PackedOutputStream.java:35-205,
+ * PackedInputStream.java:35-140).  Plain pointers and sizes only; the JNI
+ * glue in capnproto-java_amd/java/ binds exactly these entry points
+ * (INTEGRATION.md).
+ *
+ * A "piece" is what one PackedOutputStream.write() / PackedInputStream.read()
+ * call handles.  Serialize.write issues one write() per segment and one for
+ * the segment table (Serialize.java:256-288), and each call starts from fresh
+ * run state (PackedOutputStream.java:36-43), so a batch of pieces is encoded
+ * and decoded independently, bit-exact with the reference.
+ *
+ * Threading: reentrant; a context may be used from one host thread at a time,
+ * different contexts concurrently.  All *_batch calls are asynchronous on the
+ * given stream (hipStream_t passed as void*; NULL = the device's null stream).
+ */
+#ifndef CAPNP_PACKED_H
+#define CAPNP_PACKED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPK_ABI_VERSION 1
+
+/* Status codes.  Decode errors are the reference's exceptions:
+ *   CPK_EINVAL    piece length not a multiple of 8 -> DecodeException
+ *                 ("PackedInputStream reads must be word-aligned",
+ *                 PackedInputStream.java:40-42); bad arguments.
+ *   CPK_ETRUNC    packed input ended before the piece was filled ->
+ *                 DecodeException (ArrayInputStream.java:53-58,
+ *                 PackedInputStream.java:93-95).  Also a literal run cut
+ *                 short by end of input, which the reference may accept
+ *                 silently through ArrayInputStream (documented divergence,
+ *                 DESIGN.md).
+ *   CPK_EOVERRUN  a 0x00/0xFF run runs past the end of the piece ->
+ *                 DecodeException / BufferOverflowException
+ *                 (PackedInputStream.java:99-105, :110-114).
+ *   CPK_ETRAILING batch form only: the piece was filled before the end of
+ *                 its packed byte range (the reference would leave the
+ *                 bytes to the next read()).
+ *   CPK_ENOMEM, CPK_EDEVICE  allocation / HIP runtime failure (-> IOException).
+ *   CPK_EUNSUPPORTED  a piece outside what this build handles.
+ */
+#define CPK_OK 0
+#define CPK_EINVAL (-1)
+#define CPK_ETRUNC (-2)
+#define CPK_EOVERRUN (-3)
+#define CPK_ETRAILING (-4)
+#define CPK_ENOMEM (-5)
+#define CPK_EDEVICE (-6)
+#define CPK_EUNSUPPORTED (-8)
+
+typedef struct cpk_ctx_s *cpk_ctx;
+
+int cpk_abi_version(void);
+const char *cpk_status_string(int status);
+
+/* Worst-case packed size of one piece of `words` words: 8w + 2*ceil(w/2).
+ * (An isolated all-nonzero word costs 10 bytes) */
+uint64_t cpk_packed_bound(uint64_t words);
+
+/* Capacity, in bytes, the caller must allocate for the packed output of a
+ * batch whose pieces have the given word counts: sum of the bounds plus 16
+ * bytes of read slack (the decoder reads whole 16-byte lines). */
+uint64_t cpk_batch_packed_capacity(const uint64_t *h_seg_word_off, uint32_t n);
+
+/* Context bound to one HIP device.  Holds the look-back workspace. */
+int cpk_ctx_create(int device, cpk_ctx *out);
+void cpk_ctx_destroy(cpk_ctx ctx);
+int cpk_ctx_device(cpk_ctx ctx);
+
+/* Batch encode of n pieces, device-resident (replaces n calls of
+ * PackedOutputStream.write, PackedOutputStream.java:35-205).
+ *   d_in            : 8-byte aligned words; piece i is words
+ *                     [d_seg_word_off[i], d_seg_word_off[i+1]).
+ *   d_seg_word_off  : uint64[n+1], device.
+ *   max_seg_words   : host hint = max piece size in words (0 = unknown).
+ *   d_out           : 16-byte aligned, capacity cpk_batch_packed_capacity().
+ *   d_out_off       : uint64[n+1], device, written: piece i's packed bytes
+ *                     are d_out[d_out_off[i] .. d_out_off[i+1]), contiguous
+ *                     and in order, i.e. exactly the bytes the reference
+ *                     writes for pieces 0..n-1 through one sink.
+ * Returns CPK_OK or an error; asynchronous on `stream`. */
+int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_seg_word_off,
+                     uint32_t n, uint64_t max_seg_words, void *d_out,
+                     uint64_t *d_out_off, void *stream);
+
+/* Batch decode of n pieces, device-resident (replaces n calls of
+ * PackedInputStream.read, PackedInputStream.java:35-140).
+ *   d_packed        : packed bytes, readable up to round_up(d_in_off[n], 16).
+ *   d_in_off        : uint64[n+1], device; piece i's packed bytes.
+ *   d_seg_word_off  : uint64[n+1], device; piece i's unpacked words.
+ *   d_out           : 8-byte aligned; piece i -> words d_seg_word_off[i]...
+ *   d_status        : int32[n], device, written per piece (CPK_* codes).
+ * Returns CPK_OK if launched; per-piece results are in d_status. */
+int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off,
+                     const uint64_t *d_seg_word_off, uint32_t n, void *d_out,
+                     int32_t *d_status, void *stream);
+
+/* Host-memory convenience forms (the socket/file ByteBuffer path,
+ * SerializePacked.java:75-96, :119-134): stage through device memory,
+ * run the batch kernels, copy back.  Synchronous.
+ *   cpk_encode_host: h_out capacity >= cpk_batch_packed_capacity();
+ *                    h_out_off[n+1] written.
+ *   cpk_decode_host: h_status[n] written; returns CPK_OK iff all pieces OK. */
+int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_seg_word_off,
+                    uint32_t n, void *h_out, uint64_t h_out_cap, uint64_t *h_out_off);
+int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
+                    const uint64_t *h_seg_word_off, uint32_t n, void *h_out,
+                    int32_t *h_status);
+
+/* ---- benchmark support (synthetic device-resident workloads) ---- */
+
+/* Device generator of the synthetic segments described in SURVEY.md 8d:
+ * a 2-state Markov chain over words (thresholds out of 2^32), seeded per
+ * segment from (cfg, segment index).  Identical stream to the host copy in
+ * oracle/packed_oracle.c:cpko_generate. */
+typedef struct {
+  uint64_t t_zero0, t_z2n, t_n2z, t_qbyte;
+  uint32_t cfg, pad;
+} cpk_gen_params;
+
+int cpk_generate(cpk_ctx ctx, const cpk_gen_params *params, const uint64_t *d_seg_word_off,
+                 uint32_t n, void *d_out, void *stream);
+
+/* Counts 8-byte words that differ between two device buffers into
+ * *d_mismatch (uint64, device, accumulated; zero it first). */
+int cpk_count_mismatch(cpk_ctx ctx, const void *d_a, const void *d_b, uint64_t words,
+                       uint64_t *d_mismatch, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

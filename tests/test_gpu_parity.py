@@ -1,0 +1,207 @@
+"""Parity of the HIP codec with the CPU oracle (which is pinned by the
+reference's KATs, tests/test_oracle.py).  Bit-exact: this is byte work.
+
+Mirrors SerializePackedTest.assertPacksTo (SerializePackedTest.java:63-91):
+every case is checked in both directions, through the C ABI.
+"""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.loads((Path(__file__).parent / "golden" / "reference_kats.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    import capnp_packed as cp
+    c = cp.Context(0)
+    yield c
+    c.close()
+
+
+def _swo(sizes):
+    return np.concatenate([[0], np.cumsum(np.asarray(sizes, dtype=np.uint64))]).astype(np.uint64)
+
+
+def _check_batch(ctx, oracle, data, swo):
+    """Encode on the GPU, compare with the oracle byte for byte, decode back."""
+    pk, off = ctx.encode_host(data, swo)
+    opk, ooff = oracle.pack_batch(data, swo, threads=8)
+    assert np.array_equal(off, ooff), "piece offsets differ"
+    assert np.array_equal(pk, opk), "packed bytes differ"
+    dec, st = ctx.decode_host(pk, off, swo)
+    assert (st == 0).all(), st[st != 0][:8]
+    assert np.array_equal(dec, data)
+    return pk, off
+
+
+def test_assert_packs_to_kats(ctx, oracle):
+    """Each SerializePackedTest.java:20-60 vector as a piece, then all of them
+    as one batch (pieces are independent write() calls)."""
+    import capnp_packed as cp
+    datas = []
+    for k in GOLD["kats"]:
+        u, p = bytes.fromhex(k["unpacked"]), bytes.fromhex(k["packed"])
+        a = np.frombuffer(u, dtype=np.uint8)
+        swo = _swo([len(u) // 8])
+        pk, off = ctx.encode_host(a, swo)
+        assert pk.tobytes() == p, k["source"]
+        dec, st = ctx.decode_host(np.frombuffer(p, np.uint8), np.array([0, len(p)], np.uint64), swo)
+        assert st[0] == cp.OK and dec.tobytes() == u, k["source"]
+        datas.append(u)
+    data = np.frombuffer(b"".join(datas), dtype=np.uint8)
+    _check_batch(ctx, oracle, data, _swo([len(d) // 8 for d in datas]))
+
+
+def _random_words(rng, n, probs):
+    kind = rng.choice(4, size=n, p=probs)
+    w = rng.integers(1, 256, size=(n, 8), dtype=np.uint8)
+    w[kind == 0] = 0
+    one = np.where(kind == 1)[0]
+    w[one, rng.integers(0, 8, size=one.size)] = 0
+    for i in np.where(kind == 2)[0]:
+        w[i, rng.choice(8, size=int(rng.integers(2, 8)), replace=False)] = 0
+    return w.reshape(-1)
+
+
+@pytest.mark.parametrize("mix", ["uniform", "dense", "sparse", "lonely_ff"])
+def test_random_class_mixes(ctx, oracle, mix):
+    rng = np.random.default_rng(abs(hash(mix)) % 2**32)
+    probs = {"uniform": [.25, .25, .25, .25], "dense": [.01, .7, .285, .005],
+             "sparse": [.85, .05, .05, .05], "lonely_ff": [.45, .05, .05, .45]}[mix]
+    sizes = list(rng.integers(0, 8193, size=40)) + [0, 1, 2, 255, 256, 257, 8191, 8192]
+    rng.shuffle(sizes)
+    # ragged pieces so that piece starts land at every byte phase
+    data = np.concatenate([_random_words(rng, int(s), probs) for s in sizes]).astype(np.uint8)
+    _check_batch(ctx, oracle, data, _swo(sizes))
+
+
+def test_long_literal_chains(ctx, oracle):
+    """D/L stretches far longer than 256 words: the 0xFF-run chain
+    (PackedOutputStream.java:145-161), incl. the 255 cap and L heads."""
+    rng = np.random.default_rng(3)
+    pieces = []
+    for n, pl in [(8192, 0.0), (8192, 0.3), (8192, 0.9), (5000, 0.5), (600, 0.99), (300, 0.0)]:
+        w = rng.integers(1, 256, size=(n, 8), dtype=np.uint8)
+        lmask = rng.random(n) < pl
+        w[lmask, rng.integers(0, 8, size=int(lmask.sum()))] = 0
+        pieces.append(w.reshape(-1))
+    # one all-ones piece: 200 words -> 0xFF, 199 (SerializePackedTest.java:54-60)
+    pieces.append(np.ones(8 * 8192, dtype=np.uint8))
+    pieces.append(np.zeros(8 * 8192, dtype=np.uint8))   # 0x00 runs capped at 255
+    data = np.concatenate(pieces)
+    _check_batch(ctx, oracle, data, _swo([len(p) // 8 for p in pieces]))
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4])
+def test_synthetic_configs(ctx, oracle, cfg):
+    """The bench workloads at 64 KiB pieces (configs 2/4; dense 3 at 64 KiB),
+    host-generated here and device-generated below."""
+    swo = _swo([8192] * 64 + [8191, 17, 4096])
+    data = oracle.generate(oracle.preset(cfg), swo)
+    _check_batch(ctx, oracle, data, swo)
+
+
+def test_device_generator_matches_host(ctx, oracle):
+    import torch
+    import capnp_packed as cp
+    swo = _swo([8192] * 8 + [3, 100, 0, 5000])
+    for cfg in (2, 3, 4):
+        d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
+        d = torch.zeros(int(swo[-1]) + 1, dtype=torch.int64, device="cuda")
+        ctx.generate(cp.preset(cfg), d_swo, d)
+        torch.cuda.synchronize()
+        host = oracle.generate(oracle.preset(cfg), swo)
+        assert np.array_equal(d.cpu().numpy().view(np.uint8)[: host.size], host)
+
+
+def test_device_resident_roundtrip(ctx, oracle):
+    """The bench path: device generator -> encode_batch -> decode_batch."""
+    import torch
+    import capnp_packed as cp
+    n = 512
+    swo = _swo([8192] * n)
+    d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
+    d_in = torch.empty(n * 8192, dtype=torch.int64, device="cuda")
+    ctx.generate(cp.preset(2), d_swo, d_in)
+    cap = cp.batch_capacity(swo)
+    d_pk = torch.empty((cap + 15) // 16 * 16, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    ctx.encode_batch(d_in, d_swo, 8192, d_pk, d_off)
+    d_out = torch.empty_like(d_in)
+    d_st = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.count_mismatch(d_in, d_out, n * 8192, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 0
+    assert int((d_st != 0).sum().item()) == 0
+    off = d_off.cpu().numpy().astype(np.uint64)
+    host = oracle.generate(oracle.preset(2), swo)
+    opk, ooff = oracle.pack_batch(host, swo, threads=8)
+    assert np.array_equal(off, ooff)
+    assert np.array_equal(d_pk[: int(off[-1])].cpu().numpy(), opk)
+
+
+def _corrupt_cases(oracle, rng):
+    """Valid packed pieces with bytes flipped / truncated / extended."""
+    cases = []
+    for _ in range(300):
+        n = int(rng.integers(1, 64))
+        u = _random_words(rng, n, [.3, .3, .2, .2]).tobytes()
+        p = bytearray(oracle.pack(u))
+        r = rng.integers(0, 4)
+        if r == 0 and len(p) > 1:
+            p = p[: int(rng.integers(0, len(p)))]                   # truncate
+        elif r == 1:
+            p += bytes(rng.integers(0, 256, size=int(rng.integers(1, 12)), dtype=np.uint8))
+        elif r == 2 and len(p):
+            i = int(rng.integers(0, len(p)))
+            p[i] = int(rng.integers(0, 256))                       # flip one byte
+        else:
+            n = max(1, n + int(rng.integers(-2, 3)))               # wrong piece size
+        cases.append((bytes(p), n))
+    return cases
+
+
+def test_malformed_streams_match_reference_errors(ctx, oracle):
+    """Per-piece status equals the oracle's for corrupted input (the reference
+    throws exactly when the oracle reports an error, SURVEY.md 8a policy)."""
+    rng = np.random.default_rng(11)
+    cases = _corrupt_cases(oracle, rng)
+    packed = b"".join(p for p, _ in cases)
+    in_off = _swo([len(p) for p, _ in cases])
+    swo = _swo([n for _, n in cases])
+    dec, st = ctx.decode_host(np.frombuffer(packed, np.uint8), in_off, swo)
+    for i, (p, n) in enumerate(cases):
+        ost, out, used = oracle.unpack(p, 8 * n)
+        if ost == oracle.OK and used != len(p):
+            ost = oracle.ETRAILING
+        assert st[i] == ost, (i, p.hex(), n, st[i], ost)
+        if ost == oracle.OK:
+            assert dec[8 * int(swo[i]): 8 * int(swo[i + 1])].tobytes() == out
+
+
+def test_serialize_packed_message(ctx, oracle):
+    """SerializePacked.write = pack(table) || pack(seg0) || ... (Serialize.java
+    :256-288): the table is one more piece of the batch."""
+    rng = np.random.default_rng(5)
+    segs = [_random_words(rng, int(s), [.4, .2, .2, .2]).tobytes() for s in (0, 1, 7, 4000, 33)]
+    n = len(segs)
+    table = (n - 1).to_bytes(4, "little") + b"".join((len(s) // 8).to_bytes(4, "little") for s in segs)
+    if len(table) % 8:
+        table += b"\0" * 4
+    pieces = [table] + segs
+    data = np.frombuffer(b"".join(pieces), np.uint8)
+    swo = _swo([len(p) // 8 for p in pieces])
+    pk, off = _check_batch(ctx, oracle, data, swo)
+    assert pk.tobytes() == oracle.write_message(segs)
+    st, got, _ = oracle.read_message(pk.tobytes())
+    assert st == 0 and got == segs
