@@ -271,15 +271,17 @@ __global__ __launch_bounds__(kThreads, 4) void encode_kernel(
   uint32_t *hbits = reinterpret_cast<uint32_t *>(smem + kEncHbits);
   int *scr = reinterpret_cast<int *>(smem + kEncScr);
   // scr[0..15] F1 wave totals, scr[16..23] B1, scr[32..39] F2,
-  // scr[64] ticket, scr[66..67] piece base (u64)
+  // scr[64..65] ticket (alternating), scr[66..67] piece base (u64)
 
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   fill_luts(lut, false);
 
-  for (;;) {
-    if (tid == 0) scr[64] = (int)atomicAdd(ticket, 1u);
+  for (uint32_t it = 0;; ++it) {
+    // ticket slot alternates: a wave still reading this piece's slot can
+    // never see the next piece's ticket (one barrier per iteration)
+    if (tid == 0) scr[64 + (it & 1)] = (int)atomicAdd(ticket, 1u);
     __syncthreads();  // also orders the previous piece's LDS use
-    const uint32_t seg = (uint32_t)scr[64];
+    const uint32_t seg = (uint32_t)scr[64 + (it & 1)];
     if (seg >= n) break;
     const uint64_t w0 = swo[seg];
     const int W = (int)(swo[seg + 1] - w0);  // <= kTileWords (host-checked)
@@ -706,10 +708,12 @@ __global__ __launch_bounds__(kThreads, 4) void decode_kernel(
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   fill_luts(lut, true);
 
-  for (;;) {
-    if (tid == 0) scr[64] = (int)atomicAdd(ticket, 1u);
+  for (uint32_t it = 0;; ++it) {
+    // ticket slot alternates: a wave still reading this piece's slot can
+    // never see the next piece's ticket (one barrier per iteration)
+    if (tid == 0) scr[64 + (it & 1)] = (int)atomicAdd(ticket, 1u);
     __syncthreads();
-    const uint32_t seg = (uint32_t)scr[64];
+    const uint32_t seg = (uint32_t)scr[64 + (it & 1)];
     if (seg >= n) break;
     const uint64_t w0 = swo[seg];
     const int W = (int)(swo[seg + 1] - w0);
