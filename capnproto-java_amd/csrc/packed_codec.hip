@@ -37,6 +37,14 @@ constexpr int kJ = 4;                           // chunks per lane
 constexpr int kWaveWords = 64 * kChunk * kJ;    // 1024
 constexpr int kTileWords = kWaves * kWaveWords; // 8192
 constexpr int kBig = 0x3fffffff;
+// encoder geometry: 1024 threads, 8 words per lane (2 chunks of 4)
+#ifndef CPK_ENC_WPE
+#define CPK_ENC_WPE 4  // waves per SIMD the encoder's registers must allow
+#endif
+constexpr int kEncThreads = 1024;
+constexpr int kEncWaves = kEncThreads / 64;                 // 16
+constexpr int kEncJ = kTileWords / (kEncThreads * kChunk);  // 2
+constexpr int kEncWaveWords = 64 * kChunk * kEncJ;          // 512
 
 // ---------------------------------------------------------------- LDS maps
 // Encoder: staging for the packed bytes of one piece (bound 9*8192 = 73,728)
@@ -46,21 +54,11 @@ constexpr uint32_t kEncLut = kEncStage;                 // u64[256]
 constexpr uint32_t kEncDbits = kEncLut + 2048;          // u32[256]
 constexpr uint32_t kEncHbits = kEncDbits + 1024;        // u32[256]
 constexpr uint32_t kEncScr = kEncHbits + 1024;          // int[128]
-constexpr uint32_t kEncLds = kEncScr + 512;             // 78,400 B -> 2 WG / CU
+constexpr uint32_t kEncMasks = kEncScr + 512;           // u64[16 waves][8 steps][2]
+constexpr uint32_t kEncLds = kEncMasks + 2048;          // 80,448 B -> 2 WG / CU
 
-// Decoder: LUT, resolve/blk region, scratch, packed bytes.
-constexpr uint32_t kDecPkCap = 9 * kTileWords;          // canonical bound
-constexpr uint32_t kDecLut = 0;                         // u64[256]
-constexpr uint32_t kDecReg = 2048;                      // 4736 B union
-constexpr uint32_t kDecScr = kDecReg + 4736;            // int[128]
-constexpr uint32_t kDecPk = kDecScr + 512;              // 7296, 16-aligned
-constexpr uint32_t kDecLds = kDecPk + 32 + kDecPkCap + 32;  // 81,088 B
-constexpr int kMaxChunks = 512;
-constexpr uint32_t kWarm = 16;                          // warm-up bytes per walk
-
-static_assert(kDecPk % 16 == 0, "packed region must be 16-aligned");
 static_assert(kEncLut % 16 == 0, "lut must be aligned");
-static_assert(kDecLds <= 81920 && kEncLds <= 81920, "2 workgroups per CU");
+static_assert(kEncLds <= 81920, "2 encoder workgroups per CU");
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
@@ -99,6 +97,34 @@ __device__ __forceinline__ int wave_sufx_min(int v) {
 __device__ __forceinline__ int readlane(int v, int l) {
   return __builtin_amdgcn_readlane(v, l);
 }
+
+// ---- diagnostic phase timing (built only with -DCPK_PHASE_STATS) ----------
+// Thread 0 of each workgroup accumulates s_memtime deltas per phase in LDS
+// (scr[96..127] as u64[16]) and adds them to g_phase at exit.  Shares of the
+// total, not absolute times, are what a stats build is good for.
+#ifdef CPK_PHASE_STATS
+__device__ unsigned long long g_phase[64];
+#define PH_INIT(scr)                                                         \
+  unsigned long long ph_last = 0;                                            \
+  unsigned long long *ph_acc = reinterpret_cast<unsigned long long *>(&(scr)[96]); \
+  if (threadIdx.x < 16) ph_acc[threadIdx.x] = 0;                            \
+  if (threadIdx.x == 0) ph_last = __builtin_amdgcn_s_memtime();
+#define PH(i)                                                                \
+  if (threadIdx.x == 0) {                                                    \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                    \
+    ph_acc[i] += t_ - ph_last;                                               \
+    ph_last = t_;                                                            \
+  }
+#define PH_ADD(i, v) if (threadIdx.x == 0) ph_acc[i] += (v);
+#define PH_FLUSH(base)                                                       \
+  __syncthreads();                                                           \
+  if (threadIdx.x < 16) atomicAdd(&g_phase[(base) + threadIdx.x], ph_acc[threadIdx.x]);
+#else
+#define PH_INIT(scr)
+#define PH(i)
+#define PH_ADD(i, v)
+#define PH_FLUSH(base)
+#endif
 
 // nonzero-byte mask of a 32-bit half: bit b set iff byte b != 0
 __device__ __forceinline__ uint32_t nzmask4(uint32_t d) {
@@ -146,14 +172,15 @@ __device__ __forceinline__ uint64_t ld_status(uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Called by all 64 lanes of one wave.  Returns the exclusive prefix.
-__device__ uint64_t lookback(uint64_t *status, uint32_t tile, uint64_t agg) {
+// Publish a tile's aggregate as early as it is known (one lane).
+__device__ __forceinline__ void lb_publish(uint64_t *status, uint32_t tile, uint64_t agg) {
+  st_status(&status[tile], (tile == 0 ? kFlagInc : kFlagAgg) | agg);
+}
+// Called by all 64 lanes of one wave after lb_publish.  Returns the
+// exclusive prefix and publishes the inclusive one.
+__device__ uint64_t lb_resolve(uint64_t *status, uint32_t tile, uint64_t agg) {
   const int lane = lane_id();
-  if (tile == 0) {
-    if (lane == 0) st_status(&status[0], kFlagInc | agg);
-    return 0;
-  }
-  if (lane == 0) st_status(&status[tile], kFlagAgg | agg);
+  if (tile == 0) return 0;
   uint64_t excl = 0;
   int64_t top = (int64_t)tile - 1;
   uint32_t spins = 0;
@@ -214,37 +241,6 @@ __device__ bool bm_any(const uint32_t *bits, int lo, int hi) {
   return false;
 }
 
-// Append string (d2:d1:d0, len bytes) to a chunk byte stream in LDS.
-struct Emitter {
-  uint32_t *stage32;
-  int dw, fill, first_dw, last_dw;
-  uint32_t a0;
-  __device__ __forceinline__ void put(int d, uint32_t v) {
-    if (d == first_dw || d == last_dw) atomicOr(&stage32[d], v);
-    else stage32[d] = v;
-  }
-  __device__ __forceinline__ void append(uint32_t d0, uint32_t d1, uint32_t d2, int len) {
-    if (len == 0) return;
-    uint32_t sh = 8u * (uint32_t)fill;
-    uint64_t s01 = (uint64_t)d0 | ((uint64_t)d1 << 32);
-    uint64_t lo64 = s01 << sh;
-    uint64_t hi64 = ((uint64_t)d2 << sh) | (sh ? (s01 >> (64 - sh)) : 0ull);
-    uint32_t t0 = (uint32_t)lo64 | a0, t1 = (uint32_t)(lo64 >> 32);
-    uint32_t t2 = (uint32_t)hi64, t3 = (uint32_t)(hi64 >> 32);
-    int nf = fill + len;
-    int k = nf >> 2;
-    if (k >= 1) put(dw, t0);
-    if (k >= 2) put(dw + 1, t1);
-    if (k >= 3) put(dw + 2, t2);
-    a0 = k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : t3;
-    dw += k;
-    fill = nf & 3;
-  }
-  __device__ __forceinline__ void finish() {
-    if (fill) put(dw, a0);
-  }
-};
-
 // Re-materialise a value so masks derived from it earlier cannot be kept
 // alive across a phase (hipcc otherwise CSEs ~60 per-word compare masks and
 // spills the SGPRs).
@@ -258,8 +254,30 @@ __device__ __forceinline__ uint32_t word_mask(uint32_t lo, uint32_t hi) {
   return nzmask4(lo) | (nzmask4(hi) << 4);
 }
 
+// Lane-per-word encoder.  A 1024-thread workgroup holds one piece of up to
+// 8192 words: wave w owns words [512w, 512w + 512) as 8 steps of 64
+// consecutive words (lane = word).  Runs, run ends, "last D" and byte
+// offsets are 64-bit ballot masks + mbcnt inside a step, wave-uniform carries
+// across steps, and one LDS exchange across waves.
+constexpr int kSteps = kTileWords / (kEncThreads);   // 8 steps of 64 words per wave
+
+__device__ __forceinline__ uint64_t lanemask_le() {
+  const int l = lane_id();
+  return l == 63 ? ~0ull : ((2ull << l) - 1);
+}
+// highest set bit of m as a lane index (m != 0)
+__device__ __forceinline__ int hi_bit(uint64_t m) { return 63 - __builtin_clzll(m); }
+__device__ __forceinline__ int lo_bit(uint64_t m) { return __builtin_ctzll(m); }
+// number of set bits of m below this lane
+__device__ __forceinline__ int mbcnt(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// info word per (step, lane): [7:0] nonzero mask, [9:8] group,
+// [10] member, [11] zero-run head, [15:12] bytes, [23:16] run count
 template <bool kUnused = false>
-__global__ __launch_bounds__(kThreads, 4) void encode_kernel(
+__global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status,
     uint32_t *ticket) {
@@ -270,701 +288,647 @@ __global__ __launch_bounds__(kThreads, 4) void encode_kernel(
   uint32_t *dbits = reinterpret_cast<uint32_t *>(smem + kEncDbits);
   uint32_t *hbits = reinterpret_cast<uint32_t *>(smem + kEncHbits);
   int *scr = reinterpret_cast<int *>(smem + kEncScr);
-  // scr[0..15] F1 wave totals, scr[16..23] B1, scr[32..39] F2,
-  // scr[64..65] ticket (alternating), scr[66..67] piece base (u64)
+  uint64_t *mks = reinterpret_cast<uint64_t *>(smem + kEncMasks);
+  // scr[0..15] last run start per wave, [16..31] first run start,
+  // [32..47] last D, [48..63] bytes per wave, [64..65] ticket, [66..67] base
 
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   fill_luts(lut, false);
+  PH_INIT(scr)
 
   for (uint32_t it = 0;; ++it) {
-    // ticket slot alternates: a wave still reading this piece's slot can
-    // never see the next piece's ticket (one barrier per iteration)
     if (tid == 0) scr[64 + (it & 1)] = (int)atomicAdd(ticket, 1u);
     __syncthreads();  // also orders the previous piece's LDS use
-    const uint32_t seg = (uint32_t)scr[64 + (it & 1)];
+    const uint32_t seg = (uint32_t)__builtin_amdgcn_readfirstlane(scr[64 + (it & 1)]);
     if (seg >= n) break;
+    PH(0)
     const uint64_t w0 = swo[seg];
     const int W = (int)(swo[seg + 1] - w0);  // <= kTileWords (host-checked)
-    // opaque per piece: stops the compiler hoisting per-lane address math
-    // out of the persistent loop (it spilled it all to scratch)
-    int kbase = w * kWaveWords + lane * kChunk;
-    asm volatile("" : "+v"(kbase));
-#define KW(j, i) (kbase + (j) * 256 + (i))
-#define BIT(j, i) (1u << ((j) * kChunk + (i)))
+    // per-piece opaque copies of this wave's / lane's first word: keep hipcc
+    // from hoisting ~100 per-lane addresses out of the persistent loop
+    int wb = __builtin_amdgcn_readfirstlane(w * (kSteps * 64));  // first word of this wave
+    asm volatile("" : "+s"(wb));
+    int k0 = wb + lane;
+    asm volatile("" : "+v"(k0));
 
-    // ---- load + classify ----------------------------------------------------
-    // vbits: bit (j*4+i) set iff word (j,i) is inside the piece.  Loads are
-    // clamped to the last word instead of predicated (no per-word branches).
-    uint32_t vbits = 0;
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      int nv = min(max(W - (kbase + j * 256), 0), kChunk);
-      vbits |= ((1u << nv) - 1) << (j * kChunk);
-    }
-    uint32_t lo[kJ][kChunk], hi[kJ][kChunk];
-    uint32_t msk4[kJ];  // nonzero-byte mask of word i in byte i
+    // ---- pass 1: load, classify, run-start and D masks --------------------
+    uint32_t lo[kSteps], hi[kSteps], info[kSteps];
+    // run-start / D ballots of each step live in LDS (wave-private rows):
+    // kept in SGPRs they spilled.
+    uint64_t *mrow = mks + (wb >> 9) * (2 * kSteps);
+#define SMASK(s) mrow[2 * (s)]
+#define DMASK(s) mrow[2 * (s) + 1]
     const uint64_t *src = in + w0;
-    const int wlast = max(W - 1, 0);
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-#pragma unroll
-      for (int i = 0; i < kChunk; ++i) {
-        uint64_t v = W ? src[min(KW(j, i), wlast)] : 0ull;
-        v = (vbits & BIT(j, i)) ? v : 0ull;
-        lo[j][i] = (uint32_t)v;
-        hi[j][i] = (uint32_t)(v >> 32);
-      }
-      uint32_t m4 = 0;
-#pragma unroll
-      for (int i = 0; i < kChunk; ++i) m4 |= word_mask(lo[j][i], hi[j][i]) << (8 * i);
-      msk4[j] = m4;
+    for (int s = 0; s < kSteps; ++s) {
+      const int k = k0 + s * 64;
+      uint64_t v = k < W ? src[k] : 0ull;
+      lo[s] = (uint32_t)v;
+      hi[s] = (uint32_t)(v >> 32);
     }
-#define MSK(j, i) ((msk4[j] >> (8 * (i))) & 0xffu)
-#define VALID(j, i) ((vbits & BIT(j, i)) != 0)
-    // group of the word just before this wave's first word
-    int gprev = 3;
-    if (w > 0 && lane == 0) {
-      int k = w * kWaveWords - 1;
-      if (k < W) {
-        uint64_t v = in[w0 + k];
-        gprev = grp_of(word_mask((uint32_t)v, (uint32_t)(v >> 32)));
-      }
+    int gprev = 3;  // group of word wb - 1
+    if (w > 0 && lane == 0 && wb - 1 < W) {
+      uint64_t v = src[wb - 1];
+      gprev = grp_of(word_mask((uint32_t)v, (uint32_t)(v >> 32)));
     }
     gprev = readlane(gprev, 0);
-
-    // run starts: word k < W starts a run if k == 0 or its group differs
-    uint32_t sbits = 0;
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      const int glast = VALID(j, kChunk - 1) ? grp_of(MSK(j, kChunk - 1)) : 3;
-      int pg = wave_shr1(glast, gprev);
-      int gp = pg;
-#pragma unroll
-      for (int i = 0; i < kChunk; ++i) {
-        const int k = KW(j, i);
-        const int g = VALID(j, i) ? grp_of(MSK(j, i)) : 3;
-        if (g != 3 && (k == 0 || g != gp)) sbits |= BIT(j, i);
-        gp = g;
+    for (int s = 0; s < kSteps; ++s) {
+      const int k = k0 + s * 64;
+      const uint32_t m = word_mask(lo[s], hi[s]);
+      const int g = k < W ? grp_of(m) : 3;
+      const int gp = wave_shr1(g, gprev);
+      const uint64_t sb = __ballot(g != 3 && (k == 0 || g != gp));
+      const uint64_t db = __ballot(k < W && m == 0xffu);
+      if (lane == 0) {
+        SMASK(s) = sb;
+        DMASK(s) = db;
       }
-      gprev = readlane(glast, 63);
+      gprev = readlane(g, 63);
+      info[s] = m | ((uint32_t)g << 8);
     }
-
-    // ---- B1: run end e(k) = next run start after k (or W) ----------------
-    CPK_OPAQUE(sbits);
-    CPK_OPAQUE(vbits);
-    // erel[j]: e - k of words (j,0),(j,1) in halves of erel[j][0], etc.
-    uint32_t erel[kJ][2];
     {
-      int cE = kBig;
-      int pE[kJ];
+      int ls = -1, fs = kBig, ld = -1;
 #pragma unroll
-      for (int j = kJ - 1; j >= 0; --j) {
-        int aE = kBig;
-#pragma unroll
-        for (int i = kChunk - 1; i >= 0; --i)
-          if (sbits & BIT(j, i)) aE = KW(j, i);
-        int iE = wave_sufx_min(aE);
-        int xE = __shfl(iE, min(lane + 1, 63), 64);
-        if (lane == 63) xE = kBig;
-        pE[j] = min(cE, xE);
-        cE = min(cE, readlane(iE, 0));
-      }
-      if (lane == 0) scr[16 + w] = cE;
-      __syncthreads();
-      int wE = kBig;
-      for (int q = w + 1; q < kWaves; ++q) wE = min(wE, scr[16 + q]);
-#pragma unroll
-      for (int j = 0; j < kJ; ++j) {
-        int r = min(wE, pE[j]);
-        uint32_t e3, e2, e1, e0;
-        e3 = (uint32_t)max(min(r, W) - KW(j, 3), 0);
-        if (sbits & BIT(j, 3)) r = KW(j, 3);
-        e2 = (uint32_t)max(min(r, W) - KW(j, 2), 0);
-        if (sbits & BIT(j, 2)) r = KW(j, 2);
-        e1 = (uint32_t)max(min(r, W) - KW(j, 1), 0);
-        if (sbits & BIT(j, 1)) r = KW(j, 1);
-        e0 = (uint32_t)max(min(r, W) - KW(j, 0), 0);
-        erel[j][0] = e0 | (e1 << 16);
-        erel[j][1] = e2 | (e3 << 16);
-      }
-    }
-#define EREL(j, i) ((erel[j][(i) >> 1] >> (16 * ((i) & 1))) & 0xffffu)
-
-    // ---- F1: run start s(k), last D before k -> roles ---------------------
-    // zhead : Z word that emits a 0x00 tag (every 256th word of its run,
-    //         PackedOutputStream.java:125-131)
-    // member: D/L word copied verbatim inside a 0xFF literal run (:133-193)
-    // lng   : D/L word of a stretch longer than 256 words (chain below)
-    // cnt4  : run count byte of Z / D heads, min(255, e - k - 1)
-    uint32_t zhead = 0, member = 0, lng = 0;
-    uint32_t cnt4[kJ];
-    CPK_OPAQUE(sbits);
-    CPK_OPAQUE(vbits);
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) CPK_OPAQUE(msk4[j]);
-    {
-      int cS = -1, cD = -1;
-      int pS[kJ], pD[kJ];
-#pragma unroll
-      for (int j = 0; j < kJ; ++j) {
-        int aS = -1, aD = -1;
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-          if (sbits & BIT(j, i)) aS = KW(j, i);
-          if (MSK(j, i) == 0xffu) aD = KW(j, i);
+      for (int s = 0; s < kSteps; ++s) {
+        const uint64_t sb = SMASK(s), db = DMASK(s);
+        if (sb) {
+          ls = wb + s * 64 + hi_bit(sb);
+          if (fs == kBig) fs = wb + s * 64 + lo_bit(sb);
         }
-        int iS = wave_incl_max(aS), iD = wave_incl_max(aD);
-        pS[j] = max(cS, wave_shr1(iS, -1));
-        pD[j] = max(cD, wave_shr1(iD, -1));
-        cS = max(cS, readlane(iS, 63));
-        cD = max(cD, readlane(iD, 63));
+        if (db) ld = wb + s * 64 + hi_bit(db);
       }
       if (lane == 0) {
-        scr[2 * w] = cS;
-        scr[2 * w + 1] = cD;
+        scr[w] = ls;
+        scr[16 + w] = fs;
+        scr[32 + w] = ld;
       }
-      __syncthreads();
-      int wS = -1, wD = -1;
-      for (int q = 0; q < w; ++q) {
-        wS = max(wS, scr[2 * q]);
-        wD = max(wD, scr[2 * q + 1]);
-      }
+    }
+    __syncthreads();
+    PH(1)
+    // carries across waves: run start / last D entering this wave, first
+    // run start after it
+    int cS = -1, cD = -1, eOut = W;
+    for (int q = 0; q < w; ++q) {
+      cS = max(cS, scr[q]);
+      cD = max(cD, scr[32 + q]);
+    }
+    for (int q = kEncWaves - 1; q > w; --q) eOut = scr[16 + q] < kBig ? min(eOut, scr[16 + q]) : eOut;
+    // first run start in steps after s (within the wave), else eOut
+    int nextS[kSteps];
+    {
+      int r = eOut;
 #pragma unroll
-      for (int j = 0; j < kJ; ++j) {
-        int rs = max(wS, pS[j]), rd = max(wD, pD[j]);
-        uint32_t c4 = 0;
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-          const int k = KW(j, i);
-          const uint32_t m = MSK(j, i);
-          if (sbits & BIT(j, i)) rs = k;
-          const int er = (int)EREL(j, i);
-          c4 |= (uint32_t)min(255, max(er - 1, 0)) << (8 * i);
-          if (VALID(j, i)) {
-            const int g = grp_of(m);
-            if (g == 0 && ((k - rs) & 255) == 0) zhead |= BIT(j, i);
-            if (g == 1) {
-              if (k + er - rs > 256) lng |= BIT(j, i);
-              else if (rd >= rs) member |= BIT(j, i);
-            }
-          }
-          if (m == 0xffu) rd = k;
-        }
-        cnt4[j] = c4;
+      for (int s = kSteps - 1; s >= 0; --s) {
+        nextS[s] = r;
+        const uint64_t sb = SMASK(s);
+        if (sb) r = wb + s * 64 + lo_bit(sb);
       }
     }
 
-    if (__syncthreads_or(lng != 0)) {
+    // ---- pass 2: roles (PackedOutputStream.java:119-193 restated per word) --
+    const uint64_t le = lanemask_le();
+    int anyLong = 0;
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+      const int k = k0 + s * 64;
+      const int base = wb + s * 64;
+      const uint32_t m = info[s] & 0xffu;
+      const int g = (int)((info[s] >> 8) & 3);
+      const uint64_t smask_s = SMASK(s), dmask_s = DMASK(s);
+      const uint64_t sm = smask_s & le;
+      const int rs = sm ? base + hi_bit(sm) : cS;          // run start s(k)
+      const uint64_t sg = smask_s & ~le;
+      const int re = sg ? base + lo_bit(sg) : nextS[s];    // run end e(k)
+      const uint64_t dm = dmask_s & (le >> 1);             // D words before k
+      const int rd = dm ? base + hi_bit(dm) : cD;          // last D before k
+      uint32_t x = info[s];
+      int nb = 0;
+      if (g == 0) {
+        // every 256th word of a zero run is a 0x00 head (the 255 cap, :125-127)
+        if (((k - rs) & 255) == 0) {
+          x |= 1u << 11;
+          nb = 2;
+        }
+      } else if (g == 1) {
+        if (re - rs > 256) {
+          anyLong = 1;  // resolved by the chain walk below
+          nb = 8;       // provisional: L words are 8 either way, D fixed below
+        } else if (rd >= rs) {
+          x |= 1u << 10;  // inside the 0xFF run of the stretch's first D
+          nb = 8;
+        } else {
+          nb = m == 0xffu ? 10 : 8;
+        }
+      } else if (g == 2) {
+        nb = 1 + __builtin_popcount(m);
+      }
+      const uint32_t cnt = (uint32_t)min(255, max(re - k - 1, 0));
+      info[s] = (x & 0x7ffu) | ((uint32_t)nb << 12) | (cnt << 16);
+      if (smask_s) cS = base + hi_bit(smask_s);
+      if (dmask_s) cD = base + hi_bit(dmask_s);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    PH(2)
+    if (__syncthreads_or(anyLong)) {
       // D/L stretch longer than 256 words: heads chain h1 = first D,
-      // h' = first D at or after h + 256 (the 255-word cap of
-      // PackedOutputStream.java:145-147).  Walked by the run's first word.
-      // dbits = D words, hbits = run starts, then (after the walk) heads.
+      // h' = first D at or after h + 256 (PackedOutputStream.java:145-161).
       if (tid < 256) dbits[tid] = 0;
-      else hbits[tid - 256] = 0;
+      else if (tid < 512) hbits[tid - 256] = 0;
       __syncthreads();
+      // bitmaps are built from the ballots: lane 0 / 1 write 32-bit halves
 #pragma unroll
-      for (int j = 0; j < kJ; ++j)
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-          const int k = KW(j, i);
-          if (MSK(j, i) == 0xffu && VALID(j, i)) atomicOr(&dbits[k >> 5], 1u << (k & 31));
-          if (sbits & BIT(j, i)) atomicOr(&hbits[k >> 5], 1u << (k & 31));
+      for (int s = 0; s < kSteps; ++s) {
+        const int dw = (wb + s * 64) >> 5;
+        if (lane == 0) {
+          dbits[dw] = (uint32_t)DMASK(s);
+          hbits[dw] = (uint32_t)SMASK(s);
+        } else if (lane == 1) {
+          dbits[dw + 1] = (uint32_t)(DMASK(s) >> 32);
+          hbits[dw + 1] = (uint32_t)(SMASK(s) >> 32);
         }
+      }
       __syncthreads();
-      // run start of every long-stretch word (last start bit <= k)
-      int sl[kJ][kChunk];
+      // run start of every long-stretch word, then clear hbits for heads
+      int sl[kSteps];
 #pragma unroll
-      for (int j = 0; j < kJ; ++j)
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-          sl[j][i] = 0;
-          if (lng & BIT(j, i)) {
-            int k = KW(j, i), d = k >> 5;
-            uint32_t m = hbits[d] & ((k & 31) == 31 ? ~0u : ((2u << (k & 31)) - 1));
-            while (!m) m = hbits[--d];
-            sl[j][i] = d * 32 + 31 - __builtin_clz(m);
-          }
+      for (int s = 0; s < kSteps; ++s) {
+        sl[s] = 0;
+        const int k = k0 + s * 64;
+        const int nb = (int)((info[s] >> 12) & 15);
+        const int g = (int)((info[s] >> 8) & 3);
+        const int re = k + 1 + (int)(info[s] >> 16);  // only exact when < 255
+        (void)re;
+        if (g == 1 && !(info[s] & (1u << 10)) && nb == 8) {
+          int d = k >> 5;
+          uint32_t mm = hbits[d] & ((k & 31) == 31 ? ~0u : ((2u << (k & 31)) - 1));
+          while (!mm) mm = hbits[--d];
+          sl[s] = d * 32 + 31 - __builtin_clz(mm);
         }
+      }
       __syncthreads();
       if (tid < 256) hbits[tid] = 0;
       __syncthreads();
+      // walkers: the first word of each long stretch
 #pragma unroll
-      for (int j = 0; j < kJ; ++j)
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-          if ((lng & sbits & BIT(j, i)) == 0) continue;
-          const int k = KW(j, i);
-          const int e = k + (int)EREL(j, i);
-          int h = bm_next(dbits, k, e);
-          while (h < e) {
+      for (int s = 0; s < kSteps; ++s) {
+        const int k = k0 + s * 64;
+        const int base = wb + s * 64;
+        const uint64_t sg = SMASK(s) & ~lanemask_le();
+        const int re = sg ? base + lo_bit(sg) : nextS[s];
+        const bool st = (SMASK(s) >> lane) & 1;
+        if (st && ((info[s] >> 8) & 3) == 1 && re - k > 256) {
+          int h = bm_next(dbits, k, re);
+          while (h < re) {
             atomicOr(&hbits[h >> 5], 1u << (h & 31));
-            int p = h + 256;
-            if (p >= e) break;
-            h = bm_next(dbits, p, e);
+            const int p = h + 256;
+            if (p >= re) break;
+            h = bm_next(dbits, p, re);
           }
         }
+      }
       __syncthreads();
 #pragma unroll
-      for (int j = 0; j < kJ; ++j)
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) {
-          if ((lng & BIT(j, i)) == 0) continue;
-          const int k = KW(j, i);
-          if (bm_any(hbits, max(sl[j][i], k - 255), k - 1)) member |= BIT(j, i);
+      for (int s = 0; s < kSteps; ++s) {
+        const int k = k0 + s * 64;
+        const int base = wb + s * 64;
+        const uint32_t m = info[s] & 0xffu;
+        const int g = (int)((info[s] >> 8) & 3);
+        const uint64_t sm = SMASK(s) & lanemask_le();
+        const uint64_t sg = SMASK(s) & ~lanemask_le();
+        const int re = sg ? base + lo_bit(sg) : nextS[s];
+        if (g == 1 && re - sl[s] > 256 && !(info[s] & (1u << 10))) {
+          (void)sm;
+          const bool mem = bm_any(hbits, max(sl[s], k - 255), k - 1);
+          const int nb = mem ? 8 : (m == 0xffu ? 10 : 8);
+          info[s] = (info[s] & ~(0xfu << 12)) | ((uint32_t)nb << 12) | (mem ? (1u << 10) : 0u);
         }
+      }
     }
+    PH(3)
 
-    // bytes emitted by word (j, i)
-#define NBYTES(j, i)                                                              \
-  (!VALID(j, i) ? 0                                                               \
-   : MSK(j, i) == 0 ? ((zhead & BIT(j, i)) ? 2 : 0)                               \
-   : (member & BIT(j, i)) ? 8                                                     \
-   : (MSK(j, i) == 0xffu ? 10 : 1 + __builtin_popcount(MSK(j, i))))
-
-    // ---- F2: byte offsets (exclusive sum over the piece) ------------------
-    CPK_OPAQUE(vbits);
-    CPK_OPAQUE(zhead);
-    CPK_OPAQUE(member);
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) CPK_OPAQUE(msk4[j]);
-    int choff[kJ], chlen[kJ];
-    int total;
+    // ---- bytes per wave -> piece offsets -----------------------------------
     {
-      int c = 0;
+      int tot = 0;
 #pragma unroll
-      for (int j = 0; j < kJ; ++j) {
-        int a = 0;
-#pragma unroll
-        for (int i = 0; i < kChunk; ++i) a += NBYTES(j, i);
-        chlen[j] = a;
-        int inc = wave_incl_add(a);
-        choff[j] = c + inc - a;
-        c += readlane(inc, 63);
+      for (int s = 0; s < kSteps; ++s) {
+        const uint32_t nb = (info[s] >> 12) & 15u;
+        tot += __popcll(__ballot(nb & 1)) + 2 * __popcll(__ballot(nb & 2)) +
+               4 * __popcll(__ballot(nb & 4)) + 8 * __popcll(__ballot(nb & 8));
       }
-      if (lane == 0) scr[32 + w] = c;
-      __syncthreads();
-      int wb = 0;
-      total = 0;
-      for (int q = 0; q < kWaves; ++q) {
-        int t = scr[32 + q];
-        if (q < w) wb += t;
-        total += t;
-      }
-#pragma unroll
-      for (int j = 0; j < kJ; ++j) choff[j] += wb;
+      if (lane == 0) scr[48 + w] = tot;
     }
+    __syncthreads();
+    int wbytes = 0, total = 0;
+    for (int q = 0; q < kEncWaves; ++q) {
+      const int t = scr[48 + q];
+      if (q < w) wbytes += t;
+      total += t;
+    }
+    // publish the aggregate now; the prefix is resolved after compaction
+    if (tid == 0) lb_publish(status, seg, (uint64_t)total);
+    // zero the staging lines this piece uses (the strings are OR-ed in)
+    {
+      const int nl = (total + 19) >> 4;
+      uint4 z = {0u, 0u, 0u, 0u};
+      for (int c = tid; c < nl; c += kEncThreads) reinterpret_cast<uint4 *>(stage)[c] = z;
+    }
+    __syncthreads();
+    PH(4)
 
-    // ---- look-back for the piece's output offset ---------------------------
+    // ---- pass 3: packed strings into LDS ------------------------------------
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+      const uint32_t x = info[s];
+      const uint32_t nb = (x >> 12) & 15u;
+      const uint64_t b0 = __ballot(nb & 1), b1 = __ballot(nb & 2), b2 = __ballot(nb & 4),
+                     b3 = __ballot(nb & 8);
+      const int o = wbytes + mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2) + 8 * mbcnt(b3);
+      wbytes += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) + 8 * __popcll(b3);
+      if (nb == 0) continue;
+      const uint32_t l = lo[s], h = hi[s], m = x & 0xffu;
+      uint32_t d0, d1, d2;
+      if (x & (1u << 10)) {  // literal-run member: 8 bytes verbatim
+        d0 = l;
+        d1 = h;
+        d2 = 0;
+      } else {  // tag + nonzero bytes (+ count after 0x00 / 0xFF tags)
+        const uint64_t sel = lut[m];
+        const uint32_t c0 = __builtin_amdgcn_perm(h, l, (uint32_t)sel);
+        const uint32_t c1 = __builtin_amdgcn_perm(h, l, (uint32_t)(sel >> 32));
+        const uint32_t cnt = x >> 16;
+        d0 = m | (c0 << 8);
+        d1 = (c0 >> 24) | (c1 << 8);
+        d2 = c1 >> 24;
+        if (m == 0) d0 |= cnt << 8;
+        else if (m == 0xffu) d2 |= cnt << 8;
+      }
+      // place bytes [o, o + nb): dword-shift the 3-dword string
+      const uint32_t sh = (uint32_t)(o & 3) * 8u;
+      const uint64_t s01 = (uint64_t)d0 | ((uint64_t)d1 << 32);
+      const uint64_t lo64 = s01 << sh;
+      const uint64_t hi64 = ((uint64_t)d2 << sh) | (sh ? (s01 >> (64 - sh)) : 0ull);
+      uint32_t *dst = stage32 + (o >> 2);
+      const int end = (o & 3) + (int)nb;  // bytes covered from dst[0]
+      atomicOr(&dst[0], (uint32_t)lo64);
+      if (end > 4) {
+        if (end >= 8) dst[1] = (uint32_t)(lo64 >> 32);
+        else atomicOr(&dst[1], (uint32_t)(lo64 >> 32));
+      }
+      if (end > 8) {
+        if (end >= 12) dst[2] = (uint32_t)hi64;
+        else atomicOr(&dst[2], (uint32_t)hi64);
+      }
+      if (end > 12) atomicOr(&dst[3], (uint32_t)(hi64 >> 32));
+      __builtin_amdgcn_sched_barrier(0);  // one step at a time: bounds VGPRs
+    }
+    PH(5)
+
+    // ---- decoupled look-back (wave 0), overlapped with the compaction -----
     if (w == 0) {
-      uint64_t base = lookback(status, seg, (uint64_t)total);
+      uint64_t b = lb_resolve(status, seg, (uint64_t)total);
       if (lane == 0) {
-        *reinterpret_cast<uint64_t *>(&scr[66]) = base;
-        out_off[seg] = base;
-        if (seg == n - 1) out_off[n] = base + (uint64_t)total;
+        *reinterpret_cast<uint64_t *>(&scr[66]) = b;
+        out_off[seg] = b;
+        if (seg == n - 1) out_off[n] = b + (uint64_t)total;
       }
     }
     __syncthreads();
-    const uint64_t base = *reinterpret_cast<uint64_t *>(&scr[66]);
-    const int pad = (int)(base & 15);
-
-    // ---- compact the packed bytes into LDS ----------------------------------
-    CPK_OPAQUE(vbits);
-    CPK_OPAQUE(zhead);
-    CPK_OPAQUE(member);
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) CPK_OPAQUE(msk4[j]);
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      if (chlen[j] > 0) {
-        int cs = pad + choff[j], ce = cs + chlen[j];
-        stage32[cs >> 2] = 0;
-        stage32[(ce - 1) >> 2] = 0;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      if (chlen[j] == 0) continue;
-      const int cs = pad + choff[j], ce = cs + chlen[j];
-      Emitter em;
-      em.stage32 = stage32;
-      em.dw = cs >> 2;
-      em.fill = cs & 3;
-      em.first_dw = cs >> 2;
-      em.last_dw = (ce - 1) >> 2;
-      em.a0 = 0;
-#pragma unroll
-      for (int i = 0; i < kChunk; ++i) {
-        const int len = NBYTES(j, i);
-        if (len == 0) continue;
-        const uint32_t l = lo[j][i], h = hi[j][i], m = MSK(j, i);
-        uint32_t d0, d1, d2;
-        if (member & BIT(j, i)) {
-          d0 = l;
-          d1 = h;
-          d2 = 0;
-        } else {
-          const uint64_t sel = lut[m];
-          const uint32_t c0 = __builtin_amdgcn_perm(h, l, (uint32_t)sel);
-          const uint32_t c1 = __builtin_amdgcn_perm(h, l, (uint32_t)(sel >> 32));
-          d0 = m | (c0 << 8);
-          d1 = (c0 >> 24) | (c1 << 8);
-          d2 = c1 >> 24;
-          // run count after the tag (and after the 8 bytes of a 0xFF word),
-          // capped at 255 (PackedOutputStream.java:125-131, :145-164)
-          const uint32_t cnt = (cnt4[j] >> (8 * i)) & 0xffu;
-          if (m == 0) d0 |= cnt << 8;
-          else if (m == 0xffu) d2 |= cnt << 8;
-        }
-        em.append(d0, d1, d2, len);
-      }
-      em.finish();
-    }
-    __syncthreads();
-
+    PH(6)
     // ---- store: 16-byte lines, byte stores at the two shared edges --------
+    // staged byte x is global byte base + x; line L covers global
+    // [A + 16L, A + 16L + 16), A = base & ~15, i.e. staged x = 16L - pad.
     {
+      const uint64_t base = *reinterpret_cast<uint64_t *>(&scr[66]);
+      const int pad = (int)(base & 15);
       const int tb = pad + total;
       uint8_t *gbase = out + (base - (uint64_t)pad);
       const int nl = (tb + 15) >> 4;
-      for (int c = tid; c < nl; c += kThreads) {
-        int lo16 = c * 16, hi16 = lo16 + 16;
+      const uint32_t sh = (uint32_t)((16 - pad) & 3);  // (16L - pad) & 3
+      for (int c = tid; c < nl; c += kEncThreads) {
+        const int lo16 = c * 16, hi16 = lo16 + 16;
         if (lo16 >= pad && hi16 <= tb) {
-          *reinterpret_cast<uint4 *>(gbase + lo16) = *reinterpret_cast<const uint4 *>(stage + lo16);
+          const uint32_t *a = stage32 + ((lo16 - pad) >> 2);
+          uint32_t e0 = a[0], e1 = a[1], e2 = a[2], e3 = a[3], e4 = sh ? a[4] : 0u;
+          uint4 v;
+          v.x = __builtin_amdgcn_alignbyte(e1, e0, sh);
+          v.y = __builtin_amdgcn_alignbyte(e2, e1, sh);
+          v.z = __builtin_amdgcn_alignbyte(e3, e2, sh);
+          v.w = __builtin_amdgcn_alignbyte(e4, e3, sh);
+          *reinterpret_cast<uint4 *>(gbase + lo16) = v;
         } else {
-          int b0 = max(lo16, pad), b1 = min(hi16, tb);
-          for (int b = b0; b < b1; ++b) gbase[b] = stage[b];
+          const int bb0 = max(lo16, pad), bb1 = min(hi16, tb);
+          for (int b = bb0; b < bb1; ++b) gbase[b] = stage[b - pad];
         }
       }
     }
-#undef KW
-#undef BIT
-#undef MSK
-#undef VALID
-#undef EREL
-#undef NBYTES
+    PH(7)
+#undef SMASK
+#undef DMASK
   }
+  PH_FLUSH(0)
 }
 
 // ------------------------------------------------------------ decoder
-__device__ __forceinline__ void bm_set(uint32_t (&bm)[5], int idx) {
+// Wave-per-piece decoder.  Each wave owns one piece at a time and consumes
+// its packed bytes in windows of 2 KiB starting at a known tag position e:
+//   1. lane l walks its 32-byte chunk [e + 32l, e + 32l + 32) from the
+//      chunk start, speculatively treating it as a tag; visited positions
+//      form a 32-bit mask per lane;
+//   2. from its exit, each lane walks on until it lands on a position some
+//      lane visited (the two walks coincide from there: the tag chain is a
+//      function of the position);
+//   3. starting from lane 0 (whose chunk starts at the true tag e) the lane
+//      chain lane -> owner of its landing point gives every true record;
+//   4. on-path lanes re-walk their true records, count output words (wave
+//      scan), check the reference's error conditions, and write, for every
+//      8-word output block, the record covering it; all 64 lanes then
+//      gather-expand the blocks (PackedInputStream.java:82-134 per word).
+// No barriers: 32 pieces in flight per CU hide every LDS / HBM latency.
+constexpr int kDecThreads = 256;               // 4 independent waves
+constexpr uint32_t kWin = 2048;                // packed bytes resolved per window
+constexpr uint32_t kWinBuf = 2112;             // + pad (<= 15) + 64 read slack
+constexpr int kRound = 2048;                   // output words expanded per round
+constexpr uint32_t kDecWaveLds = kWinBuf + 4 * (kRound / 8) + 256;  // 3392
+constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;                // 15,616
+
+__device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
-  for (int q = 0; q < 5; ++q)
-    if ((idx >> 5) == q) bm[q] |= 1u << (idx & 31);
+  for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
+  return v;
 }
-__device__ __forceinline__ bool bm_test(const uint32_t (&bm)[5], int idx) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int q = 0; q < 5; ++q)
-    if ((idx >> 5) == q) r = bm[q];
-  return (r >> (idx & 31)) & 1;
+__device__ __forceinline__ void wave_lds_sync() {
+  // DS ops of one wave complete in order; this only stops the compiler
+  // moving LDS accesses across the point and drains this lane's queue.
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
 }
 
-// record length in bytes of the record whose tag is at pk[q]
-__device__ __forceinline__ uint32_t rec_len(const uint8_t *pk, uint32_t q) {
-  uint32_t tag = pk[q];
+// record length in bytes of the record whose tag is at piece position q
+__device__ __forceinline__ uint32_t rec_len(const uint8_t *pkw, uint32_t q) {
+  const uint32_t tag = pkw[q];
   if (tag == 0) return 2;
-  if (tag == 0xffu) return 10 + 8u * pk[q + 9];
+  if (tag == 0xffu) return 10 + 8u * pkw[q + 9];
   return 1 + __builtin_popcount(tag);
 }
 
-// speculative walk from `start`; marks record starts in [cbeg, cend)
-__device__ __forceinline__ uint32_t walk(const uint8_t *pk, uint32_t start, uint32_t cbeg,
-                                         uint32_t cend, uint32_t (&bm)[5]) {
-#pragma unroll
-  for (int q = 0; q < 5; ++q) bm[q] = 0;
-  uint32_t pos = start;
-  while (pos < cend) {
-    if (pos >= cbeg) bm_set(bm, (int)(pos - cbeg));
-    pos += rec_len(pk, pos);
+// 8 bytes at piece position x: from the LDS window when loaded, otherwise
+// (tail of a literal run reaching past the window) straight from memory
+__device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32_t lend,
+                                         const uint8_t *gpiece) {
+  uint32_t d0, d1, d2, sh;
+  if (x + 12 <= lend) {
+    // piece-relative dword grid (the LDS copy may sit at any byte phase)
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(pkw + (x & ~3u));
+    sh = x & 3;
+    d0 = p[0];
+    d1 = p[1];
+    d2 = p[2];
+  } else {
+    // address-aligned dwords of the packed buffer
+    const uintptr_t g = reinterpret_cast<uintptr_t>(gpiece + x);
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(g & ~(uintptr_t)3);
+    sh = (uint32_t)(g & 3);
+    d0 = p[0];
+    d1 = p[1];
+    d2 = sh ? p[2] : 0u;
   }
-  return pos;
-}
-
-// unaligned 8-byte read from LDS
-__device__ __forceinline__ uint64_t lds_read8(const uint8_t *base, uint32_t p) {
-  const uint32_t *a = reinterpret_cast<const uint32_t *>(base + (p & ~3u));
-  uint32_t d0 = a[0], d1 = a[1], d2 = a[2];
-  uint32_t sh = p & 3;
-  uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
-  uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-__global__ __launch_bounds__(kThreads, 4) void decode_kernel(
+__global__ __launch_bounds__(kDecThreads) void decode_kernel(
     const uint8_t *__restrict__ packed, const uint64_t *__restrict__ in_off,
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
     int32_t *__restrict__ status, uint32_t *ticket) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kDecLut);
-  uint16_t *J0 = reinterpret_cast<uint16_t *>(smem + kDecReg);          // [520]
-  uint16_t *J1 = reinterpret_cast<uint16_t *>(smem + kDecReg + 1040);   // [520]
-  uint8_t *onp = smem + kDecReg + 2080;                                 // [520]
-  uint32_t *E = reinterpret_cast<uint32_t *>(smem + kDecReg + 2608);    // [520]
-  uint32_t *blk = reinterpret_cast<uint32_t *>(smem + kDecReg);         // [1024]
-  int *scr = reinterpret_cast<int *>(smem + kDecScr);
-  uint8_t *pkr = smem + kDecPk;
-
-  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  uint64_t *lut = reinterpret_cast<uint64_t *>(smem);
+  const int lane = lane_id(), w = wave_id();
+  uint8_t *wl = smem + 2048 + w * kDecWaveLds;
+  uint8_t *wbuf = wl;                                            // window bytes
+  uint32_t *blk = reinterpret_cast<uint32_t *>(wl + kWinBuf);    // [256]
+  uint32_t *visa = blk + kRound / 8;                             // [64]
   fill_luts(lut, true);
+  __syncthreads();  // the only block-wide barrier: LUT ready
 
-  for (uint32_t it = 0;; ++it) {
-    // ticket slot alternates: a wave still reading this piece's slot can
-    // never see the next piece's ticket (one barrier per iteration)
-    if (tid == 0) scr[64 + (it & 1)] = (int)atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t seg = (uint32_t)scr[64 + (it & 1)];
+  for (;;) {
+    // every branch below is on wave-uniform (SGPR) values: the compiler
+    // must not turn the piece / window loops into divergent loops
+    // All 64 lanes add 1 (hipcc folds it into one +64 atomic): no lane-0-only
+    // branch at the loop head, which hipcc otherwise structurised into a
+    // divergent loop re-running piece 0.  Tickets count in units of 64.
+    const uint32_t tk = atomicAdd(ticket, 1u);
+    const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)tk, 0) >> 6;
     if (seg >= n) break;
     const uint64_t w0 = swo[seg];
     const int W = (int)(swo[seg + 1] - w0);
     const uint64_t a = in_off[seg];
     const uint32_t P = (uint32_t)(in_off[seg + 1] - a);
-    if (W == 0 || P == 0 || W > kTileWords || P > kDecPkCap) {
-      if (tid == 0) {
-        int st;
-        if (W == 0) st = P == 0 ? CPK_OK : CPK_ETRAILING;      // read() of 0 bytes
-        else if (P == 0) st = CPK_ETRUNC;
-        else st = CPK_EUNSUPPORTED;
-        status[seg] = st;
+    const uint8_t *gp = packed + a;
+    uint64_t *dst = out + w0;
+    int st = CPK_OK;
+    uint32_t e = 0;  // true tag position (piece-relative)
+    int ow = 0;      // output words produced
+    if (W == 0) st = P == 0 ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
+    while (W != 0) {
+      if (e >= P) {
+        if (ow < W) st = CPK_ETRUNC;  // ArrayInputStream EOF -> DecodeException
+        break;
       }
-      continue;
-    }
-    // ---- stage packed bytes: LDS byte x <-> global (a & ~15) + x ---------
-    const uint32_t pad = (uint32_t)(a & 15);
-    {
-      const uint8_t *g = packed + (a - pad);
-      const uint32_t nl = (pad + P + 15) >> 4;
-      for (uint32_t c = tid; c < nl; c += kThreads)
-        *reinterpret_cast<uint4 *>(pkr + 16 * c) = *reinterpret_cast<const uint4 *>(g + 16 * c);
-      if (tid == 0) {  // zero slack after the piece (walks peek up to +9)
-        uint32_t z = pad + P;
-        for (uint32_t b = z; b < ((z + 15) & ~15u) + 16; ++b) pkr[b] = 0;
-      }
-    }
-    __syncthreads();
-    const uint8_t *pk = pkr + pad;
+      if (ow >= W) break;  // (trailing input is flagged by the record check)
+      const uint32_t wend = min(e + kWin, P);
+      // ---- window load: LDS byte x <-> packed[(a + e) & ~15 + x] ----------
+      const uint32_t padw = (uint32_t)((a + e) & 15);
+      const uint32_t ebase = e - padw;  // piece position of wbuf[0]
+      const uint32_t need = min(e + kWin + 32, P) - ebase;  // <= 2095 bytes
+      const uint32_t lines = (need + 15) >> 4;
+      const uint4 *gsrc = reinterpret_cast<const uint4 *>(gp - padw + e);
+      for (uint32_t L = lane; L < lines; L += 64)
+        reinterpret_cast<uint4 *>(wbuf)[L] = gsrc[L];
+      const uint32_t lend = ebase + 16 * lines;  // loaded piece positions < lend
+      // pkw[q] = packed byte q (signed 64-bit offset: ebase is negative when
+      // the piece starts mid-line)
+      const uint8_t *pkw = wbuf + (int64_t)padw - (int64_t)e;
+      wave_lds_sync();
 
-    // ---- tag chain: speculative chunk walks + validation ------------------
-    uint32_t C = (P + kMaxChunks - 1) / kMaxChunks;
-    C = C < 16 ? 16 : (C + 7) & ~7u;
-    const int nch = (int)((P + C - 1) / C);
-    const int c = tid;
-    const bool active = c < nch;
-    const uint32_t cbeg = c * C;
-    const uint32_t cend = min(cbeg + C, P);
-    uint32_t bm[5] = {0, 0, 0, 0, 0};
-    uint32_t X = 0;
-    if (active) {
-      uint32_t st = c == 0 ? 0 : (cbeg > kWarm ? cbeg - kWarm : 0);
-      X = walk(pk, st, cbeg, cend, bm);
-    }
-    int rounds = 0;
-    while ((1 << rounds) < nch + 1) ++rounds;
-    bool onpath = false;
-    for (int iter = 0;; ++iter) {
-      const int t = active ? (X >= P ? nch : (int)(X / C)) : nch;
-      if (active) {
-        J0[c] = (uint16_t)t;
-        onp[c] = c == 0;
-      }
-      if (tid == 0) {
-        J0[nch] = (uint16_t)nch;
-        J1[nch] = (uint16_t)nch;
-        onp[nch] = 0;
-        E[0] = 0;
-      }
-      __syncthreads();
-      uint16_t *Jc = J0, *Jn = J1;
-      for (int r = 0; r < rounds; ++r) {
-        if (active) {
-          int j = Jc[c];
-          if (onp[c]) onp[j] = 1;
-          Jn[c] = Jc[j];
+      // ---- 1: speculative chunk walks --------------------------------------
+      const uint32_t cb = e + 32 * lane;
+      const uint32_t ce = min(cb + 32, wend);
+      uint32_t vis = 0, X = cb;
+      if (cb < wend) {
+        uint32_t pos = cb;
+        while (pos < ce) {
+          vis |= 1u << (pos - cb);
+          pos += rec_len(pkw, pos);
         }
-        __syncthreads();
-        uint16_t *tmp = Jc;
-        Jc = Jn;
-        Jn = tmp;
+        X = pos;
       }
-      onpath = active && onp[c];
-      if (onpath && t < nch) E[t] = X;
-      __syncthreads();
-      bool bad = false;
-      if (onpath && c > 0) {
-        uint32_t e = E[c];
-        if (!bm_test(bm, (int)(e - cbeg))) {
-          bad = true;
-          X = walk(pk, e, cbeg, cend, bm);
+      visa[lane] = vis;
+      wave_lds_sync();
+      // ---- 2: walk on until landing on a visited position -------------------
+      uint32_t S = X;
+      if (cb < wend) {
+        while (S < wend) {
+          const uint32_t r = S - e;
+          if ((visa[r >> 5] >> (r & 31)) & 1) break;
+          S += rec_len(pkw, S);
         }
       }
-      if (!__syncthreads_or(bad)) break;
-      if (iter > 2 * kMaxChunks + 8) break;  // unreachable: converges in <= nch
-    }
-    // keep only the true records: bits at or after the chunk's entry
-    if (!onpath) {
-#pragma unroll
-      for (int q = 0; q < 5; ++q) bm[q] = 0;
-    } else if (c > 0) {
-      int e = (int)(E[c] - cbeg);
-#pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        int lo = q * 32;
-        if (e >= lo + 32) bm[q] = 0;
-        else if (e > lo) bm[q] &= ~0u << (e - lo);
+      // ---- 3: true chain over lanes (scalar) --------------------------------
+      uint64_t onmask = 0;
+      uint32_t entry = e;
+      uint32_t enext;
+      {
+        int cur = 0;
+        for (;;) {
+          onmask |= 1ull << cur;
+          const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)S, cur);
+          if (s >= wend) {
+            enext = s;
+            break;
+          }
+          const int nx = (int)((s - e) >> 5);
+          if (lane == nx) entry = s;
+          cur = nx;
+        }
       }
-    }
-    __syncthreads();  // E/J region is reused as blk below
-
-    // ---- output word offsets of the records --------------------------------
-    int myw = 0;
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      uint32_t m = bm[q];
-      while (m) {
-        uint32_t qq = cbeg + 32 * q + __builtin_ctz(m);
-        m &= m - 1;
-        uint32_t tag = pk[qq];
-        myw += (tag == 0) ? 1 + pk[qq + 1] : (tag == 0xffu) ? 1 + pk[qq + 9] : 1;
-      }
-    }
-    int inc = wave_incl_add(myw);
-    if (lane == 63) scr[w] = inc;
-    if (tid == 0) scr[80] = 0x7fffffff;
-    __syncthreads();
-    int wb = 0, totw = 0;
-    for (int q = 0; q < kWaves; ++q) {
-      int tq = scr[q];
-      if (q < w) wb += tq;
-      totw += tq;
-    }
-    int o = wb + inc - myw;
-    // first error in stream order (PackedInputStream.java:53-138 semantics)
-    {
-      int err = 0x7fffffff;
-      int oo = o;
-#pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        uint32_t m = bm[q];
-        while (m && err == 0x7fffffff) {
-          uint32_t qq = cbeg + 32 * q + __builtin_ctz(m);
-          m &= m - 1;
-          if (oo >= W) break;
-          uint32_t tag = pk[qq];
-          int code = 0;
-          uint32_t need = 1 + __builtin_popcount(tag);
-          int nw = 1;
-          uint32_t adv = need;
-          if (qq + need > P) code = 2;                     // ETRUNC
-          else if (tag == 0) {
-            if (qq + 2 > P) code = 2;
-            else {
-              nw = 1 + pk[qq + 1];
-              adv = 2;
-              if (oo + nw > W) code = 3;                   // EOVERRUN
-            }
+      const bool on = (onmask >> lane) & 1;
+      // ---- 4: output words of each lane's true records ----------------------
+      int myw = 0;
+      if (on) {
+        for (uint32_t q = entry; q < S;) {
+          const uint32_t tag = pkw[q];
+          if (tag == 0) {
+            myw += 1 + pkw[q + 1];
+            q += 2;
           } else if (tag == 0xffu) {
-            if (qq + 10 > P) code = 2;
-            else {
-              uint32_t rn = pk[qq + 9];
+            const uint32_t rn = pkw[q + 9];
+            myw += 1 + (int)rn;
+            q += 10 + 8 * rn;
+          } else {
+            myw += 1;
+            q += 1 + __builtin_popcount(tag);
+          }
+        }
+      }
+      const int inc = wave_incl_add(myw);
+      const int T = readlane(inc, 63);
+      const int o0 = inc - myw;  // window-relative output of this lane's first record
+      // ---- 5: error checks, block map, expansion (rounds of 2048 words) -----
+      bool failed = false;
+      for (int rb = 0; rb < T; rb += kRound) {
+        int err = 0x7fffffff;
+        if (on) {
+          int o = o0;
+          for (uint32_t q = entry; q < S;) {
+            const uint32_t tag = pkw[q];
+            const uint32_t ntag = 1 + __builtin_popcount(tag);
+            int nw = 1;
+            uint32_t adv = ntag;
+            if (tag == 0) {
+              nw = 1 + pkw[q + 1];
+              adv = 2;
+            } else if (tag == 0xffu) {
+              nw = 1 + pkw[q + 9];
+              adv = 10 + 8 * (uint32_t)(nw - 1);
+            }
+            const int oo = ow + o;
+            if (rb == 0 && oo < W && err == 0x7fffffff) {
+              // PackedInputStream.java:53-138: truncated tag bytes / count /
+              // literal run -> EOF DecodeException; run past the piece ->
+              // DecodeException / BufferOverflowException
+              int code = 0;
+              if (q + ntag > P) code = 2;
+              else if (tag == 0 || tag == 0xffu) {
+                if (q + (tag ? 10u : 2u) > P) code = 2;
+                else if (oo + nw > W) code = 3;
+                else if (q + adv > P) code = 2;
+              }
+              if (!code && oo + nw == W && q + adv < P) code = 4;
+              if (code) err = (int)((q << 3) | (uint32_t)code);
+            }
+            // blocks of this round whose first word this record covers
+            const int lo = max(o, rb), hi = min(o + nw, rb + kRound);
+            for (int bb = (lo + 7) & ~7; bb < hi; bb += 8)
+              blk[(bb - rb) >> 3] = q | ((uint32_t)(bb - o) << 17);
+            o += nw;
+            q += adv;
+          }
+        }
+        if (rb == 0) {
+          err = __builtin_amdgcn_readfirstlane(wave_min(err));
+          if (err != 0x7fffffff) {
+            st = -(err & 7);
+            failed = true;
+            break;
+          }
+        }
+        wave_lds_sync();
+        const int nb = (min(kRound, T - rb) + 7) >> 3;
+        for (int b = lane; b < nb; b += 64) {
+          const uint32_t v = blk[b];
+          uint32_t q = v & 0x1ffffu;
+          int ofs = (int)(v >> 17);
+          const int wbase = ow + rb + 8 * b;  // piece word of the block's first word
+          uint64_t words[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const uint32_t tag = pkw[q];
+            uint64_t x;
+            int nw;
+            uint32_t adv;
+            if (tag == 0) {
+              x = 0;
+              nw = 1 + pkw[q + 1];
+              adv = 2;
+            } else if (tag == 0xffu) {
+              const uint32_t rn = pkw[q + 9];
               nw = 1 + (int)rn;
               adv = 10 + 8 * rn;
-              if (oo + nw > W) code = 3;
-              else if (qq + adv > P) code = 2;
+              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp);
+            } else {
+              const uint64_t raw = read8(pkw, q + 1, lend, gp);
+              const uint64_t sel = lut[tag];
+              const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
+              const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
+              const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
+              x = (uint64_t)x0 | ((uint64_t)x1 << 32);
+              nw = 1;
+              adv = 1 + __builtin_popcount(tag);
+            }
+            words[i] = x;
+            // past the window's last word: stay put (never stored)
+            if (++ofs == nw && wbase + i + 1 < ow + T) {
+              q += adv;
+              ofs = 0;
             }
           }
-          if (!code && oo + nw == W && qq + adv < P) code = 4;  // ETRAILING
-          if (code) err = (int)((qq << 3) | code);
-          oo += nw;
-        }
-      }
-      if (totw < W && err == 0x7fffffff && c == 0) err = (int)((P << 3) | 2);
-      if (err != 0x7fffffff) atomicMin(&scr[80], err);
-    }
-    __syncthreads();
-    const int err = scr[80];
-    if (err != 0x7fffffff) {
-      if (tid == 0) status[seg] = -(err & 7);
-      continue;
-    }
-    if (totw != W) {  // cannot happen once the checks above pass
-      if (tid == 0) status[seg] = CPK_ETRUNC;
-      continue;
-    }
-    // ---- block starts: for every 8-word output block, covering record -----
-    {
-      int oo = o;
+          const int kw = min(8, ow + T - wbase);
+          uint64_t *d = dst + wbase;
+          if (kw == 8 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
 #pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        uint32_t m = bm[q];
-        while (m) {
-          uint32_t qq = cbeg + 32 * q + __builtin_ctz(m);
-          m &= m - 1;
-          uint32_t tag = pk[qq];
-          int nw = (tag == 0) ? 1 + pk[qq + 1] : (tag == 0xffu) ? 1 + pk[qq + 9] : 1;
-          for (int bb = (oo + 7) >> 3; bb * 8 < oo + nw; ++bb)
-            blk[bb] = qq | ((uint32_t)(bb * 8 - oo) << 17);
-          oo += nw;
-        }
-      }
-    }
-    __syncthreads();
-    // ---- gather-expand ------------------------------------------------------
-    const int nblk = (W + 7) >> 3;
-    uint64_t *dst = out + w0;
-    for (int b = tid; b < nblk; b += kThreads) {
-      uint32_t v = blk[b];
-      uint32_t q = v & 0x1ffffu;
-      int ofs = (int)(v >> 17);
-      uint64_t words[8];
+            for (int i = 0; i < 8; i += 2) {
+              uint4 v4;
+              v4.x = (uint32_t)words[i];
+              v4.y = (uint32_t)(words[i] >> 32);
+              v4.z = (uint32_t)words[i + 1];
+              v4.w = (uint32_t)(words[i + 1] >> 32);
+              *reinterpret_cast<uint4 *>(d + i) = v4;
+            }
+          } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        uint32_t tag = pk[q];
-        uint64_t x;
-        int nw;
-        uint32_t adv;
-        if (tag == 0) {
-          x = 0;
-          nw = 1 + pk[q + 1];
-          adv = 2;
-        } else if (tag == 0xffu) {
-          uint32_t rn = pk[q + 9];
-          nw = 1 + (int)rn;
-          adv = 10 + 8 * rn;
-          x = lds_read8(pk, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1));
-        } else {
-          uint64_t raw = lds_read8(pk, q + 1);
-          uint64_t sel = lut[tag];
-          uint32_t lo = (uint32_t)raw, hi = (uint32_t)(raw >> 32);
-          uint32_t e0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
-          uint32_t e1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
-          x = (uint64_t)e0 | ((uint64_t)e1 << 32);
-          nw = 1;
-          adv = 1 + __builtin_popcount(tag);
+            for (int i = 0; i < 8; ++i)
+              if (i < kw) d[i] = words[i];
+          }
         }
-        words[i] = x;
-        // past the end of the piece: stay on the last record (never stored)
-        if (++ofs == nw && b * 8 + i + 1 < W) {
-          q += adv;
-          ofs = 0;
-        }
+        wave_lds_sync();  // blk reused by the next round
       }
-      const int kw = min(8, W - b * 8);
-      uint64_t *d = dst + (uint64_t)b * 8;
-      if (kw == 8 && (((uintptr_t)d) & 15) == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; i += 2) {
-          uint4 v4;
-          v4.x = (uint32_t)words[i];
-          v4.y = (uint32_t)(words[i] >> 32);
-          v4.z = (uint32_t)words[i + 1];
-          v4.w = (uint32_t)(words[i + 1] >> 32);
-          *reinterpret_cast<uint4 *>(d + i) = v4;
-        }
-      } else {
-        for (int i = 0; i < kw; ++i) d[i] = words[i];
-      }
+      if (failed) break;
+      ow += T;
+      e = enext;
     }
-    if (tid == 0) status[seg] = CPK_OK;
+    status[seg] = st;  // every lane the same value: no lane-dependent branch
   }
 }
 
@@ -1074,6 +1038,15 @@ extern "C" {
 
 int cpk_abi_version(void) { return CPK_ABI_VERSION; }
 
+#ifdef CPK_PHASE_STATS
+// diagnostic builds only: read and clear the per-phase cycle sums
+int cpk_debug_phase_stats(unsigned long long *host64) {
+  if (hipMemcpyFromSymbol(host64, HIP_SYMBOL(cpk::g_phase), 64 * 8) != hipSuccess) return CPK_EDEVICE;
+  unsigned long long z[64] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(cpk::g_phase), z, sizeof z) == hipSuccess ? CPK_OK : CPK_EDEVICE;
+}
+#endif
+
 const char *cpk_status_string(int s) {
   switch (s) {
     case CPK_OK: return "ok";
@@ -1148,7 +1121,7 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   if (hipMemsetAsync(ctx->tickets, 0, 16, s) != hipSuccess) return CPK_EDEVICE;
   unsigned grid = (unsigned)(2 * ctx->cus);
   if (grid > n) grid = n;
-  hipLaunchKernelGGL(cpk::encode_kernel<false>, dim3(grid), dim3(cpk::kThreads), cpk::kEncLds, s,
+  hipLaunchKernelGGL(cpk::encode_kernel<false>, dim3(grid), dim3(cpk::kEncThreads), cpk::kEncLds, s,
                      (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
                      ctx->tickets);
   return hip_ok(hipGetLastError());
@@ -1163,9 +1136,10 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(ctx->tickets + 1, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
-  unsigned grid = (unsigned)(2 * ctx->cus);
-  if (grid > n) grid = n;
-  hipLaunchKernelGGL(cpk::decode_kernel, dim3(grid), dim3(cpk::kThreads), cpk::kDecLds, s,
+  // persistent: 8 blocks of 4 independent waves per CU (32 pieces in flight)
+  unsigned grid = (unsigned)(8 * ctx->cus);
+  if (grid > (n + 3) / 4) grid = (n + 3) / 4;
+  hipLaunchKernelGGL(cpk::decode_kernel, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
                      (const uint8_t *)d_packed, d_in_off, d_swo, n, (uint64_t *)d_out, d_status,
                      ctx->tickets + 1);
   return hip_ok(hipGetLastError());

@@ -1,0 +1,45 @@
+"""Per-phase cycle shares of the codec kernels (diagnostic stats build).
+Usage: python tools/phase_stats.py [config] [segments]"""
+import ctypes, sys
+from pathlib import Path
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO / "capnproto-java_amd")]
+import numpy as np, torch
+import capnp_packed as cp
+
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+L = cp.load(REPO / "capnproto-java_amd" / "lib" / "libcapnp_packed_hip_stats.so")
+L.cpk_debug_phase_stats.argtypes = [ctypes.c_void_p]
+ctx = cp.Context(0)
+swo = np.arange(0, (n + 1) * 8192, 8192, dtype=np.uint64)
+d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
+d_in = torch.empty(n * 8192, dtype=torch.int64, device="cuda")
+ctx.generate(cp.preset(cfg), d_swo, d_in)
+cap = cp.batch_capacity(swo)
+d_pk = torch.empty((cap + 255) // 256 * 256, dtype=torch.uint8, device="cuda")
+d_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+d_out = torch.empty_like(d_in)
+d_st = torch.empty(n, dtype=torch.int32, device="cuda")
+for _ in range(2):
+    ctx.encode_batch(d_in, d_swo, 8192, d_pk, d_off)
+    ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
+torch.cuda.synchronize()
+buf = np.zeros(64, dtype=np.uint64)
+L.cpk_debug_phase_stats(buf.ctypes.data)
+ctx.encode_batch(d_in, d_swo, 8192, d_pk, d_off)
+ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
+torch.cuda.synchronize()
+L.cpk_debug_phase_stats(buf.ctypes.data)
+enames = ["ticket", "load+classify", "roles", "long chains", "offsets+zero",
+          "strings->LDS", "look-back", "store"]
+dnames = ["ticket", "stage packed", "first walk", "resolve loop", "clear bits",
+          "offsets+errors", "blk map", "expand+store"]
+for title, base, names in (("encode", 0, enames), ("decode", 16, dnames)):
+    v = buf[base:base + len(names)].astype(float)
+    tot = v.sum()
+    print(f"{title}: total {tot / 1e6:.1f} Mcycles over all WGs; per piece {tot / n:.0f} cyc")
+    for nm, x in zip(names, v):
+        print(f"   {nm:22s} {100 * x / tot:6.2f} %   {x / n:8.0f} cyc/piece")
+print("decode resolve iterations per piece:", buf[16 + 9] / n)
+print("P/U =", int(d_off[-1].item()) / (8.0 * n * 8192), "bad status", int((d_st != 0).sum().item()))
