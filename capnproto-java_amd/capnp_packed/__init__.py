@@ -28,8 +28,8 @@ TILE_WORDS = 8192  # largest piece this build encodes/decodes
 EXPORTS = [
     "cpk_abi_version", "cpk_status_string", "cpk_packed_bound", "cpk_batch_packed_capacity",
     "cpk_ctx_create", "cpk_ctx_destroy", "cpk_ctx_device", "cpk_encode_batch",
-    "cpk_decode_batch", "cpk_encode_host", "cpk_decode_host", "cpk_generate",
-    "cpk_count_mismatch",
+    "cpk_decode_batch", "cpk_decode_stream", "cpk_encode_host", "cpk_decode_host",
+    "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch",
 ]
 
 
@@ -75,6 +75,8 @@ def load(path: Path | None = None) -> ctypes.CDLL:
         "cpk_decode_batch": ([vp, vp, vp, vp, u32, vp, vp, vp], i32),
         "cpk_encode_host": ([vp, vp, vp, u32, vp, u64, vp], i32),
         "cpk_decode_host": ([vp, vp, vp, vp, u32, vp, vp], i32),
+        "cpk_decode_stream": ([vp, vp, u64, vp, u32, vp, vp, vp, vp], i32),
+        "cpk_decode_stream_host": ([vp, vp, u64, vp, u32, vp, vp, vp], i32),
         "cpk_generate": ([vp, ctypes.POINTER(GenParams), vp, u32, vp, vp], i32),
         "cpk_count_mismatch": ([vp, vp, vp, u64, vp, vp], i32),
     }
@@ -188,6 +190,26 @@ class Context:
         if rc not in (OK, ETRUNC, EOVERRUN, ETRAILING, EUNSUPPORTED, EINVAL):
             _check(rc, "cpk_decode_host")
         return out[: int(8 * swo[-1])], st[:n]
+
+
+def _decode_stream_host(self, packed: np.ndarray, seg_word_off: np.ndarray):
+    """PackedInputStream.read per piece, back to back over one stream.
+    -> (decoded uint8 array, piece boundaries uint64[n+1], status int32[n])."""
+    swo = np.ascontiguousarray(seg_word_off, dtype=np.uint64)
+    n = len(swo) - 1
+    pk = np.ascontiguousarray(packed, dtype=np.uint8)
+    out = np.zeros(int(8 * swo[-1]) + 8, dtype=np.uint8)
+    io = np.zeros(n + 1, dtype=np.uint64)
+    st = np.zeros(max(n, 1), dtype=np.int32)
+    rc = self._lib.cpk_decode_stream_host(self.handle, pk.ctypes.data if pk.size else None,
+                                          pk.size, swo.ctypes.data, n, out.ctypes.data,
+                                          io.ctypes.data, st.ctypes.data)
+    if rc not in (OK, ETRUNC, EOVERRUN, ETRAILING, EUNSUPPORTED, EINVAL):
+        _check(rc, "cpk_decode_stream_host")
+    return out[: int(8 * swo[-1])], io, st[:n]
+
+
+Context.decode_stream_host = _decode_stream_host
 
 
 def gen_params(cfg: int, z: float, lz: float, q: float) -> GenParams:

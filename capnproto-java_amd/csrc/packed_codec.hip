@@ -312,19 +312,19 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
     asm volatile("" : "+v"(k0));
 
     // ---- pass 1: load, classify, run-start and D masks --------------------
-    uint32_t lo[kSteps], hi[kSteps], info[kSteps];
+    uint32_t info[kSteps];
     // run-start / D ballots of each step live in LDS (wave-private rows):
     // kept in SGPRs they spilled.
     uint64_t *mrow = mks + (wb >> 9) * (2 * kSteps);
 #define SMASK(s) mrow[2 * (s)]
 #define DMASK(s) mrow[2 * (s) + 1]
     const uint64_t *src = in + w0;
+    // all 8 loads in flight at once (clamped, not predicated: no branches)
+    uint64_t wv[kSteps];
+    {
+      const int kl = max(W - 1, 0);
 #pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-      const int k = k0 + s * 64;
-      uint64_t v = k < W ? src[k] : 0ull;
-      lo[s] = (uint32_t)v;
-      hi[s] = (uint32_t)(v >> 32);
+      for (int s = 0; s < kSteps; ++s) wv[s] = W ? src[min(k0 + s * 64, kl)] : 0ull;
     }
     int gprev = 3;  // group of word wb - 1
     if (w > 0 && lane == 0 && wb - 1 < W) {
@@ -335,7 +335,8 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
 #pragma unroll
     for (int s = 0; s < kSteps; ++s) {
       const int k = k0 + s * 64;
-      const uint32_t m = word_mask(lo[s], hi[s]);
+      const uint64_t v = k < W ? wv[s] : 0ull;
+      const uint32_t m = word_mask((uint32_t)v, (uint32_t)(v >> 32));
       const int g = k < W ? grp_of(m) : 3;
       const int gp = wave_shr1(g, gprev);
       const uint64_t sb = __ballot(g != 3 && (k == 0 || g != gp));
@@ -546,7 +547,10 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
       const int o = wbytes + mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2) + 8 * mbcnt(b3);
       wbytes += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) + 8 * __popcll(b3);
       if (nb == 0) continue;
-      const uint32_t l = lo[s], h = hi[s], m = x & 0xffu;
+      // the words are re-read here (L2 / Infinity-Cache hit) instead of being
+      // held in 16 VGPRs across the passes: 2 workgroups per CU instead of 1
+      const uint64_t v = src[k0 + s * 64];
+      const uint32_t l = (uint32_t)v, h = (uint32_t)(v >> 32), m = x & 0xffu;
       uint32_t d0, d1, d2;
       if (x & (1u << 10)) {  // literal-run member: 8 bytes verbatim
         d0 = l;
@@ -652,6 +656,11 @@ constexpr int kRound = 2048;                   // output words expanded per roun
 constexpr uint32_t kDecWaveLds = kWinBuf + 4 * (kRound / 8) + 256;  // 3392
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;                // 15,616
 
+__device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
+  return v;
+}
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
@@ -698,10 +707,18 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
+// kStream = false: piece i's packed bytes are [in_off[i], in_off[i+1]) and a
+//   piece that fills before its range ends is CPK_ETRAILING.
+// kStream = true: one wave decodes pieces 0..n-1 back to back from one
+//   packed stream of `avail` bytes; each read() fills its piece and leaves
+//   the rest of the stream to the next (PackedInputStream.java:35-140 as
+//   Serialize.read calls it, Serialize.java:165-175); in_off[0..n] is
+//   written with the piece boundaries found.
+template <bool kStream>
 __global__ __launch_bounds__(kDecThreads) void decode_kernel(
-    const uint8_t *__restrict__ packed, const uint64_t *__restrict__ in_off,
+    const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
-    int32_t *__restrict__ status, uint32_t *ticket) {
+    int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem);
   const int lane = lane_id(), w = wave_id();
@@ -711,26 +728,39 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
   uint32_t *visa = blk + kRound / 8;                             // [64]
   fill_luts(lut, true);
   __syncthreads();  // the only block-wide barrier: LUT ready
+  if (kStream && (blockIdx.x != 0 || w != 0)) return;
+  uint64_t scur = 0;      // stream mode: start of the next piece
+  int sfail = CPK_OK;     // stream mode: a failed piece stops the stream
 
-  for (;;) {
+  for (uint32_t sidx = 0;; ++sidx) {
     // every branch below is on wave-uniform (SGPR) values: the compiler
     // must not turn the piece / window loops into divergent loops
     // All 64 lanes add 1 (hipcc folds it into one +64 atomic): no lane-0-only
     // branch at the loop head, which hipcc otherwise structurised into a
     // divergent loop re-running piece 0.  Tickets count in units of 64.
-    const uint32_t tk = atomicAdd(ticket, 1u);
-    const uint32_t seg = (uint32_t)__builtin_amdgcn_readlane((int)tk, 0) >> 6;
+    uint32_t seg;
+    if (kStream) {
+      seg = sidx;
+    } else {
+      const uint32_t tk = atomicAdd(ticket, 1u);
+      seg = (uint32_t)__builtin_amdgcn_readlane((int)tk, 0) >> 6;
+    }
     if (seg >= n) break;
     const uint64_t w0 = swo[seg];
     const int W = (int)(swo[seg + 1] - w0);
-    const uint64_t a = in_off[seg];
-    const uint32_t P = (uint32_t)(in_off[seg + 1] - a);
+    const uint64_t a = kStream ? scur : in_off[seg];
+    const uint32_t P = kStream ? (uint32_t)min(avail - scur, (uint64_t)0xffffffffu)
+                               : (uint32_t)(in_off[seg + 1] - a);
+    if (kStream && sfail != CPK_OK) {
+      status[seg] = sfail;
+      continue;
+    }
     const uint8_t *gp = packed + a;
     uint64_t *dst = out + w0;
     int st = CPK_OK;
     uint32_t e = 0;  // true tag position (piece-relative)
     int ow = 0;      // output words produced
-    if (W == 0) st = P == 0 ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
+    if (W == 0) st = (P == 0 || kStream) ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
     while (W != 0) {
       if (e >= P) {
         if (ow < W) st = CPK_ETRUNC;  // ArrayInputStream EOF -> DecodeException
@@ -817,6 +847,7 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
       const int o0 = inc - myw;  // window-relative output of this lane's first record
       // ---- 5: error checks, block map, expansion (rounds of 2048 words) -----
       bool failed = false;
+      uint32_t fin = 0;  // end of the record that fills the piece (if any)
       for (int rb = 0; rb < T; rb += kRound) {
         int err = 0x7fffffff;
         if (on) {
@@ -845,8 +876,9 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
                 else if (oo + nw > W) code = 3;
                 else if (q + adv > P) code = 2;
               }
-              if (!code && oo + nw == W && q + adv < P) code = 4;
+              if (!kStream && !code && oo + nw == W && q + adv < P) code = 4;
               if (code) err = (int)((q << 3) | (uint32_t)code);
+              if (oo + nw == W) fin = q + adv;
             }
             // blocks of this round whose first word this record covers
             const int lo = max(o, rb), hi = min(o + nw, rb + kRound);
@@ -863,9 +895,10 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
             failed = true;
             break;
           }
+          fin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u(fin));
         }
         wave_lds_sync();
-        const int nb = (min(kRound, T - rb) + 7) >> 3;
+        const int nb = (min(min(kRound, T - rb), W - ow - rb) + 7) >> 3;
         for (int b = lane; b < nb; b += 64) {
           const uint32_t v = blk[b];
           uint32_t q = v & 0x1ffffu;
@@ -904,7 +937,7 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
               ofs = 0;
             }
           }
-          const int kw = min(8, ow + T - wbase);
+          const int kw = min(8, min(ow + T, W) - wbase);
           uint64_t *d = dst + wbase;
           if (kw == 8 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
 #pragma unroll
@@ -925,10 +958,21 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
         wave_lds_sync();  // blk reused by the next round
       }
       if (failed) break;
+      if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
+        ow = W;
+        e = fin;
+        break;
+      }
       ow += T;
       e = enext;
     }
     status[seg] = st;  // every lane the same value: no lane-dependent branch
+    if (kStream) {
+      in_off[seg] = a;
+      scur = a + e;
+      sfail = st;
+      if (seg == n - 1) in_off[n] = scur;
+    }
   }
 }
 
@@ -1087,7 +1131,7 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
   }
   if (hipFuncSetAttribute((const void *)cpk::encode_kernel<false>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kEncLds) != hipSuccess ||
-      hipFuncSetAttribute((const void *)cpk::decode_kernel,
+      hipFuncSetAttribute((const void *)cpk::decode_kernel<false>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess) {
     hipFree(c->tickets);
     free(c);
@@ -1139,9 +1183,22 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   // persistent: 8 blocks of 4 independent waves per CU (32 pieces in flight)
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (n + 3) / 4) grid = (n + 3) / 4;
-  hipLaunchKernelGGL(cpk::decode_kernel, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
-                     (const uint8_t *)d_packed, d_in_off, d_swo, n, (uint64_t *)d_out, d_status,
-                     ctx->tickets + 1);
+  hipLaunchKernelGGL(cpk::decode_kernel<false>, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
+                     (const uint8_t *)d_packed, const_cast<uint64_t *>(d_in_off), d_swo, n,
+                     (uint64_t *)d_out, d_status, ctx->tickets + 1, (uint64_t)0);
+  return hip_ok(hipGetLastError());
+}
+
+int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
+                      const uint64_t *d_swo, uint32_t n, void *d_out, uint64_t *d_in_off,
+                      int32_t *d_status, void *stream) {
+  if (!ctx || (n && (!d_in_off || !d_swo || !d_status))) return CPK_EINVAL;
+  if (((uintptr_t)d_packed & 15) || ((uintptr_t)d_out & 7)) return CPK_EINVAL;
+  if (n == 0) return CPK_OK;
+  DeviceGuard g(ctx->device);
+  hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds,
+                     (hipStream_t)stream, (const uint8_t *)d_packed, d_in_off, d_swo, n,
+                     (uint64_t *)d_out, d_status, ctx->tickets + 1, avail);
   return hip_ok(hipGetLastError());
 }
 
@@ -1231,6 +1288,57 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
   rc = cpk_decode_batch(ctx, d_pk, d_io, d_swo, n, d_out, d_st, nullptr);
   if (rc) goto done;
   if (hipMemcpy(h_status, d_st, n * 4ull, hipMemcpyDeviceToHost) ||
+      (words && hipMemcpy((uint8_t *)h_out + 8 * h_swo[0], d_out, words * 8, hipMemcpyDeviceToHost))) {
+    rc = CPK_EDEVICE;
+    goto done;
+  }
+  for (uint32_t i = 0; i < n; ++i)
+    if (h_status[i] != CPK_OK) {
+      rc = h_status[i];
+      break;
+    }
+done:
+  if (d_pk) hipFree(d_pk);
+  if (d_out) hipFree(d_out);
+  if (d_swo) hipFree(d_swo);
+  if (d_io) hipFree(d_io);
+  if (d_st) hipFree(d_st);
+  return rc;
+}
+
+int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
+                           const uint64_t *h_swo, uint32_t n, void *h_out, uint64_t *h_in_off,
+                           int32_t *h_status) {
+  if (!ctx || !h_swo || !h_in_off || !h_status) return CPK_EINVAL;
+  if (n == 0) {
+    h_in_off[0] = 0;
+    return CPK_OK;
+  }
+  DeviceGuard g(ctx->device);
+  uint64_t words = h_swo[n] - h_swo[0];
+  void *d_pk = nullptr, *d_out = nullptr;
+  uint64_t *d_swo = nullptr, *d_io = nullptr;
+  int32_t *d_st = nullptr;
+  int rc = CPK_OK;
+  std::vector<uint64_t> rs;
+  if (hipMalloc(&d_pk, avail + 64) != hipSuccess || hipMalloc(&d_out, words * 8 + 8) != hipSuccess ||
+      hipMalloc(&d_swo, (n + 1) * 8ull) != hipSuccess ||
+      hipMalloc(&d_io, (n + 1) * 8ull) != hipSuccess || hipMalloc(&d_st, n * 4ull) != hipSuccess) {
+    rc = CPK_ENOMEM;
+    goto done;
+  }
+  rs.resize(n + 1);
+  for (uint32_t i = 0; i <= n; ++i) rs[i] = h_swo[i] - h_swo[0];
+  if (hipMemset(d_pk, 0, avail + 64) ||
+      (avail && hipMemcpy(d_pk, h_packed, avail, hipMemcpyHostToDevice)) ||
+      hipMemcpy(d_swo, rs.data(), (n + 1) * 8ull, hipMemcpyHostToDevice)) {
+    rc = CPK_EDEVICE;
+    goto done;
+  }
+  rc = cpk_decode_stream(ctx, d_pk, avail, d_swo, n, d_out, d_io, d_st, nullptr);
+  if (rc) goto done;
+  if (hipMemcpy(h_status, d_st, n * 4ull, hipMemcpyDeviceToHost) ||
+      hipMemcpy(h_in_off, d_io, (n + 1) * 8ull, hipMemcpyDeviceToHost) ||
       (words && hipMemcpy((uint8_t *)h_out + 8 * h_swo[0], d_out, words * 8, hipMemcpyDeviceToHost))) {
     rc = CPK_EDEVICE;
     goto done;

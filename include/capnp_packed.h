@@ -104,6 +104,17 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
                      const uint64_t *d_seg_word_off, uint32_t n, void *d_out,
                      int32_t *d_status, void *stream);
 
+/* Stream decode (Serialize.read over PackedInputStream, Serialize.java:
+ * 165-175): pieces 0..n-1 are decoded back to back from one packed stream of
+ * `avail` bytes; each piece's read() stops when the piece is full and leaves
+ * the rest to the next (PackedInputStream.java:35-140), so no packed offsets
+ * are needed.  d_in_off[n+1] is written with the piece boundaries found
+ * (d_in_off[n] = bytes consumed).  A failed piece stops the stream: it and
+ * every later piece get its status.  Asynchronous on `stream`. */
+int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
+                      const uint64_t *d_seg_word_off, uint32_t n, void *d_out,
+                      uint64_t *d_in_off, int32_t *d_status, void *stream);
+
 /* Host-memory convenience forms (the socket/file ByteBuffer path,
  * SerializePacked.java:75-96, :119-134): stage through device memory,
  * run the batch kernels, copy back.  Synchronous.
@@ -115,6 +126,9 @@ int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_seg_word_of
 int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
                     const uint64_t *h_seg_word_off, uint32_t n, void *h_out,
                     int32_t *h_status);
+int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
+                           const uint64_t *h_seg_word_off, uint32_t n, void *h_out,
+                           uint64_t *h_in_off, int32_t *h_status);
 
 /* ---- benchmark support (synthetic device-resident workloads) ---- */
 

@@ -1,0 +1,126 @@
+// SerializePackedTest (runtime/src/test/java/org/capnproto/SerializePackedTest.java)
+// written against the C++ mirror of the reference API (capnproto-java_amd/
+// csrc/host/packed_stream.hpp), every byte through the MI355X kernels.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../capnproto-java_amd/csrc/host/packed_stream.hpp"
+
+using namespace capnp_amd;
+using Bytes = std::vector<uint8_t>;
+
+static int failures = 0;
+#define EXPECT(cond, msg)                                   \
+  do {                                                      \
+    if (!(cond)) {                                          \
+      std::fprintf(stderr, "FAIL %s:%d %s\n", __FILE__, __LINE__, msg); \
+      ++failures;                                           \
+    }                                                       \
+  } while (0)
+
+// assertPacksTo, SerializePackedTest.java:63-91
+static void assertPacksTo(Gpu &gpu, const Bytes &unpacked, const Bytes &packed) {
+  {
+    Bytes bytes(packed.size());
+    ArrayOutputStream writer(bytes.data(), bytes.size());
+    PackedOutputStream pos(gpu, writer);
+    pos.write(unpacked.data(), unpacked.size());
+    EXPECT(bytes == packed, "packed bytes");
+    EXPECT(writer.position() == packed.size(), "packed length");
+  }
+  {
+    ArrayInputStream reader(packed.data(), packed.size());
+    PackedInputStream stream(gpu, reader);
+    Bytes bytes(unpacked.size());
+    size_t n = 0;
+    try {
+      n = stream.read(bytes.data(), bytes.size());
+    } catch (const std::exception &e) {
+      EXPECT(false, e.what());
+    }
+    EXPECT(n == unpacked.size(), "read length");
+    EXPECT(bytes == unpacked, "unpacked bytes");
+  }
+}
+
+static Bytes rep(Bytes b, int times) {
+  Bytes out;
+  for (int i = 0; i < times; ++i) out.insert(out.end(), b.begin(), b.end());
+  return out;
+}
+static Bytes cat(std::initializer_list<Bytes> parts) {
+  Bytes out;
+  for (auto &p : parts) out.insert(out.end(), p.begin(), p.end());
+  return out;
+}
+
+int main() {
+  Gpu gpu(0);
+  // testSimplePacking, SerializePackedTest.java:20-60
+  assertPacksTo(gpu, {}, {});
+  assertPacksTo(gpu, {0, 0, 0, 0, 0, 0, 0, 0}, {0, 0});
+  assertPacksTo(gpu, {0, 0, 12, 0, 0, 34, 0, 0}, {0x24, 12, 34});
+  assertPacksTo(gpu, {1, 3, 2, 4, 5, 7, 6, 8}, {0xff, 1, 3, 2, 4, 5, 7, 6, 8, 0});
+  assertPacksTo(gpu, {0, 0, 0, 0, 0, 0, 0, 0, 1, 3, 2, 4, 5, 7, 6, 8},
+                {0, 0, 0xff, 1, 3, 2, 4, 5, 7, 6, 8, 0});
+  assertPacksTo(gpu, {0, 0, 12, 0, 0, 34, 0, 0, 1, 3, 2, 4, 5, 7, 6, 8},
+                {0x24, 12, 34, 0xff, 1, 3, 2, 4, 5, 7, 6, 8, 0});
+  assertPacksTo(gpu, {1, 3, 2, 4, 5, 7, 6, 8, 8, 6, 7, 4, 5, 2, 3, 1},
+                {0xff, 1, 3, 2, 4, 5, 7, 6, 8, 1, 8, 6, 7, 4, 5, 2, 3, 1});
+  const Bytes w18 = {1, 2, 3, 4, 5, 6, 7, 8};
+  assertPacksTo(gpu, cat({rep(w18, 4), {0, 2, 4, 0, 9, 0, 5, 1}}),
+                cat({{0xff}, w18, {3}, rep(w18, 3), {0xd6, 2, 4, 9, 5, 1}}));
+  assertPacksTo(gpu, cat({w18, w18, {6, 2, 4, 3, 9, 0, 5, 1}, w18, {0, 2, 4, 0, 9, 0, 5, 1}}),
+                cat({{0xff}, w18, {3}, w18, {6, 2, 4, 3, 9, 0, 5, 1}, w18, {0xd6, 2, 4, 9, 5, 1}}));
+  assertPacksTo(gpu, cat({{8, 0, 100, 6, 0, 1, 1, 2}, Bytes(24, 0), {0, 0, 1, 0, 2, 0, 3, 1}}),
+                {0xed, 8, 100, 6, 1, 1, 2, 0, 2, 0xd4, 1, 2, 3, 1});
+  assertPacksTo(gpu, cat({{0, 0, 0, 0, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0}, Bytes(8, 0)}),
+                {0x10, 2, 0x40, 1, 0, 0});
+  assertPacksTo(gpu, Bytes(8 * 200, 0), {0, 199});
+  Bytes packedOnes(10 + 8 * 199, 1);
+  packedOnes[0] = 255;
+  packedOnes[9] = 199;
+  assertPacksTo(gpu, Bytes(8 * 200, 1), packedOnes);
+
+  // read_shouldThrowDecodingExceptionOnEmptyArrayInputStream (:93-98)
+  {
+    Bytes empty;
+    ArrayInputStream in(empty.data(), 0);
+    bool threw = false;
+    try {
+      SerializePacked::read(gpu, in);
+    } catch (const DecodeException &) {
+      threw = true;
+    }
+    EXPECT(threw, "empty stream must throw DecodeException");
+  }
+  // read_shouldThrowDecodingExceptionWhenTryingToReadMoreThanAvailable (:100-105)
+  {
+    Bytes bytes = {17, 0, 127, 0, 0, 0, 0};
+    ArrayInputStream in(bytes.data(), bytes.size());
+    bool threw = false;
+    try {
+      SerializePacked::read(gpu, in);
+    } catch (const DecodeException &) {
+      threw = true;
+    }
+    EXPECT(threw, "truncated stream must throw DecodeException");
+  }
+  // SerializeTest.testSegmentReading (SerializeTest.java:82-141) through packing
+  for (int nseg = 1; nseg <= 4; ++nseg) {
+    std::vector<Bytes> segs;
+    for (int i = 0; i < nseg; ++i) segs.push_back(rep({(uint8_t)i, 0, 0, 0, 0, 0, 0, 0}, i));
+    Bytes stream = SerializePacked::write(gpu, segs);
+    ArrayInputStream in(stream.data(), stream.size());
+    auto got = SerializePacked::read(gpu, in);
+    EXPECT(got == segs, "segments round trip");
+    EXPECT(in.remaining() == 0, "stream consumed");
+  }
+  if (failures) {
+    std::fprintf(stderr, "%d failure(s)\n", failures);
+    return 1;
+  }
+  std::printf("serialize_packed_test: all passed\n");
+  return 0;
+}

@@ -205,3 +205,29 @@ def test_serialize_packed_message(ctx, oracle):
     assert pk.tobytes() == oracle.write_message(segs)
     st, got, _ = oracle.read_message(pk.tobytes())
     assert st == 0 and got == segs
+
+
+def test_stream_decode_message(ctx, oracle):
+    """SerializePacked.read: the reader knows each segment's size from the
+    table but not where its packed bytes end -- each read() stops when its
+    piece is full (PackedInputStream.java:35-140, Serialize.java:165-175)."""
+    rng = np.random.default_rng(9)
+    for trial in range(20):
+        nseg = int(rng.integers(1, 6))
+        segs = [_random_words(rng, int(rng.integers(0, 9000)), [.3, .3, .2, .2]).tobytes()
+                for _ in range(nseg)]
+        stream = oracle.write_message(segs)
+        table = (nseg - 1).to_bytes(4, "little") + b"".join((len(s) // 8).to_bytes(4, "little") for s in segs)
+        if len(table) % 8:
+            table += b"\0" * 4
+        pieces = [table] + segs
+        swo = _swo([len(p) // 8 for p in pieces])
+        extra = bytes(rng.integers(0, 256, size=int(rng.integers(0, 40)), dtype=np.uint8))
+        dec, bounds, st = ctx.decode_stream_host(np.frombuffer(stream + extra, np.uint8), swo)
+        assert (st == 0).all(), st
+        assert dec.tobytes() == b"".join(pieces)
+        assert int(bounds[-1]) == len(stream)
+    # truncated stream -> DecodeException (SerializePackedTest.java:100-105)
+    dec, bounds, st = ctx.decode_stream_host(np.frombuffer(bytes([17, 0, 127, 0, 0, 0, 0]), np.uint8),
+                                             _swo([1, 127]))
+    assert st[0] != 0 or st[1] != 0
