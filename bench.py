@@ -139,16 +139,11 @@ def main():
                 break
 
     if dist:
-        t = torch.tensor([wall, enc_ms, dec_ms, float(mism + bad_status), float(P)],
-                         dtype=torch.float64, device=dev)
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        wall = float(tmax[0])
-        enc_ms, dec_ms = float(tmax[1]), float(tmax[2])
-        errors = int(tsum[3])
-        P_total = float(tsum[4])
+        from capnp_packed.shard import reduce_max_sum
+        mx, sm = reduce_max_sum([wall, enc_ms, dec_ms, float(mism + bad_status), float(P)])
+        wall, enc_ms, dec_ms = mx[0], mx[1], mx[2]
+        errors = int(sm[3])
+        P_total = sm[4]
     else:
         errors = mism + bad_status
         P_total = float(P)

@@ -23,13 +23,13 @@ _PKG = Path(__file__).resolve().parents[1]
 LIB_PATH = _PKG / "lib" / "libcapnp_packed_hip.so"
 
 OK, EINVAL, ETRUNC, EOVERRUN, ETRAILING, ENOMEM, EDEVICE, EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6, -8
-TILE_WORDS = 8192  # largest piece this build encodes/decodes
+TILE_WORDS = 8192  # encoder tile: larger pieces are cut into tiles
 
 EXPORTS = [
     "cpk_abi_version", "cpk_status_string", "cpk_packed_bound", "cpk_batch_packed_capacity",
     "cpk_ctx_create", "cpk_ctx_destroy", "cpk_ctx_device", "cpk_encode_batch",
     "cpk_decode_batch", "cpk_decode_stream", "cpk_encode_host", "cpk_decode_host",
-    "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch",
+    "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch", "cpk_ctx_take_error",
 ]
 
 
@@ -52,8 +52,10 @@ class GenParams(ctypes.Structure):
 _lib = None
 
 
-def load(path: Path | None = None) -> ctypes.CDLL:
-    """Load the HIP codec library; raises if it is missing (no fallback)."""
+def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
+    """Load the HIP codec library; raises if it is missing (no fallback).
+    strict=False tolerates an older build without some entry points (A/B
+    timing tools only)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -79,8 +81,11 @@ def load(path: Path | None = None) -> ctypes.CDLL:
         "cpk_decode_stream_host": ([vp, vp, u64, vp, u32, vp, vp, vp], i32),
         "cpk_generate": ([vp, ctypes.POINTER(GenParams), vp, u32, vp, vp], i32),
         "cpk_count_mismatch": ([vp, vp, vp, u64, vp, vp], i32),
+        "cpk_ctx_take_error": ([vp, vp], i32),
     }
     for name, (args, res) in sig.items():
+        if not strict and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
@@ -144,6 +149,11 @@ class Context:
                                         int(max_seg_words), d_out.data_ptr(), d_out_off.data_ptr(),
                                         self._stream(stream))
         _check(rc, "cpk_encode_batch")
+
+    def take_error(self, stream=None) -> int:
+        """Synchronises `stream`; CPK_EINVAL if an encode since the last call
+        met a piece larger than its max_seg_words hint (output undefined)."""
+        return self._lib.cpk_ctx_take_error(self.handle, self._stream(stream))
 
     def decode_batch(self, d_packed, d_in_off, d_seg_word_off, d_out, d_status, stream=None):
         n = d_seg_word_off.numel() - 1

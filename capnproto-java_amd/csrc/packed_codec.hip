@@ -274,13 +274,137 @@ __device__ __forceinline__ int mbcnt(uint64_t m) {
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// ---- tiled pieces: run state carried across 8192-word tiles --------------
+// A piece longer than one tile is cut into tiles that are encoded by
+// different workgroups.  What a tile's roles need from before it is the state
+// of the run that crosses its first word (PackedOutputStream.java:119-161):
+// a zero run's phase (heads every 256 words from the run start) or a D/L
+// stretch's last 0xFF head.  Each tile publishes the state at its end in
+// tstate[tau] ([63:62] flag, [33:32] group, [31:0] value):
+//   LOCAL  value known: Z -> (tile end - run start) mod 256; D/L -> distance
+//          from the tile end back to the last head (0 = no D yet); M -> none;
+//   PASS   the whole tile continues one run and maps the state through
+//          unchanged (zero run: 8192 is a multiple of 256) or, all-D, to
+//          min(dist, 256) -- republished as LOCAL once resolved.
+// A continued tile resolves its entry state by a look-back to the nearest
+// LOCAL (tile 0 of every piece is LOCAL), the pattern of lb_resolve.
+constexpr uint64_t kStLocal = 1ull << 62, kStPass = 2ull << 62;
+constexpr int kNoHead = -(1 << 28);
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+// first D word at or after x (< W) from the D ballots of pass 1 (mks[2q+1]
+// is the D mask of 64-word step q); W if none
+__device__ int enc_first_d(const uint64_t *mks, int x, int W) {
+  if (x >= W) return W;
+  int q = x >> 6;
+  uint64_t m = mks[2 * q + 1] & (~0ull << (x & 63));
+  while (!m) {
+    ++q;
+    if (q * 64 >= W) return W;
+    m = mks[2 * q + 1];
+  }
+  return min(q * 64 + __builtin_ctzll(m), W);
+}
+// walk the head chain from the first D >= x; distance from W back to the
+// last head, 0 if there is none
+__device__ int enc_chain_dist(const uint64_t *mks, int x, int W) {
+  int last = -1;
+  int h = enc_first_d(mks, x, W);
+  while (h < W) {
+    last = h;
+    h = enc_first_d(mks, h + 256, W);
+  }
+  return last >= 0 ? W - last : 0;
+}
+// wave 0, all lanes: publish this tile's exit state, resolve its entry state
+// into scr[69..71]
+__device__ void enc_tile_state(const uint64_t *mks, int *scr, uint64_t *tstate, uint32_t tau,
+                               int j, int W, bool lastTile, int g0, int gm1) {
+  const int lane = lane_id();
+  const int gF = scr[72];
+  int sF = -1;
+  bool allD = true;
+  for (int q = 0; q < kEncWaves; ++q) {
+    sF = max(sF, scr[q]);
+    allD = allD && scr[76 + q] != 0;
+  }
+  uint64_t outv = 0;
+  if (!lastTile) {
+    if (gF == 2) outv = kStLocal | (2ull << 32);
+    else if (sF >= 0)
+      outv = kStLocal | ((uint64_t)gF << 32) |
+             (gF == 0 ? (uint64_t)((-sF) & 255) : (uint64_t)enc_chain_dist(mks, sF, W));
+    else if (gF == 0) outv = kStPass;
+    else if (allD) outv = kStPass | (1ull << 32);
+    if (outv && lane == 0) st_status(&tstate[tau], outv);
+  }
+  int rsIn = -1, hlIn = kNoHead, cont = 0;
+  if (j > 0 && W > 0 && g0 == gm1) {
+    cont = g0 + 1;
+    if (g0 != 2) {
+      int64_t top = (int64_t)tau - 1;
+      bool sawD = false;
+      uint64_t val = 0;
+      uint32_t spins = 0;
+      for (;;) {
+        const int64_t idx = top - lane;
+        const uint64_t v = idx >= 0 ? ld_status(&tstate[idx]) : kStLocal;
+        const uint64_t loc = __ballot((v >> 62) == 1);
+        const int first = loc ? __builtin_ctzll(loc) : 64;
+        const uint64_t rel = first >= 63 ? ~0ull : ((2ull << first) - 1);
+        if (__ballot((v >> 62) == 0) & rel) {
+          if (++spins > (1u << 24)) break;  // cannot happen with in-order tickets
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        sawD = sawD || __ballot(lane < first && ((v >> 32) & 1)) != 0;
+        if (first < 64) {
+          val = readlane64(v, first);
+          break;
+        }
+        top -= 64;
+      }
+      const uint32_t x = (uint32_t)val;
+      if (g0 == 0) {
+        rsIn = -(int)(x & 255);
+        if (!lastTile && outv == kStPass && lane == 0)
+          st_status(&tstate[tau], kStLocal | (uint64_t)(x & 255));
+      } else {
+        uint32_t dist = x;  // 0: no head yet in the stretch
+        if (sawD) dist = (dist == 0 || dist > 256) ? 256u : dist;
+        rsIn = -kTileWords;  // forces the chain walk for the continued stretch
+        hlIn = dist ? -(int)dist : kNoHead;
+        if (!lastTile && (outv >> 62) == 2 && lane == 0)
+          st_status(&tstate[tau], kStLocal | (1ull << 32) | (uint64_t)((dist == 0 || dist > 256) ? 256u : dist));
+      }
+    }
+  }
+  if (!lastTile && !outv) {
+    // one D/L stretch over the whole tile, with L words: its chain goes on
+    // from the entry head
+    outv = kStLocal | (1ull << 32) | (uint64_t)enc_chain_dist(mks, max(hlIn + 256, 0), W);
+    if (lane == 0) st_status(&tstate[tau], outv);
+  }
+  if (lane == 0) {
+    scr[69] = rsIn;
+    scr[70] = hlIn;
+    scr[71] = cont;
+  }
+}
+
 // info word per (step, lane): [7:0] nonzero mask, [9:8] group,
-// [10] member, [11] zero-run head, [15:12] bytes, [23:16] run count
-template <bool kUnused = false>
+// [10] member, [11] zero-run head, [15:12] bytes, [23:16] run count,
+// [24] word of a D/L stretch longer than 256 words (chain walk decides)
+template <bool kTiled>
 __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status,
-    uint32_t *ticket) {
+    uint32_t *ticket, const uint32_t *__restrict__ tmap, const uint64_t *__restrict__ toff,
+    uint64_t *tstate, uint32_t *err) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t *stage = smem;
   uint32_t *stage32 = reinterpret_cast<uint32_t *>(smem);
@@ -290,20 +414,46 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
   int *scr = reinterpret_cast<int *>(smem + kEncScr);
   uint64_t *mks = reinterpret_cast<uint64_t *>(smem + kEncMasks);
   // scr[0..15] last run start per wave, [16..31] first run start,
-  // [32..47] last D, [48..63] bytes per wave, [64..65] ticket, [66..67] base
+  // [32..47] last D, [48..63] bytes per wave, [64..65] ticket, [66..67] base,
+  // tiled only: [68] run end after the tile, [69] run start entering it,
+  // [70] last 0xFF head entering it, [71] continued group + 1, [72] group of
+  // the tile's last word, [76..91] all-D flag per wave
 
   const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
   fill_luts(lut, false);
   PH_INIT(scr)
 
+  // tiled: work item = tile tau of T (pieces cut into 8192-word tiles, in
+  // stream order); otherwise work item = piece
+  const uint32_t T = kTiled ? (uint32_t)toff[n] : n;
   for (uint32_t it = 0;; ++it) {
     if (tid == 0) scr[64 + (it & 1)] = (int)atomicAdd(ticket, 1u);
     __syncthreads();  // also orders the previous piece's LDS use
-    const uint32_t seg = (uint32_t)__builtin_amdgcn_readfirstlane(scr[64 + (it & 1)]);
-    if (seg >= n) break;
+    const uint32_t tau = (uint32_t)__builtin_amdgcn_readfirstlane(scr[64 + (it & 1)]);
+    if (tau >= T) break;
     PH(0)
-    const uint64_t w0 = swo[seg];
-    const int W = (int)(swo[seg + 1] - w0);  // <= kTileWords (host-checked)
+    uint32_t seg = tau;
+    int j = 0;             // tile index within the piece
+    bool lastTile = true;  // no tile of this piece follows
+    uint64_t w0, rest = 0;  // rest: words of the piece after this tile
+    int W;
+    if (kTiled) {
+      seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)tmap[tau]);
+      j = (int)(tau - (uint32_t)toff[seg]);
+      const uint64_t p0 = swo[seg], pw = swo[seg + 1] - p0, tb = (uint64_t)j * kTileWords;
+      const uint64_t rem = pw - tb;
+      w0 = p0 + tb;
+      W = rem < (uint64_t)kTileWords ? (int)rem : kTileWords;
+      lastTile = rem <= (uint64_t)kTileWords;
+      rest = rem - (uint64_t)W;
+    } else {
+      w0 = swo[seg];
+      const uint64_t pw = swo[seg + 1] - w0;
+      if (pw > (uint64_t)kTileWords) {  // max_seg_words hint was wrong
+        if (tid == 0) atomicOr(err, 1u);
+      }
+      W = pw > (uint64_t)kTileWords ? kTileWords : (int)pw;
+    }
     // per-piece opaque copies of this wave's / lane's first word: keep hipcc
     // from hoisting ~100 per-lane addresses out of the persistent loop
     int wb = __builtin_amdgcn_readfirstlane(w * (kSteps * 64));  // first word of this wave
@@ -326,12 +476,14 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
 #pragma unroll
       for (int s = 0; s < kSteps; ++s) wv[s] = W ? src[min(k0 + s * 64, kl)] : 0ull;
     }
-    int gprev = 3;  // group of word wb - 1
-    if (w > 0 && lane == 0 && wb - 1 < W) {
+    int gprev = 3;  // group of word wb - 1 (3 = none: a run starts at word 0)
+    if (lane == 0 && (w > 0 ? wb - 1 < W : j > 0)) {
       uint64_t v = src[wb - 1];
       gprev = grp_of(word_mask((uint32_t)v, (uint32_t)(v >> 32)));
     }
     gprev = readlane(gprev, 0);
+    const int gm1 = gprev;  // wave 0: group of the word before the tile
+    bool allD = true;
 #pragma unroll
     for (int s = 0; s < kSteps; ++s) {
       const int k = k0 + s * 64;
@@ -339,8 +491,9 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
       const uint32_t m = word_mask((uint32_t)v, (uint32_t)(v >> 32));
       const int g = k < W ? grp_of(m) : 3;
       const int gp = wave_shr1(g, gprev);
-      const uint64_t sb = __ballot(g != 3 && (k == 0 || g != gp));
+      const uint64_t sb = __ballot(g != 3 && g != gp);
       const uint64_t db = __ballot(k < W && m == 0xffu);
+      allD = allD && db == ~0ull;
       if (lane == 0) {
         SMASK(s) = sb;
         DMASK(s) = db;
@@ -349,7 +502,7 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
       info[s] = m | ((uint32_t)g << 8);
     }
     {
-      int ls = -1, fs = kBig, ld = -1;
+      int ls = -kBig, fs = kBig, ld = -1;  // -kBig: no start (below any carried start)
 #pragma unroll
       for (int s = 0; s < kSteps; ++s) {
         const uint64_t sb = SMASK(s), db = DMASK(s);
@@ -363,13 +516,46 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
         scr[w] = ls;
         scr[16 + w] = fs;
         scr[32 + w] = ld;
+        if (kTiled) scr[76 + w] = allD;
+      }
+    }
+    if (kTiled && w == kEncWaves - 1) {
+      // run end after the tile (looked up to 256 words ahead: counts cap at
+      // 255, stretches longer than 256 words take the chain walk anyway)
+      int look = W;
+      if (!lastTile) {
+        uint64_t v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint64_t p = (uint64_t)(64 * r + lane);
+          v[r] = p < rest ? src[W + 64 * r + lane] : 0ull;
+        }
+        int gp = gprev;  // group of word W - 1
+        look = W + 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int g = (uint64_t)(64 * r + lane) < rest
+                            ? grp_of(word_mask((uint32_t)v[r], (uint32_t)(v[r] >> 32)))
+                            : 3;
+          const uint64_t b = __ballot(g != wave_shr1(g, gp));
+          if (b && look == W + 256) look = W + 64 * r + lo_bit(b);
+          gp = readlane(g, 63);
+        }
+      }
+      if (lane == 0) {
+        scr[68] = look;
+        scr[72] = gprev;
       }
     }
     __syncthreads();
+    if (kTiled) {
+      if (w == 0) enc_tile_state(mks, scr, tstate, tau, j, W, lastTile, readlane((int)info[0], 0) >> 8 & 3, gm1);
+      __syncthreads();
+    }
     PH(1)
     // carries across waves: run start / last D entering this wave, first
     // run start after it
-    int cS = -1, cD = -1, eOut = W;
+    int cS = kTiled ? scr[69] : -1, cD = -1, eOut = kTiled ? scr[68] : W;
     for (int q = 0; q < w; ++q) {
       cS = max(cS, scr[q]);
       cD = max(cD, scr[32 + q]);
@@ -414,6 +600,7 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
       } else if (g == 1) {
         if (re - rs > 256) {
           anyLong = 1;  // resolved by the chain walk below
+          x |= 1u << 24;  // long-stretch word
           nb = 8;       // provisional: L words are 8 either way, D fixed below
         } else if (rd >= rs) {
           x |= 1u << 10;  // inside the 0xFF run of the stretch's first D
@@ -425,7 +612,7 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
         nb = 1 + __builtin_popcount(m);
       }
       const uint32_t cnt = (uint32_t)min(255, max(re - k - 1, 0));
-      info[s] = (x & 0x7ffu) | ((uint32_t)nb << 12) | (cnt << 16);
+      info[s] = (x & 0x10007ffu) | ((uint32_t)nb << 12) | (cnt << 16);
       if (smask_s) cS = base + hi_bit(smask_s);
       if (dmask_s) cD = base + hi_bit(dmask_s);
       __builtin_amdgcn_sched_barrier(0);
@@ -443,7 +630,8 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
         const int dw = (wb + s * 64) >> 5;
         if (lane == 0) {
           dbits[dw] = (uint32_t)DMASK(s);
-          hbits[dw] = (uint32_t)SMASK(s);
+          // a stretch continued from the previous tile: a start marker at 0
+          hbits[dw] = (uint32_t)SMASK(s) | (kTiled && dw == 0 && scr[71] == 2 ? 1u : 0u);
         } else if (lane == 1) {
           dbits[dw + 1] = (uint32_t)(DMASK(s) >> 32);
           hbits[dw + 1] = (uint32_t)(SMASK(s) >> 32);
@@ -456,15 +644,12 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
       for (int s = 0; s < kSteps; ++s) {
         sl[s] = 0;
         const int k = k0 + s * 64;
-        const int nb = (int)((info[s] >> 12) & 15);
-        const int g = (int)((info[s] >> 8) & 3);
-        const int re = k + 1 + (int)(info[s] >> 16);  // only exact when < 255
-        (void)re;
-        if (g == 1 && !(info[s] & (1u << 10)) && nb == 8) {
+        if ((info[s] >> 24) & 1) {
           int d = k >> 5;
           uint32_t mm = hbits[d] & ((k & 31) == 31 ? ~0u : ((2u << (k & 31)) - 1));
           while (!mm) mm = hbits[--d];
           sl[s] = d * 32 + 31 - __builtin_clz(mm);
+          if (kTiled && sl[s] == 0 && scr[71] == 2) sl[s] = -kTileWords;  // continued stretch
         }
       }
       __syncthreads();
@@ -479,28 +664,39 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
         const int re = sg ? base + lo_bit(sg) : nextS[s];
         const bool st = (SMASK(s) >> lane) & 1;
         if (st && ((info[s] >> 8) & 3) == 1 && re - k > 256) {
-          int h = bm_next(dbits, k, re);
-          while (h < re) {
+          const int rw = min(re, W);
+          int h = bm_next(dbits, k, rw);
+          while (h < rw) {
             atomicOr(&hbits[h >> 5], 1u << (h & 31));
             const int p = h + 256;
-            if (p >= re) break;
-            h = bm_next(dbits, p, re);
+            if (p >= rw) break;
+            h = bm_next(dbits, p, rw);
           }
+        }
+      }
+      if (kTiled && tid == 0 && scr[71] == 2) {
+        // the continued stretch: its chain goes on from the last head of the
+        // previous tile, h' = first D >= h + 256 (PackedOutputStream.java:145-161)
+        int rw = scr[68];
+        for (int q = 0; q < kEncWaves; ++q) rw = scr[16 + q] < kBig ? min(rw, scr[16 + q]) : rw;
+        rw = min(rw, W);
+        int h = bm_next(dbits, max(scr[70] + 256, 0), rw);
+        while (h < rw) {
+          atomicOr(&hbits[h >> 5], 1u << (h & 31));
+          const int p = h + 256;
+          if (p >= rw) break;
+          h = bm_next(dbits, p, rw);
         }
       }
       __syncthreads();
 #pragma unroll
       for (int s = 0; s < kSteps; ++s) {
         const int k = k0 + s * 64;
-        const int base = wb + s * 64;
         const uint32_t m = info[s] & 0xffu;
-        const int g = (int)((info[s] >> 8) & 3);
-        const uint64_t sm = SMASK(s) & lanemask_le();
-        const uint64_t sg = SMASK(s) & ~lanemask_le();
-        const int re = sg ? base + lo_bit(sg) : nextS[s];
-        if (g == 1 && re - sl[s] > 256 && !(info[s] & (1u << 10))) {
-          (void)sm;
-          const bool mem = bm_any(hbits, max(sl[s], k - 255), k - 1);
+        if ((info[s] >> 24) & 1) {
+          // member iff a head of its stretch lies in [k - 255, k - 1]
+          bool mem = bm_any(hbits, max(max(sl[s], k - 255), 0), k - 1);
+          if (kTiled && sl[s] < 0) mem = mem || k - 255 <= scr[70];
           const int nb = mem ? 8 : (m == 0xffu ? 10 : 8);
           info[s] = (info[s] & ~(0xfu << 12)) | ((uint32_t)nb << 12) | (mem ? (1u << 10) : 0u);
         }
@@ -527,7 +723,7 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
       total += t;
     }
     // publish the aggregate now; the prefix is resolved after compaction
-    if (tid == 0) lb_publish(status, seg, (uint64_t)total);
+    if (tid == 0) lb_publish(status, tau, (uint64_t)total);
     // zero the staging lines this piece uses (the strings are OR-ed in)
     {
       const int nl = (total + 19) >> 4;
@@ -560,7 +756,7 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
         const uint64_t sel = lut[m];
         const uint32_t c0 = __builtin_amdgcn_perm(h, l, (uint32_t)sel);
         const uint32_t c1 = __builtin_amdgcn_perm(h, l, (uint32_t)(sel >> 32));
-        const uint32_t cnt = x >> 16;
+        const uint32_t cnt = (x >> 16) & 0xffu;
         d0 = m | (c0 << 8);
         d1 = (c0 >> 24) | (c1 << 8);
         d2 = c1 >> 24;
@@ -590,11 +786,11 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
 
     // ---- decoupled look-back (wave 0), overlapped with the compaction -----
     if (w == 0) {
-      uint64_t b = lb_resolve(status, seg, (uint64_t)total);
+      uint64_t b = lb_resolve(status, tau, (uint64_t)total);
       if (lane == 0) {
         *reinterpret_cast<uint64_t *>(&scr[66]) = b;
-        out_off[seg] = b;
-        if (seg == n - 1) out_off[n] = b + (uint64_t)total;
+        if (j == 0) out_off[seg] = b;
+        if (tau == T - 1) out_off[n] = b + (uint64_t)total;
       }
     }
     __syncthreads();
@@ -631,6 +827,66 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
 #undef DMASK
   }
   PH_FLUSH(0)
+}
+
+// Tile plan for the tiled encoder: toff[i] = first tile of piece i (one tile
+// per 8192 words, at least one per piece), toff[n] = T, tmap[tau] = piece of
+// tile tau.  Single pass: 8192 pieces per workgroup, in ticket order, block
+// prefixes by look-back.  Tiles beyond `cap` (a wrong max_seg_words hint) are
+// reported in *err and not planned.
+constexpr int kPlanThreads = 1024, kPlanPer = 8;
+__global__ __launch_bounds__(kPlanThreads) void tile_plan_kernel(
+    const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ toff,
+    uint32_t *__restrict__ tmap, uint64_t cap, uint64_t *pstatus, uint32_t *ticket,
+    uint32_t *err) {
+  __shared__ int wsum[kPlanThreads / 64];
+  __shared__ uint32_t blk_s;
+  __shared__ uint64_t base_s;
+  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+  if (tid == 0) blk_s = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t blk = blk_s;
+  const uint64_t i0 = (uint64_t)blk * (kPlanThreads * kPlanPer) + (uint64_t)tid * kPlanPer;
+  int c[kPlanPer];
+  int t = 0;
+#pragma unroll
+  for (int q = 0; q < kPlanPer; ++q) {
+    const uint64_t i = i0 + q;
+    c[q] = 0;
+    if (i < n) {
+      const uint64_t pw = swo[i + 1] - swo[i];
+      c[q] = pw == 0 ? 1 : (int)((pw + kTileWords - 1) / kTileWords);
+    }
+    t += c[q];
+  }
+  const int incl = wave_incl_add(t);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int wex = 0, tot = 0;
+  for (int q = 0; q < kPlanThreads / 64; ++q) {
+    if (q < w) wex += wsum[q];
+    tot += wsum[q];
+  }
+  if (tid == 0) lb_publish(pstatus, blk, (uint64_t)tot);
+  if (w == 0) {
+    const uint64_t b = lb_resolve(pstatus, blk, (uint64_t)tot);
+    if (lane == 0) base_s = b;
+  }
+  __syncthreads();
+  uint64_t o = base_s + (uint64_t)(wex + incl - t);
+#pragma unroll
+  for (int q = 0; q < kPlanPer; ++q) {
+    const uint64_t i = i0 + q;
+    if (i < n) {
+      toff[i] = o;
+      for (int k = 0; k < c[q]; ++k) {
+        if (o + k < cap) tmap[o + k] = (uint32_t)i;
+        else atomicOr(err, 2u);
+      }
+      if (i == n - 1) toff[n] = o + c[q] < cap ? o + c[q] : cap;
+      o += c[q];
+    }
+  }
 }
 
 // ------------------------------------------------------------ decoder
@@ -715,7 +971,7 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
 //   Serialize.read calls it, Serialize.java:165-175); in_off[0..n] is
 //   written with the piece boundaries found.
 template <bool kStream>
-__global__ __launch_bounds__(kDecThreads) void decode_kernel(
+__global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
     const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
     int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail) {
@@ -809,7 +1065,15 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
       uint64_t onmask = 0;
       uint32_t entry = e;
       uint32_t enext;
-      {
+      // common case: every lane's walk lands in the next lane's chunk
+      const int na = (int)((wend - e + 31) >> 5);  // active lanes (chunks)
+      const bool ok = lane < na - 1 ? (S < wend && (int)((S - e) >> 5) == lane + 1)
+                                    : (lane == na - 1 ? S >= wend : true);
+      if (__ballot(!ok) == 0) {
+        onmask = na == 64 ? ~0ull : ((1ull << na) - 1);
+        entry = (uint32_t)wave_shr1((int)S, (int)e);
+        enext = (uint32_t)__builtin_amdgcn_readlane((int)S, na - 1);
+      } else {
         int cur = 0;
         for (;;) {
           onmask |= 1ull << cur;
@@ -877,13 +1141,14 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
                 else if (q + adv > P) code = 2;
               }
               if (!kStream && !code && oo + nw == W && q + adv < P) code = 4;
-              if (code) err = (int)((q << 3) | (uint32_t)code);
+              if (code) err = (int)(((q - e) << 3) | (uint32_t)code);  // window-relative
               if (oo + nw == W) fin = q + adv;
             }
             // blocks of this round whose first word this record covers
             const int lo = max(o, rb), hi = min(o + nw, rb + kRound);
+            // window-relative record position (< 2 KiB) | offset in the run
             for (int bb = (lo + 7) & ~7; bb < hi; bb += 8)
-              blk[(bb - rb) >> 3] = q | ((uint32_t)(bb - o) << 17);
+              blk[(bb - rb) >> 3] = (q - e) | ((uint32_t)(bb - o) << 16);
             o += nw;
             q += adv;
           }
@@ -899,60 +1164,57 @@ __global__ __launch_bounds__(kDecThreads) void decode_kernel(
         }
         wave_lds_sync();
         const int nb = (min(min(kRound, T - rb), W - ow - rb) + 7) >> 3;
+        const bool al16 = (((uintptr_t)(dst + ow + rb)) & 15) == 0;  // uniform
         for (int b = lane; b < nb; b += 64) {
           const uint32_t v = blk[b];
-          uint32_t q = v & 0x1ffffu;
-          int ofs = (int)(v >> 17);
+          uint32_t q = e + (v & 0xffffu);
+          int ofs = (int)(v >> 16);
           const int wbase = ow + rb + 8 * b;  // piece word of the block's first word
-          uint64_t words[8];
+          const int kw = min(8, min(ow + T, W) - wbase);
+          uint64_t *d = dst + wbase;
+          uint64_t prev = 0;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
+            // branch-free per word: the expansion LUT maps tag 0x00 to zero
+            // bytes and 0xFF to the identity, so one v_perm serves all three
+            // record kinds (PackedInputStream.java:84-134)
             const uint32_t tag = pkw[q];
-            uint64_t x;
-            int nw;
-            uint32_t adv;
-            if (tag == 0) {
-              x = 0;
-              nw = 1 + pkw[q + 1];
-              adv = 2;
-            } else if (tag == 0xffu) {
-              const uint32_t rn = pkw[q + 9];
-              nw = 1 + (int)rn;
-              adv = 10 + 8 * rn;
-              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp);
-            } else {
-              const uint64_t raw = read8(pkw, q + 1, lend, gp);
-              const uint64_t sel = lut[tag];
-              const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
-              const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
-              const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
-              x = (uint64_t)x0 | ((uint64_t)x1 << 32);
-              nw = 1;
-              adv = 1 + __builtin_popcount(tag);
+            const bool z = tag == 0, f = tag == 0xffu;
+            const uint32_t c = pkw[q + (z ? 1u : 9u)];
+            const uint32_t cnt = (z || f) ? c : 0u;
+            const int nw = 1 + (int)cnt;
+            const uint32_t adv = z ? 2u : f ? 10u + 8u * cnt : 1u + __builtin_popcount(tag);
+            const uint32_t src = (f && ofs > 0) ? q + 10 + 8 * (uint32_t)(ofs - 1) : q + 1;
+            const uint64_t raw = read8(pkw, src, lend, gp);
+            const uint64_t sel = lut[tag];
+            const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
+            const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
+            const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
+            const uint64_t x = (uint64_t)x0 | ((uint64_t)x1 << 32);
+            // words go out as they are made: 16-byte stores of pairs when the
+            // round's output is 16-byte aligned (uniform), else 8-byte stores
+            if (al16) {
+              if (i & 1) {
+                if (i < kw) {
+                  uint4 v4;
+                  v4.x = (uint32_t)prev;
+                  v4.y = (uint32_t)(prev >> 32);
+                  v4.z = x0;
+                  v4.w = x1;
+                  *reinterpret_cast<uint4 *>(d + i - 1) = v4;
+                } else if (i - 1 < kw) {
+                  d[i - 1] = prev;
+                }
+              }
+              prev = x;
+            } else if (i < kw) {
+              d[i] = x;
             }
-            words[i] = x;
             // past the window's last word: stay put (never stored)
             if (++ofs == nw && wbase + i + 1 < ow + T) {
               q += adv;
               ofs = 0;
             }
-          }
-          const int kw = min(8, min(ow + T, W) - wbase);
-          uint64_t *d = dst + wbase;
-          if (kw == 8 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
-#pragma unroll
-            for (int i = 0; i < 8; i += 2) {
-              uint4 v4;
-              v4.x = (uint32_t)words[i];
-              v4.y = (uint32_t)(words[i] >> 32);
-              v4.z = (uint32_t)words[i + 1];
-              v4.w = (uint32_t)(words[i + 1] >> 32);
-              *reinterpret_cast<uint4 *>(d + i) = v4;
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-              if (i < kw) d[i] = words[i];
           }
         }
         wave_lds_sync();  // blk reused by the next round
@@ -1045,7 +1307,9 @@ struct cpk_ctx_s {
   int cus;
   uint64_t *status;       // look-back words
   uint64_t status_cap;    // entries
-  uint32_t *tickets;      // [0] encode, [1] decode  (16 B, memset block)
+  uint32_t *tickets;      // [0] encode, [1] decode, [2] tile plan, [3] error bits
+  void *plan;             // tiled encode: toff | tmap | pstatus | tstate
+  uint64_t plan_cap;      // bytes
 };
 
 namespace {
@@ -1076,6 +1340,19 @@ int ensure_status(cpk_ctx ctx, uint64_t n) {
   ctx->status_cap = cap;
   return CPK_OK;
 }
+int ensure_plan(cpk_ctx ctx, uint64_t bytes) {
+  if (bytes <= ctx->plan_cap) return CPK_OK;
+  if (ctx->plan) hipFree(ctx->plan);
+  ctx->plan = nullptr;
+  uint64_t cap = bytes + bytes / 4;
+  if (hipMalloc(&ctx->plan, cap) != hipSuccess) {
+    ctx->plan_cap = 0;
+    return CPK_ENOMEM;
+  }
+  ctx->plan_cap = cap;
+  return CPK_OK;
+}
+uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 }  // namespace
 
 extern "C" {
@@ -1131,6 +1408,8 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
   }
   if (hipFuncSetAttribute((const void *)cpk::encode_kernel<false>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kEncLds) != hipSuccess ||
+      hipFuncSetAttribute((const void *)cpk::encode_kernel<true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kEncLds) != hipSuccess ||
       hipFuncSetAttribute((const void *)cpk::decode_kernel<false>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess) {
     hipFree(c->tickets);
@@ -1145,6 +1424,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (!ctx) return;
   DeviceGuard g(ctx->device);
   if (ctx->status) hipFree(ctx->status);
+  if (ctx->plan) hipFree(ctx->plan);
   if (ctx->tickets) hipFree(ctx->tickets);
   free(ctx);
 }
@@ -1154,21 +1434,77 @@ int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
 int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n,
                      uint64_t max_seg_words, void *d_out, uint64_t *d_out_off, void *stream) {
   if (!ctx || (!d_swo && n) || !d_out_off) return CPK_EINVAL;
-  if (max_seg_words == 0 || max_seg_words > (uint64_t)cpk::kTileWords) return CPK_EUNSUPPORTED;
   if (((uintptr_t)d_out & 15) || ((uintptr_t)d_in & 7)) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
-  int rc = ensure_status(ctx, n);
-  if (rc) return rc;
-  if (hipMemsetAsync(ctx->status, 0, (size_t)n * 8, s) != hipSuccess) return CPK_EDEVICE;
   if (hipMemsetAsync(ctx->tickets, 0, 16, s) != hipSuccess) return CPK_EDEVICE;
+  if (max_seg_words != 0 && max_seg_words <= (uint64_t)cpk::kTileWords) {
+    // one workgroup per piece
+    int rc = ensure_status(ctx, n);
+    if (rc) return rc;
+    if (hipMemsetAsync(ctx->status, 0, (size_t)n * 8, s) != hipSuccess) return CPK_EDEVICE;
+    unsigned grid = (unsigned)(2 * ctx->cus);
+    if (grid > n) grid = n;
+    hipLaunchKernelGGL(cpk::encode_kernel<false>, dim3(grid), dim3(cpk::kEncThreads), cpk::kEncLds,
+                       s, (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
+                       ctx->tickets, (const uint32_t *)nullptr, (const uint64_t *)nullptr,
+                       (uint64_t *)nullptr, ctx->tickets + 3);
+    return hip_ok(hipGetLastError());
+  }
+  // tiled: pieces cut into 8192-word tiles; the tile count is bounded from the
+  // hint, or from the batch's word count when there is no hint
+  uint64_t tiles;
+  if (max_seg_words) {
+    tiles = (uint64_t)n * ((max_seg_words + cpk::kTileWords - 1) / cpk::kTileWords);
+  } else {
+    uint64_t ends[2];
+    if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return CPK_EDEVICE;
+    tiles = (uint64_t)n + (ends[1] - ends[0]) / cpk::kTileWords;
+  }
+  const uint64_t blocks = ((uint64_t)n + cpk::kPlanThreads * cpk::kPlanPer - 1) /
+                          (cpk::kPlanThreads * cpk::kPlanPer);
+  const uint64_t o_tmap = align256(((uint64_t)n + 1) * 8);
+  const uint64_t o_pst = o_tmap + align256(tiles * 4);
+  const uint64_t o_tst = o_pst + align256(blocks * 8);
+  const uint64_t bytes = o_tst + align256(tiles * 8);
+  int rc = ensure_plan(ctx, bytes);
+  if (rc) return rc;
+  rc = ensure_status(ctx, tiles);
+  if (rc) return rc;
+  uint8_t *plan = (uint8_t *)ctx->plan;
+  uint64_t *toff = (uint64_t *)plan;
+  uint32_t *tmap = (uint32_t *)(plan + o_tmap);
+  uint64_t *pst = (uint64_t *)(plan + o_pst);
+  uint64_t *tst = (uint64_t *)(plan + o_tst);
+  if (hipMemsetAsync(pst, 0, blocks * 8, s) != hipSuccess ||
+      hipMemsetAsync(tst, 0, tiles * 8, s) != hipSuccess ||
+      hipMemsetAsync(ctx->status, 0, tiles * 8, s) != hipSuccess)
+    return CPK_EDEVICE;
+  hipLaunchKernelGGL(cpk::tile_plan_kernel, dim3((unsigned)blocks), dim3(cpk::kPlanThreads), 0, s,
+                     d_swo, n, toff, tmap, tiles, pst, ctx->tickets + 2, ctx->tickets + 3);
   unsigned grid = (unsigned)(2 * ctx->cus);
-  if (grid > n) grid = n;
-  hipLaunchKernelGGL(cpk::encode_kernel<false>, dim3(grid), dim3(cpk::kEncThreads), cpk::kEncLds, s,
+  if (grid > tiles) grid = (unsigned)tiles;
+  hipLaunchKernelGGL(cpk::encode_kernel<true>, dim3(grid), dim3(cpk::kEncThreads), cpk::kEncLds, s,
                      (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
-                     ctx->tickets);
+                     ctx->tickets, (const uint32_t *)tmap, (const uint64_t *)toff, tst,
+                     ctx->tickets + 3);
   return hip_ok(hipGetLastError());
+}
+
+int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
+  if (!ctx) return CPK_EINVAL;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t e = 0;
+  if (hipMemcpyAsync(&e, ctx->tickets + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CPK_EDEVICE;
+  if (e && hipMemsetAsync(ctx->tickets + 3, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
+  return e ? CPK_EINVAL : CPK_OK;
 }
 
 int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off,
@@ -1236,6 +1572,8 @@ int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32
     goto done;
   }
   rc = cpk_encode_batch(ctx, d_in, d_swo, n, maxw, d_out, d_off, nullptr);
+  if (rc) goto done;
+  rc = cpk_ctx_take_error(ctx, nullptr);
   if (rc) goto done;
   if (hipMemcpy(h_out_off, d_off, (n + 1) * 8ull, hipMemcpyDeviceToHost)) {
     rc = CPK_EDEVICE;

@@ -77,11 +77,16 @@ void cpk_ctx_destroy(cpk_ctx ctx);
 int cpk_ctx_device(cpk_ctx ctx);
 
 /* Batch encode of n pieces, device-resident (replaces n calls of
- * PackedOutputStream.write, PackedOutputStream.java:35-205).
+ * PackedOutputStream.write, PackedOutputStream.java:35-205).  Pieces of any
+ * size: up to 8192 words one workgroup encodes a piece; larger pieces are cut
+ * into 8192-word tiles that carry the run state across tile boundaries.
  *   d_in            : 8-byte aligned words; piece i is words
  *                     [d_seg_word_off[i], d_seg_word_off[i+1]).
  *   d_seg_word_off  : uint64[n+1], device.
- *   max_seg_words   : host hint = max piece size in words (0 = unknown).
+ *   max_seg_words   : host bound on every piece's size in words; 0 = unknown
+ *                     (the call then reads d_seg_word_off[0], [n] back and
+ *                     synchronises `stream`).  A piece larger than the bound
+ *                     is reported by cpk_ctx_take_error (output undefined).
  *   d_out           : 16-byte aligned, capacity cpk_batch_packed_capacity().
  *   d_out_off       : uint64[n+1], device, written: piece i's packed bytes
  *                     are d_out[d_out_off[i] .. d_out_off[i+1]), contiguous
@@ -91,6 +96,11 @@ int cpk_ctx_device(cpk_ctx ctx);
 int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_seg_word_off,
                      uint32_t n, uint64_t max_seg_words, void *d_out,
                      uint64_t *d_out_off, void *stream);
+
+/* Synchronises `stream` and returns CPK_EINVAL if an encode issued since the
+ * last call met a piece larger than its max_seg_words bound, else CPK_OK
+ * (clears the flag).  The host forms below check it themselves. */
+int cpk_ctx_take_error(cpk_ctx ctx, void *stream);
 
 /* Batch decode of n pieces, device-resident (replaces n calls of
  * PackedInputStream.read, PackedInputStream.java:35-140).

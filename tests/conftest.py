@@ -4,7 +4,7 @@ from pathlib import Path
 import pytest
 
 REPO = Path(__file__).resolve().parents[1]
-for p in (REPO, REPO / "oracle", REPO / "capnproto-java_amd"):
+for p in (REPO, REPO / "oracle", REPO / "capnproto-java_amd", REPO / "tools"):
     if str(p) not in sys.path:
         sys.path.insert(0, str(p))
 

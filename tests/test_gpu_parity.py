@@ -231,3 +231,113 @@ def test_stream_decode_message(ctx, oracle):
     dec, bounds, st = ctx.decode_stream_host(np.frombuffer(bytes([17, 0, 127, 0, 0, 0, 0]), np.uint8),
                                              _swo([1, 127]))
     assert st[0] != 0 or st[1] != 0
+
+
+# ---- pieces larger than one 8192-word tile (tiled encoder) -----------------
+D8 = np.full(8, 7, np.uint8)
+L8 = np.array([0, 1, 2, 3, 4, 5, 6, 7], np.uint8)
+Z8 = np.zeros(8, np.uint8)
+
+
+def _runs_piece(rng, n):
+    """Long Z / D / L / D-L runs placed to cross tile boundaries."""
+    import tile_model
+    return np.frombuffer(tile_model.rand_piece(rng, n), np.uint8)
+
+
+def test_tiled_pieces_random(ctx, oracle):
+    rng = np.random.default_rng(21)
+    sizes = [8193, 16384, 16385, 20000, 8192 * 5 + 3, 70000] + list(rng.integers(8193, 60000, size=10))
+    sizes += [0, 5, 8192]
+    pieces = [_runs_piece(rng, int(s)) if s else np.zeros(0, np.uint8) for s in sizes]
+    data = np.concatenate(pieces)
+    _check_batch(ctx, oracle, data, _swo(sizes))
+
+
+def test_tiled_boundary_runs(ctx, oracle):
+    """Runs that start / end at, just before and just after tile boundaries,
+    whole tiles of one run (zero: phase carried; all-D: head distance
+    min(d, 256); D/L with L words: chain carried)."""
+    T = 8192
+    pieces = [
+        [Z8] * (5 * T + 17), [D8] * (4 * T + 300), [L8] * (3 * T + 1),
+        [L8] * (T - 100) + [D8] + [L8] * (2 * T), [D8] * (T - 1) + [L8] * (T + 5) + [D8] * (T + 7),
+        [Z8] * (T - 255) + [D8] * (T + 256) + [Z8] * (T + 257),
+        [L8] * (T - 256) + [D8] * 2 + [L8] * (T + 3),
+        [D8] * (T + 1), [Z8] * (T + 1), [Z8] * T + [D8] * T + [L8] * T + [Z8] * 3,
+        [L8] * (2 * T - 255) + [D8] + [L8] * 600,
+        [D8] * 100 + [Z8] * (2 * T) + [D8] * (T + 40),
+    ]
+    rng = np.random.default_rng(4)
+    for lead in (0, 1, 255, 256, 257):   # shift every boundary pattern
+        parts = [np.concatenate([rng.integers(1, 256, size=8 * lead, dtype=np.uint8)] + p) for p in pieces]
+        data = np.concatenate(parts)
+        _check_batch(ctx, oracle, data, _swo([len(p) // 8 for p in parts]))
+
+
+def test_config3_messages(ctx, oracle):
+    """messages of 4 segments of 4-256 KiB, dense
+    (<10 % zero words), each preceded by its segment-table piece."""
+    rng = np.random.default_rng(8)
+    sizes = []
+    for m in range(12):
+        segs = [int(rng.choice([512, 1024, 2048, 4096, 8192, 16384, 32768])) for _ in range(4)]
+        sizes += [3] + segs   # table: (4 segments) -> 1 + 4 u32 = 20 B -> 3 words
+    swo = _swo(sizes)
+    data = oracle.generate(oracle.preset(3), swo)
+    _check_batch(ctx, oracle, data, swo)
+
+
+def test_tiled_path_for_small_pieces(ctx, oracle):
+    """max_seg_words = 0 (unknown) takes the tiled path for any batch."""
+    import torch
+    rng = np.random.default_rng(12)
+    sizes = list(rng.integers(0, 20000, size=30)) + [8192, 1, 0]
+    swo = _swo(sizes)
+    data = oracle.generate(oracle.preset(2), swo)
+    d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
+    d_in = torch.from_numpy(np.concatenate([data, np.zeros(8, np.uint8)]).view(np.int64).copy()).cuda()
+    cap = batch_capacity_16(swo)
+    d_pk = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    d_off = torch.zeros(len(sizes) + 1, dtype=torch.int64, device="cuda")
+    ctx.encode_batch(d_in, d_swo, 0, d_pk, d_off)
+    assert ctx.take_error() == 0
+    opk, ooff = oracle.pack_batch(data, swo, threads=8)
+    off = d_off.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(off, ooff)
+    assert np.array_equal(d_pk[: int(off[-1])].cpu().numpy(), opk)
+
+
+def batch_capacity_16(swo):
+    import capnp_packed as cp
+    return (cp.batch_capacity(swo) + 15) // 16 * 16
+
+
+def test_wrong_size_hint_is_reported(ctx, oracle):
+    """A piece larger than max_seg_words: no fault, reported by take_error."""
+    import torch
+    import capnp_packed as cp
+    for sizes, hint in (([9000, 10], 100), ([30000, 10], 9000)):
+        swo = _swo(sizes)
+        d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
+        d_in = torch.ones(int(swo[-1]), dtype=torch.int64, device="cuda")
+        d_pk = torch.zeros(batch_capacity_16(swo), dtype=torch.uint8, device="cuda")
+        d_off = torch.zeros(len(sizes) + 1, dtype=torch.int64, device="cuda")
+        ctx.encode_batch(d_in, d_swo, hint, d_pk, d_off)
+        assert ctx.take_error() == cp.EINVAL
+        assert ctx.take_error() == cp.OK
+
+
+def test_short_stretch_after_long(ctx, oracle):
+    """A short D/L stretch whose 0xFF head lies within 255 words of a long
+    stretch's last head: the head is not a member of the other stretch's run
+    (PackedOutputStream.java:133-161 scan is per stretch)."""
+    pieces = []
+    for sep in ([Z8], [np.array([1, 0, 0, 2, 0, 3, 0, 0], np.uint8)]):
+        for gap in (0, 5, 100, 250):
+            p = [D8] * 300 + sep + [L8] * gap + [D8] + [L8] * 3 + sep + [D8] * 2
+            pieces.append(np.concatenate(p))
+            p = [L8] * 10 + [D8] * 700 + sep + [L8] * gap + [D8] * 3
+            pieces.append(np.concatenate(p))
+    data = np.concatenate(pieces)
+    _check_batch(ctx, oracle, data, _swo([len(p) // 8 for p in pieces]))

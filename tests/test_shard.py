@@ -1,0 +1,54 @@
+"""N>1 path without GPUs: shard planning and the timing reduction over gloo
+(world size 2), the same calls bench.py makes over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def test_plan_shards_balanced_by_bytes():
+    from capnp_packed.shard import plan_shards
+    sizes = np.array([512, 32768, 1024, 8192, 8192, 16384, 4, 0, 2048] * 50, dtype=np.uint64)
+    swo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    for world in (1, 2, 4, 8):
+        b = plan_shards(swo, world)
+        assert b[0] == 0 and b[-1] == len(sizes) and (np.diff(b) >= 0).all()
+        per = [int(swo[b[r + 1]] - swo[b[r]]) for r in range(world)]
+        assert sum(per) == int(swo[-1])
+        assert max(per) - min(per) <= 32768 + 1  # within one piece
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from capnp_packed.shard import reduce_max_sum
+    mx, sm = reduce_max_sum([1.0 + rank, 10.0 * rank])
+    dist.barrier()
+    q.put((rank, mx, sm))
+    dist.destroy_process_group()
+
+
+def test_reduce_over_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, mx, sm in got:
+        assert mx == [2.0, 10.0] and sm == [3.0, 10.0]
