@@ -160,12 +160,18 @@ def main():
     dom = "decode" if dec_ms >= enc_ms else "encode"
     dom_ms = max(enc_ms, dec_ms)
     achieved = (U + P) / (dom_ms * 1e-3) / 1e9
+    # HBM bytes per launch of the dominant kernel from the committed PMC
+    # passes (tools/profile.sh + tools/pmc_summary.py), when they were taken
+    # on this same workload
     traffic = None
     pmc = REPO / "profiles" / "pmc_traffic.json"
+    workload_key = f"config{args.config}:{n}x{sw}"
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get(dom)
-        except Exception:
+            t = json.loads(pmc.read_text())
+            if t.get("workload") == workload_key and dom in t:
+                traffic = int(t[dom]["hbm_bytes"])
+        except (ValueError, KeyError, TypeError):
             traffic = None
 
     cpu = None

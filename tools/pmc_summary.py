@@ -1,0 +1,53 @@
+"""Summarise rocprofv3 PMC passes (tools/profile.sh output) per kernel:
+mean counter value per dispatch of encode_kernel / decode_kernel, plus the
+HBM-traffic fields bench.py reads (FETCH_SIZE doubled on gfx950 and
+WRITE_SIZE, both in KB per rocprofv3 -> bytes).
+usage: python tools/pmc_summary.py gpurun_out/<tag> [--json out.json WORKLOAD]
+(WORKLOAD: the bench config string the passes ran, stored with the numbers so
+bench.py only reports traffic measured on its own workload)"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+root = Path(sys.argv[1])
+vals = defaultdict(lambda: defaultdict(list))
+for f in sorted(root.glob("*/*_counter_collection.csv")):
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            k = r["Kernel_Name"]
+            short = ("encode_kernel" if "encode_kernel" in k else "decode_kernel" if "decode_kernel" in k
+                     else k.split("(")[0][-40:])
+            vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+out = {}
+for kern in ("encode_kernel", "decode_kernel"):
+    if kern not in vals:
+        continue
+    d = {c: sum(v) / len(v) for c, v in vals[kern].items()}
+    out[kern] = d
+    print(kern)
+    for c in sorted(d):
+        print(f"  {c:24s} {d[c]:18.1f}")
+    if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d:
+        print(f"  VALU instr / wave      {d['SQ_INSTS_VALU'] / d['SQ_WAVES']:.0f}")
+        print(f"  SALU instr / wave      {d['SQ_INSTS_SALU'] / d['SQ_WAVES']:.0f}")
+        print(f"  LDS  instr / wave      {d['SQ_INSTS_LDS'] / d['SQ_WAVES']:.0f}")
+    if "SQ_WAVE_CYCLES" in d:
+        wc = d["SQ_WAVE_CYCLES"]
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+            if c in d:
+                print(f"  {c:22s} {100 * d[c] / wc:6.1f} % of wave cycles")
+if len(sys.argv) > 3 and sys.argv[2] == "--json":
+    traffic = {}
+    for kern, key in (("encode_kernel", "encode"), ("decode_kernel", "decode")):
+        d = out.get(kern, {})
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            # rocprofv3 reports KB; gfx950 FETCH_SIZE counts half the bytes of
+            # wide streaming reads (MI355X_MICROARCH.md HBM section)
+            traffic[key] = {"fetch_bytes": 2 * 1024 * d["FETCH_SIZE"], "write_bytes": 1024 * d["WRITE_SIZE"],
+                            "hbm_bytes": 2 * 1024 * d["FETCH_SIZE"] + 1024 * d["WRITE_SIZE"]}
+    traffic["workload"] = sys.argv[4] if len(sys.argv) > 4 else None
+    traffic["source"] = str(root)
+    Path(sys.argv[3]).write_text(json.dumps(traffic, indent=1))
+    print(json.dumps(traffic))
