@@ -1065,15 +1065,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       uint64_t onmask = 0;
       uint32_t entry = e;
       uint32_t enext;
-      // common case: every lane's walk lands in the next lane's chunk
-      const int na = (int)((wend - e + 31) >> 5);  // active lanes (chunks)
-      const bool ok = lane < na - 1 ? (S < wend && (int)((S - e) >> 5) == lane + 1)
-                                    : (lane == na - 1 ? S >= wend : true);
-      if (__ballot(!ok) == 0) {
-        onmask = na == 64 ? ~0ull : ((1ull << na) - 1);
-        entry = (uint32_t)wave_shr1((int)S, (int)e);
-        enext = (uint32_t)__builtin_amdgcn_readlane((int)S, na - 1);
-      } else {
+      {
         int cur = 0;
         for (;;) {
           onmask |= 1ull << cur;
@@ -1164,57 +1156,62 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
         }
         wave_lds_sync();
         const int nb = (min(min(kRound, T - rb), W - ow - rb) + 7) >> 3;
-        const bool al16 = (((uintptr_t)(dst + ow + rb)) & 15) == 0;  // uniform
         for (int b = lane; b < nb; b += 64) {
           const uint32_t v = blk[b];
           uint32_t q = e + (v & 0xffffu);
           int ofs = (int)(v >> 16);
           const int wbase = ow + rb + 8 * b;  // piece word of the block's first word
-          const int kw = min(8, min(ow + T, W) - wbase);
-          uint64_t *d = dst + wbase;
-          uint64_t prev = 0;
+          uint64_t words[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            // branch-free per word: the expansion LUT maps tag 0x00 to zero
-            // bytes and 0xFF to the identity, so one v_perm serves all three
-            // record kinds (PackedInputStream.java:84-134)
+            // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
+            // run (tag word, then the counted words), or a tagged word
             const uint32_t tag = pkw[q];
-            const bool z = tag == 0, f = tag == 0xffu;
-            const uint32_t c = pkw[q + (z ? 1u : 9u)];
-            const uint32_t cnt = (z || f) ? c : 0u;
-            const int nw = 1 + (int)cnt;
-            const uint32_t adv = z ? 2u : f ? 10u + 8u * cnt : 1u + __builtin_popcount(tag);
-            const uint32_t src = (f && ofs > 0) ? q + 10 + 8 * (uint32_t)(ofs - 1) : q + 1;
-            const uint64_t raw = read8(pkw, src, lend, gp);
-            const uint64_t sel = lut[tag];
-            const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
-            const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
-            const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
-            const uint64_t x = (uint64_t)x0 | ((uint64_t)x1 << 32);
-            // words go out as they are made: 16-byte stores of pairs when the
-            // round's output is 16-byte aligned (uniform), else 8-byte stores
-            if (al16) {
-              if (i & 1) {
-                if (i < kw) {
-                  uint4 v4;
-                  v4.x = (uint32_t)prev;
-                  v4.y = (uint32_t)(prev >> 32);
-                  v4.z = x0;
-                  v4.w = x1;
-                  *reinterpret_cast<uint4 *>(d + i - 1) = v4;
-                } else if (i - 1 < kw) {
-                  d[i - 1] = prev;
-                }
-              }
-              prev = x;
-            } else if (i < kw) {
-              d[i] = x;
+            uint64_t x;
+            int nw;
+            uint32_t adv;
+            if (tag == 0) {
+              x = 0;
+              nw = 1 + pkw[q + 1];
+              adv = 2;
+            } else if (tag == 0xffu) {
+              const uint32_t rn = pkw[q + 9];
+              nw = 1 + (int)rn;
+              adv = 10 + 8 * rn;
+              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp);
+            } else {
+              const uint64_t raw = read8(pkw, q + 1, lend, gp);
+              const uint64_t sel = lut[tag];
+              const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
+              const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
+              const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
+              x = (uint64_t)x0 | ((uint64_t)x1 << 32);
+              nw = 1;
+              adv = 1 + __builtin_popcount(tag);
             }
+            words[i] = x;
             // past the window's last word: stay put (never stored)
             if (++ofs == nw && wbase + i + 1 < ow + T) {
               q += adv;
               ofs = 0;
             }
+          }
+          const int kw = min(8, min(ow + T, W) - wbase);
+          uint64_t *d = dst + wbase;
+          if (kw == 8 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+              uint4 v4;
+              v4.x = (uint32_t)words[i];
+              v4.y = (uint32_t)(words[i] >> 32);
+              v4.z = (uint32_t)words[i + 1];
+              v4.w = (uint32_t)(words[i + 1] >> 32);
+              *reinterpret_cast<uint4 *>(d + i) = v4;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              if (i < kw) d[i] = words[i];
           }
         }
         wave_lds_sync();  // blk reused by the next round
