@@ -61,6 +61,37 @@ static_assert(kEncLut % 16 == 0, "lut must be aligned");
 static_assert(kEncLds <= 81920, "2 encoder workgroups per CU");
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// ---- ticket counters ------------------------------------------------------
+// One counter word saturates near 88 returning atomics per microsecond
+// (MI355X_MICROARCH.md, row "dequeue").  Work with no order dependence (the
+// decoder) is sharded per XCD: the k-th ticket taken from counter x is item
+// 8k + x, every item is taken exactly once, and a wave whose counter runs
+// dry moves on to the next counter, so coverage never depends on where the
+// waves were placed (the XCD id only picks the first counter).  Work whose
+// items depend on their predecessors (the encoders' look-back) keeps one
+// ordered counter.
+constexpr int kTkStride = 32;          // u32 words between counters (128 B)
+constexpr int kTkEnc = 0;              // encoder counters [8]
+constexpr int kTkDec = 8 * kTkStride;  // decoder counters [8]
+constexpr int kTkPlan = 16 * kTkStride;
+constexpr int kTkErr = 17 * kTkStride;
+constexpr int kTkWords = 18 * kTkStride;
+__device__ __forceinline__ int xcc_id() {
+  int x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7;
+}
+// all 64 lanes call it (one folded +64 atomic per wave); the wave's item
+__device__ __forceinline__ uint32_t take_ticket(uint32_t *ctr, int x) {
+  const uint32_t t = atomicAdd(&ctr[x * kTkStride], 1u);
+  return (((uint32_t)__builtin_amdgcn_readlane((int)t, 0) >> 6) << 3) | (uint32_t)x;
+}
+// ordered single-counter form
+__device__ __forceinline__ uint32_t take_ordered(uint32_t *ctr) {
+  const uint32_t t = atomicAdd(ctr, 1u);
+  return (uint32_t)__builtin_amdgcn_readlane((int)t, 0) >> 6;
+}
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
 // ------------------------------------------------------------ wave scans
@@ -119,11 +150,26 @@ __device__ unsigned long long g_phase[64];
 #define PH_FLUSH(base)                                                       \
   __syncthreads();                                                           \
   if (threadIdx.x < 16) atomicAdd(&g_phase[(base) + threadIdx.x], ph_acc[threadIdx.x]);
+// wave-level form (barrier-free kernels): per-wave sums, lane 0 flushes
+#define WPH_INIT                                                             \
+  unsigned long long wph_last = __builtin_amdgcn_s_memtime(), wph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define WPH(i)                                                               \
+  {                                                                          \
+    unsigned long long t_ = __builtin_amdgcn_s_memtime();                    \
+    wph_acc[i] += t_ - wph_last;                                             \
+    wph_last = t_;                                                           \
+  }
+#define WPH_FLUSH(base)                                                      \
+  if ((threadIdx.x & 63) == 0)                                               \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_phase[(base) + i_], wph_acc[i_]);
 #else
 #define PH_INIT(scr)
 #define PH(i)
 #define PH_ADD(i, v)
 #define PH_FLUSH(base)
+#define WPH_INIT
+#define WPH(i)
+#define WPH_FLUSH(base)
 #endif
 
 // nonzero-byte mask of a 32-bit half: bit b set iff byte b != 0
@@ -156,6 +202,14 @@ __device__ void fill_luts(uint64_t *lut, bool expand) {
     }
     lut[m] = v;
   }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // DS ops of one wave complete in order; this only stops the compiler
+  // moving LDS accesses across the point and drains this lane's queue.
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");  // re-read LDS after this point (no forwarding)
 }
 
 // ------------------------------------------------------------ look-back
@@ -205,6 +259,54 @@ __device__ uint64_t lb_resolve(uint64_t *status, uint32_t tile, uint64_t agg) {
     excl += val;
     if (first < 64) break;
     top -= 64;
+  }
+  if (lane == 0) st_status(&status[tile], kFlagInc | (excl + agg));
+  return excl;
+}
+
+// Wide form: each poll reads the 256 nearest predecessors (4 per lane), so
+// the inclusive-prefix frontier advances 256 items per memory round trip
+// instead of 64 -- the bound on items per second when thousands of waves
+// resolve at once.
+__device__ uint64_t lb_resolve_wide(uint64_t *status, uint32_t tile, uint64_t agg) {
+  const int lane = lane_id();
+  if (tile == 0) return 0;
+  uint64_t excl = 0;
+  int64_t top = (int64_t)tile - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    uint64_t v[4];
+    int fi = 4;  // first inclusive among this lane's four (nearest first)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t idx = top - 4 * lane - i;
+      v[i] = idx >= 0 ? ld_status(&status[idx]) : kFlagInc;
+    }
+#pragma unroll
+    for (int i = 3; i >= 0; --i)
+      if ((v[i] >> 62) == 2) fi = i;
+    const uint64_t has = __ballot(fi < 4);
+    const int fl = has ? __builtin_ctzll(has) : 64;
+    const int firstPos = fl < 64 ? 4 * fl + __builtin_amdgcn_readlane(fi, fl) : 256;
+    bool z = false;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pos = 4 * lane + i;
+      if (pos <= firstPos) {
+        z = z || (v[i] >> 62) == 0;
+        sum += v[i] & kValMask;
+      }
+    }
+    if (__ballot(z)) {
+      if (++spins > (1u << 24)) break;  // cannot happen with in-order tickets
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    excl += sum;
+    if (firstPos < 256) break;
+    top -= 256;
   }
   if (lane == 0) st_status(&status[tile], kFlagInc | (excl + agg));
   return excl;
@@ -320,12 +422,56 @@ __device__ int enc_chain_dist(const uint64_t *mks, int x, int W) {
   }
   return last >= 0 ? W - last : 0;
 }
+// Exit state of a full tile from its final run (start sF, -1 if the run
+// covers the whole tile; group gF) or 0 when it needs the entry state (a
+// tile-long D/L stretch with L words).  mks: per 64-word step {S, D} masks.
+__device__ uint64_t tile_exit_state(const uint64_t *mks, int W, int gF, int sF, bool allD) {
+  if (gF == 2) return kStLocal | (2ull << 32);
+  if (sF >= 0)
+    return kStLocal | ((uint64_t)gF << 32) |
+           (gF == 0 ? (uint64_t)((-sF) & 255) : (uint64_t)enc_chain_dist(mks, sF, W));
+  if (gF == 0) return kStPass;
+  if (allD) return kStPass | (1ull << 32);
+  return 0;
+}
+// Entry state by look-back over tstate (all 64 lanes of one wave): the
+// nearest LOCAL state before tau, PASS tiles composed on the way.  Returns
+// the Z phase (g0 == 0) or the D/L head distance (0 = none yet).
+__device__ uint32_t tile_entry_state(uint64_t *tstate, uint32_t tau, int g0) {
+  const int lane = lane_id();
+  int64_t top = (int64_t)tau - 1;
+  bool sawD = false;
+  uint64_t val = 0;
+  uint32_t spins = 0;
+  for (;;) {
+    const int64_t idx = top - lane;
+    const uint64_t v = idx >= 0 ? ld_status(&tstate[idx]) : kStLocal;
+    const uint64_t loc = __ballot((v >> 62) == 1);
+    const int first = loc ? __builtin_ctzll(loc) : 64;
+    const uint64_t rel = first >= 63 ? ~0ull : ((2ull << first) - 1);
+    if (__ballot((v >> 62) == 0) & rel) {
+      if (++spins > (1u << 24)) break;  // cannot happen with in-order tickets
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    sawD = sawD || __ballot(lane < first && ((v >> 32) & 1)) != 0;
+    if (first < 64) {
+      val = readlane64(v, first);
+      break;
+    }
+    top -= 64;
+  }
+  uint32_t x = (uint32_t)val;
+  if (g0 == 0) return x & 255;
+  if (sawD) x = (x == 0 || x > 256) ? 256u : x;
+  return x;
+}
+
 // wave 0, all lanes: publish this tile's exit state, resolve its entry state
 // into scr[69..71]
 __device__ void enc_tile_state(const uint64_t *mks, int *scr, uint64_t *tstate, uint32_t tau,
                                int j, int W, bool lastTile, int g0, int gm1) {
   const int lane = lane_id();
-  const int gF = scr[72];
   int sF = -1;
   bool allD = true;
   for (int q = 0; q < kEncWaves; ++q) {
@@ -334,52 +480,22 @@ __device__ void enc_tile_state(const uint64_t *mks, int *scr, uint64_t *tstate, 
   }
   uint64_t outv = 0;
   if (!lastTile) {
-    if (gF == 2) outv = kStLocal | (2ull << 32);
-    else if (sF >= 0)
-      outv = kStLocal | ((uint64_t)gF << 32) |
-             (gF == 0 ? (uint64_t)((-sF) & 255) : (uint64_t)enc_chain_dist(mks, sF, W));
-    else if (gF == 0) outv = kStPass;
-    else if (allD) outv = kStPass | (1ull << 32);
+    outv = tile_exit_state(mks, W, scr[72], sF, allD);
     if (outv && lane == 0) st_status(&tstate[tau], outv);
   }
   int rsIn = -1, hlIn = kNoHead, cont = 0;
   if (j > 0 && W > 0 && g0 == gm1) {
     cont = g0 + 1;
     if (g0 != 2) {
-      int64_t top = (int64_t)tau - 1;
-      bool sawD = false;
-      uint64_t val = 0;
-      uint32_t spins = 0;
-      for (;;) {
-        const int64_t idx = top - lane;
-        const uint64_t v = idx >= 0 ? ld_status(&tstate[idx]) : kStLocal;
-        const uint64_t loc = __ballot((v >> 62) == 1);
-        const int first = loc ? __builtin_ctzll(loc) : 64;
-        const uint64_t rel = first >= 63 ? ~0ull : ((2ull << first) - 1);
-        if (__ballot((v >> 62) == 0) & rel) {
-          if (++spins > (1u << 24)) break;  // cannot happen with in-order tickets
-          __builtin_amdgcn_s_sleep(2);
-          continue;
-        }
-        sawD = sawD || __ballot(lane < first && ((v >> 32) & 1)) != 0;
-        if (first < 64) {
-          val = readlane64(v, first);
-          break;
-        }
-        top -= 64;
-      }
-      const uint32_t x = (uint32_t)val;
+      const uint32_t x = tile_entry_state(tstate, tau, g0);
       if (g0 == 0) {
-        rsIn = -(int)(x & 255);
-        if (!lastTile && outv == kStPass && lane == 0)
-          st_status(&tstate[tau], kStLocal | (uint64_t)(x & 255));
+        rsIn = -(int)x;
+        if (!lastTile && outv == kStPass && lane == 0) st_status(&tstate[tau], kStLocal | (uint64_t)x);
       } else {
-        uint32_t dist = x;  // 0: no head yet in the stretch
-        if (sawD) dist = (dist == 0 || dist > 256) ? 256u : dist;
         rsIn = -kTileWords;  // forces the chain walk for the continued stretch
-        hlIn = dist ? -(int)dist : kNoHead;
+        hlIn = x ? -(int)x : kNoHead;
         if (!lastTile && (outv >> 62) == 2 && lane == 0)
-          st_status(&tstate[tau], kStLocal | (1ull << 32) | (uint64_t)((dist == 0 || dist > 256) ? 256u : dist));
+          st_status(&tstate[tau], kStLocal | (1ull << 32) | (uint64_t)((x == 0 || x > 256) ? 256u : x));
       }
     }
   }
@@ -829,12 +945,340 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
   PH_FLUSH(0)
 }
 
+// ------------------------------------------------------------ encoder v2
+// Wave-per-tile encoder: no workgroup barriers.  A wave takes the next tile
+// (1024 words of a piece, in stream order) from an ordered ticket and
+//   1. loads its words (one per lane per 64-word step) and classifies them:
+//      nonzero-byte mask, group, run-start / D ballots (a wave-private LDS
+//      row per step), plus a 256-word look-ahead for the end of the run
+//      crossing the tile end;
+//   2. publishes its exit run state (tile_exit_state) and, when its first
+//      run continues the previous tile's, resolves its entry state;
+//   3. walks the 16 steps in order with wave-uniform carries -- run start,
+//      last D, last 0xFF head of the current stretch -- and gives every word
+//      its role (PackedOutputStream.java:64-193 restated per word, see
+//      DESIGN.md): within one 64-word step a stretch that continues from
+//      before has at most one new head (heads are >= 256 words apart) and a
+//      stretch that starts in the step has its first D as head;
+//   4. publishes its packed size and resolves its output offset by
+//      decoupled look-back;
+//   5. builds each word's packed string (tag + v_perm-compacted bytes +
+//      count), ORs it into a 1 KiB wave-private LDS ring at its output
+//      offset, and streams complete 16-byte lines to memory; only the lines
+//      shared with the neighbouring tiles take byte stores.
+// Per-word state lives in LDS between the passes (rolled loops keep the
+// registers at <= 64 per lane).
+constexpr int kE2Words = 1024;                 // words per tile (multiple of 256)
+constexpr int kE2Steps = kE2Words / 64;        // 16
+constexpr int kE2Threads = 256;                // 4 independent waves
+constexpr uint32_t kE2Ring = 1024;             // output ring per wave (bytes)
+constexpr uint32_t kE2Info = kE2Ring;                      // u32[16][64] per-word roles
+constexpr uint32_t kE2Mks = kE2Info + kE2Words * 4;        // u64[16][2] {S, D}
+constexpr uint32_t kE2Nxs = kE2Mks + kE2Steps * 16;        // int[16] first start after step
+constexpr uint32_t kE2WaveLds = kE2Nxs + kE2Steps * 4;     // 5,440
+constexpr uint32_t kE2Lds = 2048 + 4 * kE2WaveLds;         // 23,808 B
+#ifndef CPK_E2_WPE
+#define CPK_E2_WPE 6  // LDS (23.8 KB per workgroup) allows 6 workgroups per CU
+#endif
+
+// stores bytes [lo, hi) of global line L from the ring, then clears them
+__device__ __forceinline__ void e2_store_partial(uint8_t *out, uint8_t *ring, uint64_t L, int lo,
+                                                 int hi) {
+  const int lane = lane_id();
+  if (lane >= lo && lane < hi) {
+    const uint32_t rp = (uint32_t)((L * 16 + lane) & (kE2Ring - 1));
+    out[L * 16 + lane] = ring[rp];
+    ring[rp] = 0;
+  }
+}
+
+__global__ __launch_bounds__(kE2Threads, CPK_E2_WPE) void encode2_kernel(
+    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
+    uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status,
+    uint32_t *ticket, const uint32_t *__restrict__ tmap, const uint64_t *__restrict__ toff,
+    uint64_t *tstate) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint64_t *lut = reinterpret_cast<uint64_t *>(smem);
+  const int lane = lane_id(), w = wave_id();
+  uint8_t *wl = smem + 2048 + w * kE2WaveLds;
+  uint8_t *ring = wl;
+  uint32_t *ring32 = reinterpret_cast<uint32_t *>(ring);
+  uint32_t *inf = reinterpret_cast<uint32_t *>(wl + kE2Info);  // [s * 64 + lane]
+  uint64_t *mks = reinterpret_cast<uint64_t *>(wl + kE2Mks);   // [2s] S, [2s+1] D
+  int *nxs = reinterpret_cast<int *>(wl + kE2Nxs);
+  fill_luts(lut, false);
+  for (int i = lane; i < (int)(kE2Ring / 16); i += 64)
+    reinterpret_cast<uint4 *>(ring)[i] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();  // the only block-wide barrier: LUT ready
+  const uint32_t T = (uint32_t)toff[n];
+  // ordered tickets; the next one is requested while the current tile runs
+  uint32_t tnext = take_ordered(ticket);
+  WPH_INIT
+  for (;;) {
+    const uint32_t tau = tnext;
+    if (tau >= T) break;
+    tnext = take_ordered(ticket);
+    const uint32_t seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)tmap[tau]);
+    const int j = (int)(tau - (uint32_t)toff[seg]);
+    const uint64_t p0 = swo[seg], pw = swo[seg + 1] - p0;
+    const uint64_t tb = (uint64_t)j * kE2Words, rem = pw - tb;
+    const int W = rem < (uint64_t)kE2Words ? (int)rem : kE2Words;
+    const bool lastTile = rem <= (uint64_t)kE2Words;
+    const int rl = (int)min(rem - (uint64_t)W, (uint64_t)256);  // look-ahead words
+    const uint64_t *src = in + p0 + tb;
+    int k0 = lane;
+    asm volatile("" : "+v"(k0));  // keep per-lane addresses out of the loop head
+    const int kl = max(W - 1, 0);
+    WPH(0)
+
+    // ---- 1: loads, classes, ballots ----------------------------------------
+    int gm1 = 3;  // group of the word before the tile (3: none)
+    if (j > 0) {
+      const uint64_t v = src[-1];
+      gm1 = grp_of(word_mask((uint32_t)v, (uint32_t)(v >> 32)));
+    }
+    int gprev = gm1, sF = -1;
+    bool allD = true;
+    {
+      uint64_t wv[kE2Steps];
+#pragma unroll
+      for (int s = 0; s < kE2Steps; ++s) wv[s] = W ? src[min(k0 + 64 * s, kl)] : 0ull;
+#pragma unroll
+      for (int s = 0; s < kE2Steps; ++s) {
+        const int k = k0 + 64 * s;
+        const uint64_t v = k < W ? wv[s] : 0ull;
+        const uint32_t m = word_mask((uint32_t)v, (uint32_t)(v >> 32));
+        const int g = k < W ? grp_of(m) : 3;
+        const uint64_t S = __ballot(g != 3 && g != wave_shr1(g, gprev));
+        const uint64_t D = __ballot(k < W && m == 0xffu);
+        if (lane == 0) {
+          mks[2 * s] = S;
+          mks[2 * s + 1] = D;
+        }
+        allD = allD && D == ~0ull;
+        if (S) sF = 64 * s + hi_bit(S);
+        gprev = readlane(g, 63);
+        inf[64 * s + lane] = m | ((uint32_t)g << 8);
+      }
+    }
+    const int gF = gprev;  // group of word 1023 (full tiles)
+    int look = W;          // first run start after the tile, capped 256 on
+    if (!lastTile) {
+      uint64_t la[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) la[r] = src[W + min(64 * r + k0, rl - 1)];
+      look = W + 256;
+      int gp = gprev;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int g = 64 * r + lane < rl ? grp_of(word_mask((uint32_t)la[r], (uint32_t)(la[r] >> 32))) : 3;
+        const uint64_t b = __ballot(g != wave_shr1(g, gp));
+        if (b && look == W + 256) look = W + 64 * r + lo_bit(b);
+        gp = readlane(g, 63);
+      }
+    }
+    wave_lds_sync();
+    // nxs[s] := first run start after step s
+    if (lane == 0) {
+      int r = look;
+      for (int s = kE2Steps - 1; s >= 0; --s) {
+        nxs[s] = r;
+        const uint64_t S = mks[2 * s];
+        if (S) r = 64 * s + lo_bit(S);
+      }
+    }
+
+    // ---- 2: exit state out, entry state in ----------------------------------
+    WPH(1)
+    uint64_t outv = 0;
+    if (!lastTile) {
+      outv = tile_exit_state(mks, W, gF, sF, allD);
+      if (outv && lane == 0) st_status(&tstate[tau], outv);
+    }
+    const int g0 = __builtin_amdgcn_readfirstlane((int)inf[0]) >> 8 & 3;
+    const bool cont = j > 0 && W > 0 && g0 == gm1;
+    int rsC = 0, hC = kNoHead;  // run start / last 0xFF head before the step
+    if (cont && g0 != 2) {
+      const uint32_t x = tile_entry_state(tstate, tau, g0);
+      if (g0 == 0) {
+        rsC = -(int)x;
+        if (!lastTile && outv == kStPass && lane == 0) st_status(&tstate[tau], kStLocal | (uint64_t)x);
+      } else {
+        hC = x ? -(int)x : kNoHead;
+        if (!lastTile && (outv >> 62) == 2 && lane == 0)
+          st_status(&tstate[tau], kStLocal | (1ull << 32) | (uint64_t)((x == 0 || x > 256) ? 256u : x));
+      }
+    }
+    if (!lastTile && !outv) {
+      outv = kStLocal | (1ull << 32) | (uint64_t)enc_chain_dist(mks, max(hC + 256, 0), W);
+      if (lane == 0) st_status(&tstate[tau], outv);
+    }
+    wave_lds_sync();
+
+    // ---- 3: roles (PackedOutputStream.java:64-193 per word) -----------------
+    WPH(2)
+    const uint64_t le = lanemask_le(), lt = le >> 1;
+    int gC = gm1, rdC = -kBig, total = 0;
+#pragma unroll 1
+    for (int s = 0; s < kE2Steps; ++s) {
+      const int base = 64 * s;
+      const int k = k0 + base;
+      const uint64_t S = mks[2 * s], D = mks[2 * s + 1];
+      const int nx = nxs[s];
+      const uint32_t x = inf[base + lane];
+      const uint32_t m = x & 0xffu;
+      const int g = (int)((x >> 8) & 3);
+      const int fst = S ? lo_bit(S) : 64;  // first run start in the step
+      // the D/L stretch continuing into the step: its new head, if any, is
+      // the first D at or after hC + 256 before the step's first run start
+      int hNew = kNoHead;
+      if (gC == 1 && fst > 0) {
+        const int t0 = hC == kNoHead ? 0 : max(hC + 256 - base, 0);
+        if (t0 < fst) {
+          const uint64_t sg = (fst == 64 ? ~0ull : ((1ull << fst) - 1)) & (~0ull << t0);
+          const uint64_t c = D & sg;
+          if (c) hNew = base + lo_bit(c);
+        }
+      }
+      const uint64_t sle = S & le, sgt = S & ~le, dlt = D & lt;
+      const int rs = sle ? base + hi_bit(sle) : rsC;
+      const int re = sgt ? base + lo_bit(sgt) : nx;
+      const int rd = dlt ? base + hi_bit(dlt) : rdC;
+      uint32_t flags = 0;
+      int nb = 0;
+      if (g == 0) {
+        // a 0x00 head every 256 words of a zero run (the 255 cap, :119-131)
+        if (((k - rs) & 255) == 0) {
+          flags = 1u << 11;
+          nb = 2;
+        }
+      } else if (g == 1) {
+        bool mem;
+        if (lane < fst) {  // stretch continuing from before the step
+          mem = k != hNew && ((hC != kNoHead && k <= hC + 255) || (hNew != kNoHead && k > hNew));
+        } else {           // stretch started in this step: its first D heads
+          mem = rd >= rs;
+        }
+        flags = mem ? (1u << 10) : 0u;
+        nb = mem ? 8 : (m == 0xffu ? 10 : 8);
+      } else if (g == 2) {
+        nb = 1 + __builtin_popcount(m);
+      }
+      const uint32_t cnt = (uint32_t)min(255, max(re - k - 1, 0));
+      inf[base + lane] = m | flags | ((uint32_t)nb << 12) | (cnt << 16);
+      total += __popcll(__ballot(nb & 1)) + 2 * __popcll(__ballot(nb & 2)) +
+               4 * __popcll(__ballot(nb & 4)) + 8 * __popcll(__ballot(nb & 8));
+      // carries into the next step
+      const int gL = readlane(g, 63);
+      if (gL == 1) {
+        if (S) {
+          const uint64_t dm = D & (~0ull << hi_bit(S));
+          hC = dm ? base + lo_bit(dm) : kNoHead;
+        } else if (hNew != kNoHead) {
+          hC = hNew;
+        }
+      } else {
+        hC = kNoHead;
+      }
+      if (S) rsC = base + hi_bit(S);
+      if (D) rdC = base + hi_bit(D);
+      gC = gL;
+    }
+
+    // ---- 4: output offset by look-back --------------------------------------
+    WPH(3)
+    if (lane == 0) lb_publish(status, tau, (uint64_t)total);
+    const uint64_t obase = lb_resolve(status, tau, (uint64_t)total);
+    if (lane == 0) {
+      if (j == 0) out_off[seg] = obase;
+      if (tau == T - 1) out_off[n] = obase + (uint64_t)total;
+    }
+    wave_lds_sync();
+
+    // ---- 5: strings -> LDS ring -> 16-byte lines ---------------------------
+    WPH(4)
+    const int pad = (int)(obase & 15);
+    const uint64_t L0 = obase >> 4;
+    uint64_t fl = (obase + 15) >> 4;  // next whole line to store
+    bool headDone = pad == 0;
+    int off = 0;
+    // the words again (L2 / Infinity-Cache hits: the tile was read moments
+    // ago), one step ahead
+    uint64_t vn = W ? src[min(k0, kl)] : 0ull;
+#pragma unroll 1
+    for (int s = 0; s < kE2Steps; ++s) {
+      const uint64_t v = vn;
+      if (s + 1 < kE2Steps) vn = W ? src[min(k0 + 64 * (s + 1), kl)] : 0ull;
+      const uint32_t x = inf[64 * s + lane];
+      const int nb = (int)((x >> 12) & 15u);
+      const int incl = wave_incl_add(nb);
+      const int o = off + incl - nb;
+      off += readlane(incl, 63);
+      if (nb) {
+        const uint32_t l = (uint32_t)v, h = (uint32_t)(v >> 32), m = x & 0xffu;
+        uint32_t d0, d1, d2;
+        if (x & (1u << 10)) {  // literal-run member: 8 bytes verbatim
+          d0 = l;
+          d1 = h;
+          d2 = 0;
+        } else {  // tag + nonzero bytes (+ count after 0x00 / 0xFF tags)
+          const uint64_t sel = lut[m];
+          const uint32_t c0 = __builtin_amdgcn_perm(h, l, (uint32_t)sel);
+          const uint32_t c1 = __builtin_amdgcn_perm(h, l, (uint32_t)(sel >> 32));
+          const uint32_t cnt = (x >> 16) & 0xffu;
+          d0 = m | (c0 << 8);
+          d1 = (c0 >> 24) | (c1 << 8);
+          d2 = c1 >> 24;
+          if (m == 0) d0 |= cnt << 8;
+          else if (m == 0xffu) d2 |= cnt << 8;
+        }
+        const uint32_t rp = (uint32_t)((obase + (uint64_t)o) & (kE2Ring - 1));
+        const uint32_t sh = (rp & 3) * 8u;
+        const uint64_t s01 = (uint64_t)d0 | ((uint64_t)d1 << 32);
+        const uint64_t lo64 = s01 << sh;
+        const uint64_t hi64 = ((uint64_t)d2 << sh) | (sh ? (s01 >> (64 - sh)) : 0ull);
+        const uint32_t q = rp >> 2;
+        const int end = (int)(rp & 3) + nb;
+        constexpr uint32_t kMask = kE2Ring / 4 - 1;
+        atomicOr(&ring32[q], (uint32_t)lo64);
+        if (end > 4) atomicOr(&ring32[(q + 1) & kMask], (uint32_t)(lo64 >> 32));
+        if (end > 8) atomicOr(&ring32[(q + 2) & kMask], (uint32_t)hi64);
+        if (end > 12) atomicOr(&ring32[(q + 3) & kMask], (uint32_t)(hi64 >> 32));
+      }
+      wave_lds_sync();
+      if (!headDone && off >= 16 - pad) {
+        e2_store_partial(out, ring, L0, pad, 16);
+        headDone = true;
+      }
+      const uint64_t le16 = (obase + (uint64_t)off) >> 4;  // lines below are complete
+      for (uint64_t L = fl + (uint64_t)lane; L < le16; L += 64) {
+        uint4 *rl4 = reinterpret_cast<uint4 *>(ring + ((L * 16) & (kE2Ring - 1)));
+        *reinterpret_cast<uint4 *>(out + L * 16) = *rl4;
+        *rl4 = uint4{0u, 0u, 0u, 0u};
+      }
+      if (le16 > fl) fl = le16;
+      wave_lds_sync();
+    }
+    // the tail line (shared with the next tile) and a head line never filled
+    const uint64_t done = obase + (uint64_t)total;
+    if (!headDone) {
+      if (total) e2_store_partial(out, ring, L0, pad, pad + total);
+    } else if (done & 15) {
+      e2_store_partial(out, ring, done >> 4, 0, (int)(done & 15));
+    }
+    wave_lds_sync();
+    WPH(5)
+  }
+  WPH_FLUSH(32)
+}
+
 // Tile plan for the tiled encoder: toff[i] = first tile of piece i (one tile
 // per 8192 words, at least one per piece), toff[n] = T, tmap[tau] = piece of
 // tile tau.  Single pass: 8192 pieces per workgroup, in ticket order, block
 // prefixes by look-back.  Tiles beyond `cap` (a wrong max_seg_words hint) are
 // reported in *err and not planned.
 constexpr int kPlanThreads = 1024, kPlanPer = 8;
+template <int kTW>
 __global__ __launch_bounds__(kPlanThreads) void tile_plan_kernel(
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ toff,
     uint32_t *__restrict__ tmap, uint64_t cap, uint64_t *pstatus, uint32_t *ticket,
@@ -855,7 +1299,7 @@ __global__ __launch_bounds__(kPlanThreads) void tile_plan_kernel(
     c[q] = 0;
     if (i < n) {
       const uint64_t pw = swo[i + 1] - swo[i];
-      c[q] = pw == 0 ? 1 : (int)((pw + kTileWords - 1) / kTileWords);
+      c[q] = pw == 0 ? 1 : (int)((pw + kTW - 1) / kTW);
     }
     t += c[q];
   }
@@ -922,12 +1366,6 @@ __device__ __forceinline__ int wave_min(int v) {
   for (int d = 32; d >= 1; d >>= 1) v = min(v, __shfl_xor(v, d, 64));
   return v;
 }
-__device__ __forceinline__ void wave_lds_sync() {
-  // DS ops of one wave complete in order; this only stops the compiler
-  // moving LDS accesses across the point and drains this lane's queue.
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-  __builtin_amdgcn_wave_barrier();
-}
 
 // record length in bytes of the record whose tag is at piece position q
 __device__ __forceinline__ uint32_t rec_len(const uint8_t *pkw, uint32_t q) {
@@ -985,6 +1423,8 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
   fill_luts(lut, true);
   __syncthreads();  // the only block-wide barrier: LUT ready
   if (kStream && (blockIdx.x != 0 || w != 0)) return;
+  int xq = xcc_id(), dry = 0;
+  WPH_INIT
   uint64_t scur = 0;      // stream mode: start of the next piece
   int sfail = CPK_OK;     // stream mode: a failed piece stops the stream
 
@@ -994,12 +1434,13 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
     // All 64 lanes add 1 (hipcc folds it into one +64 atomic): no lane-0-only
     // branch at the loop head, which hipcc otherwise structurised into a
     // divergent loop re-running piece 0.  Tickets count in units of 64.
-    uint32_t seg;
-    if (kStream) {
-      seg = sidx;
-    } else {
-      const uint32_t tk = atomicAdd(ticket, 1u);
-      seg = (uint32_t)__builtin_amdgcn_readlane((int)tk, 0) >> 6;
+    uint32_t seg = sidx;
+    if (!kStream) {
+      for (;;) {
+        seg = take_ticket(ticket, xq);
+        if (seg < n || ++dry >= 8) break;
+        xq = (xq + 1) & 7;  // this counter ran dry: help the next one
+      }
     }
     if (seg >= n) break;
     const uint64_t w0 = swo[seg];
@@ -1024,6 +1465,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       }
       if (ow >= W) break;  // (trailing input is flagged by the record check)
       const uint32_t wend = min(e + kWin, P);
+      WPH(0)
       // ---- window load: LDS byte x <-> packed[(a + e) & ~15 + x] ----------
       const uint32_t padw = (uint32_t)((a + e) & 15);
       const uint32_t ebase = e - padw;  // piece position of wbuf[0]
@@ -1038,6 +1480,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       const uint8_t *pkw = wbuf + (int64_t)padw - (int64_t)e;
       wave_lds_sync();
 
+      WPH(1)
       // ---- 1: speculative chunk walks --------------------------------------
       const uint32_t cb = e + 32 * lane;
       const uint32_t ce = min(cb + 32, wend);
@@ -1061,6 +1504,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
           S += rec_len(pkw, S);
         }
       }
+      WPH(2)
       // ---- 3: true chain over lanes (scalar) --------------------------------
       uint64_t onmask = 0;
       uint32_t entry = e;
@@ -1080,6 +1524,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
         }
       }
       const bool on = (onmask >> lane) & 1;
+      WPH(3)
       // ---- 4: output words of each lane's true records ----------------------
       int myw = 0;
       if (on) {
@@ -1101,6 +1546,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       const int inc = wave_incl_add(myw);
       const int T = readlane(inc, 63);
       const int o0 = inc - myw;  // window-relative output of this lane's first record
+      WPH(4)
       // ---- 5: error checks, block map, expansion (rounds of 2048 words) -----
       bool failed = false;
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
@@ -1155,6 +1601,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
           fin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u(fin));
         }
         wave_lds_sync();
+        WPH(5)
         const int nb = (min(min(kRound, T - rb), W - ow - rb) + 7) >> 3;
         for (int b = lane; b < nb; b += 64) {
           const uint32_t v = blk[b];
@@ -1215,6 +1662,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
           }
         }
         wave_lds_sync();  // blk reused by the next round
+        WPH(6)
       }
       if (failed) break;
       if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
@@ -1233,6 +1681,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       if (seg == n - 1) in_off[n] = scur;
     }
   }
+  WPH_FLUSH(16)
 }
 
 // ------------------------------------------------------------ bench support
@@ -1304,9 +1753,10 @@ struct cpk_ctx_s {
   int cus;
   uint64_t *status;       // look-back words
   uint64_t status_cap;    // entries
-  uint32_t *tickets;      // [0] encode, [1] decode, [2] tile plan, [3] error bits
+  uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
   void *plan;             // tiled encode: toff | tmap | pstatus | tstate
   uint64_t plan_cap;      // bytes
+  int encoder;            // 1: workgroup-per-piece encoder (default); 2: wave-per-tile
 };
 
 namespace {
@@ -1397,9 +1847,16 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
   cpk_ctx c = (cpk_ctx)calloc(1, sizeof(cpk_ctx_s));
   if (!c) return CPK_ENOMEM;
   c->device = device;
+  {
+    // CPK_ENCODER=2 selects the wave-per-tile encoder (experimental: its
+    // per-1024-word look-back does not scale yet)
+    const char *e = getenv("CPK_ENCODER");
+    c->encoder = (e && e[0] == '2') ? 2 : 1;
+  }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
-  if (hipMalloc(&c->tickets, 16) != hipSuccess) {
+  if (hipMalloc(&c->tickets, cpk::kTkWords * 4) != hipSuccess ||
+      hipMemset(c->tickets, 0, cpk::kTkWords * 4) != hipSuccess) {
     free(c);
     return CPK_ENOMEM;
   }
@@ -1407,6 +1864,8 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
                           hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kEncLds) != hipSuccess ||
       hipFuncSetAttribute((const void *)cpk::encode_kernel<true>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kEncLds) != hipSuccess ||
+      hipFuncSetAttribute((const void *)cpk::encode2_kernel,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kE2Lds) != hipSuccess ||
       hipFuncSetAttribute((const void *)cpk::decode_kernel<false>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess) {
     hipFree(c->tickets);
@@ -1435,8 +1894,10 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
-  if (hipMemsetAsync(ctx->tickets, 0, 16, s) != hipSuccess) return CPK_EDEVICE;
-  if (max_seg_words != 0 && max_seg_words <= (uint64_t)cpk::kTileWords) {
+  // counters (not the error word: that is cleared by cpk_ctx_take_error)
+  if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
+  const bool v2 = ctx->encoder == 2;
+  if (!v2 && max_seg_words != 0 && max_seg_words <= (uint64_t)cpk::kTileWords) {
     // one workgroup per piece
     int rc = ensure_status(ctx, n);
     if (rc) return rc;
@@ -1446,21 +1907,23 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
     hipLaunchKernelGGL(cpk::encode_kernel<false>, dim3(grid), dim3(cpk::kEncThreads), cpk::kEncLds,
                        s, (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
                        ctx->tickets, (const uint32_t *)nullptr, (const uint64_t *)nullptr,
-                       (uint64_t *)nullptr, ctx->tickets + 3);
+                       (uint64_t *)nullptr, ctx->tickets + cpk::kTkErr);
     return hip_ok(hipGetLastError());
   }
-  // tiled: pieces cut into 8192-word tiles; the tile count is bounded from the
-  // hint, or from the batch's word count when there is no hint
+  // tiled: pieces cut into tiles (1024 words for the wave-per-tile encoder,
+  // 8192 for the workgroup one); the tile count is bounded from the hint, or
+  // from the batch's word count when there is no hint
+  const uint64_t tw = v2 ? (uint64_t)cpk::kE2Words : (uint64_t)cpk::kTileWords;
   uint64_t tiles;
   if (max_seg_words) {
-    tiles = (uint64_t)n * ((max_seg_words + cpk::kTileWords - 1) / cpk::kTileWords);
+    tiles = (uint64_t)n * ((max_seg_words + tw - 1) / tw);
   } else {
     uint64_t ends[2];
     if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
       return CPK_EDEVICE;
-    tiles = (uint64_t)n + (ends[1] - ends[0]) / cpk::kTileWords;
+    tiles = (uint64_t)n + (ends[1] - ends[0]) / tw;
   }
   const uint64_t blocks = ((uint64_t)n + cpk::kPlanThreads * cpk::kPlanPer - 1) /
                           (cpk::kPlanThreads * cpk::kPlanPer);
@@ -1481,14 +1944,27 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
       hipMemsetAsync(tst, 0, tiles * 8, s) != hipSuccess ||
       hipMemsetAsync(ctx->status, 0, tiles * 8, s) != hipSuccess)
     return CPK_EDEVICE;
-  hipLaunchKernelGGL(cpk::tile_plan_kernel, dim3((unsigned)blocks), dim3(cpk::kPlanThreads), 0, s,
-                     d_swo, n, toff, tmap, tiles, pst, ctx->tickets + 2, ctx->tickets + 3);
+  if (v2) {
+    hipLaunchKernelGGL(cpk::tile_plan_kernel<cpk::kE2Words>, dim3((unsigned)blocks),
+                       dim3(cpk::kPlanThreads), 0, s, d_swo, n, toff, tmap, tiles, pst,
+                       ctx->tickets + cpk::kTkPlan, ctx->tickets + cpk::kTkErr);
+    // persistent: 6 workgroups of 4 independent waves per CU
+    unsigned grid = (unsigned)(6 * ctx->cus);
+    if (grid > (tiles + 3) / 4) grid = (unsigned)((tiles + 3) / 4);
+    hipLaunchKernelGGL(cpk::encode2_kernel, dim3(grid), dim3(cpk::kE2Threads), cpk::kE2Lds, s,
+                       (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
+                       ctx->tickets, (const uint32_t *)tmap, (const uint64_t *)toff, tst);
+    return hip_ok(hipGetLastError());
+  }
+  hipLaunchKernelGGL(cpk::tile_plan_kernel<cpk::kTileWords>, dim3((unsigned)blocks),
+                     dim3(cpk::kPlanThreads), 0, s, d_swo, n, toff, tmap, tiles, pst,
+                     ctx->tickets + cpk::kTkPlan, ctx->tickets + cpk::kTkErr);
   unsigned grid = (unsigned)(2 * ctx->cus);
   if (grid > tiles) grid = (unsigned)tiles;
   hipLaunchKernelGGL(cpk::encode_kernel<true>, dim3(grid), dim3(cpk::kEncThreads), cpk::kEncLds, s,
                      (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
                      ctx->tickets, (const uint32_t *)tmap, (const uint64_t *)toff, tst,
-                     ctx->tickets + 3);
+                     ctx->tickets + cpk::kTkErr);
   return hip_ok(hipGetLastError());
 }
 
@@ -1497,10 +1973,10 @@ int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   uint32_t e = 0;
-  if (hipMemcpyAsync(&e, ctx->tickets + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+  if (hipMemcpyAsync(&e, ctx->tickets + cpk::kTkErr, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return CPK_EDEVICE;
-  if (e && hipMemsetAsync(ctx->tickets + 3, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
+  if (e && hipMemsetAsync(ctx->tickets + cpk::kTkErr, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
   return e ? CPK_EINVAL : CPK_OK;
 }
 
@@ -1512,13 +1988,14 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   if (n == 0) return CPK_OK;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(ctx->tickets + 1, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
+  if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
+    return CPK_EDEVICE;
   // persistent: 8 blocks of 4 independent waves per CU (32 pieces in flight)
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (n + 3) / 4) grid = (n + 3) / 4;
   hipLaunchKernelGGL(cpk::decode_kernel<false>, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
                      (const uint8_t *)d_packed, const_cast<uint64_t *>(d_in_off), d_swo, n,
-                     (uint64_t *)d_out, d_status, ctx->tickets + 1, (uint64_t)0);
+                     (uint64_t *)d_out, d_status, ctx->tickets + cpk::kTkDec, (uint64_t)0);
   return hip_ok(hipGetLastError());
 }
 
@@ -1531,7 +2008,7 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
   DeviceGuard g(ctx->device);
   hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds,
                      (hipStream_t)stream, (const uint8_t *)d_packed, d_in_off, d_swo, n,
-                     (uint64_t *)d_out, d_status, ctx->tickets + 1, avail);
+                     (uint64_t *)d_out, d_status, ctx->tickets + cpk::kTkDec, avail);
   return hip_ok(hipGetLastError());
 }
 

@@ -31,15 +31,16 @@ ctx.encode_batch(d_in, d_swo, 8192, d_pk, d_off)
 ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
 torch.cuda.synchronize()
 L.cpk_debug_phase_stats(buf.ctypes.data)
-enames = ["ticket", "load+classify", "roles", "long chains", "offsets+zero",
-          "strings->LDS", "look-back", "store"]
-dnames = ["ticket", "stage packed", "first walk", "resolve loop", "clear bits",
-          "offsets+errors", "blk map", "expand+store"]
-for title, base, names in (("encode", 0, enames), ("decode", 16, dnames)):
-    v = buf[base:base + len(names)].astype(float)
-    tot = v.sum()
-    print(f"{title}: total {tot / 1e6:.1f} Mcycles over all WGs; per piece {tot / n:.0f} cyc")
-    for nm, x in zip(names, v):
-        print(f"   {nm:22s} {100 * x / tot:6.2f} %   {x / n:8.0f} cyc/piece")
-print("decode resolve iterations per piece:", buf[16 + 9] / n)
+e2names = ["ticket+setup", "load+classify", "exit/entry state", "roles", "look-back", "strings+store"]
+v = buf[32:32 + len(e2names)].astype(float)
+tot = v.sum()
+print(f"encode2: total {tot / 1e6:.1f} Mcycles over all waves; per piece {tot / n:.0f} cyc")
+for nm, x in zip(e2names, v):
+    print(f"   {nm:22s} {100 * x / max(tot, 1):6.2f} %   {x / n:8.0f} cyc/piece")
+dnames = ["ticket+piece", "window load", "chunk walks", "lane chain", "count walk", "errors+blk map", "expand+store"]
+v = buf[16:16 + len(dnames)].astype(float)
+tot = v.sum()
+print(f"decode: total {tot / 1e6:.1f} Mcycles over all waves; per piece {tot / n:.0f} cyc")
+for nm, x in zip(dnames, v):
+    print(f"   {nm:22s} {100 * x / max(tot, 1):6.2f} %   {x / n:8.0f} cyc/piece")
 print("P/U =", int(d_off[-1].item()) / (8.0 * n * 8192), "bad status", int((d_st != 0).sum().item()))

@@ -21,11 +21,15 @@ d_out = torch.empty_like(d_in)
 d_st = torch.empty(n, dtype=torch.int32, device="cuda")
 cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
 handles = []
-for lp in libs:
+import os
+for spec in libs:
+    # "lib.so@1": context created with CPK_ENCODER=1 (workgroup-per-piece encoder)
+    lp, _, enc = spec.partition("@")
+    os.environ["CPK_ENCODER"] = enc or "1"
     cp._lib = None
     L = cp.load(Path(lp), strict=False)
     ctx = cp.Context(0)
-    handles.append((Path(lp).name, L, ctx))
+    handles.append((Path(lp).name + (f"@{enc}" if enc else ""), L, ctx))
 for cfg in cfgs:
     cp._lib = handles[0][1]
     handles[0][2].generate(cp.preset(cfg), d_swo, d_in)
@@ -36,6 +40,7 @@ for cfg in cfgs:
             cp._lib = L
             ctx._lib = L
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ctx._lib = L
             e[0].record(); ctx.encode_batch(d_in, d_swo, hint, d_pk, d_off); e[1].record()
             ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st); e[2].record()
             torch.cuda.synchronize()
