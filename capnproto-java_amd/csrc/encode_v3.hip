@@ -1,0 +1,620 @@
+// encode_v3.hip -- included by packed_codec.hip inside namespace cpk.
+//
+// Workgroup-per-tile encoder.  The batch's words [swo[0], swo[n]) are cut
+// into fixed tiles of kE3TileWords consecutive words regardless of where the
+// pieces start: a piece start is a run boundary inside a tile
+// (PackedOutputStream.java:36-43 re-initialises all run state per write()).
+// A 256-thread workgroup encodes one tile in three phases:
+//   1. each wave loads its 16 steps of 64 words (lane = word), computes every
+//      word's nonzero-byte tag and keeps words and tags in registers; the tags
+//      also go to LDS (one byte per word) for the other waves, and the last
+//      wave classifies up to 4 steps past the tile to find where the run
+//      crossing its end stops (the counts need it);
+//   2. each wave derives the run state entering its first word from the tags
+//      before it -- or, when the tile's first run continues the previous
+//      tile's, from that tile's published exit state -- then walks its steps
+//      with wave-uniform carries and gives every word its role
+//      (PackedOutputStream.java:119-193 restated per word):
+//      run boundaries, 0x00 heads every 256 words of a zero run, 0xFF heads
+//      and literal-run members by a carry-propagate add over the D and D/L
+//      masks (a D/L stretch longer than 256 words walks the head chain), and
+//      the packed size of every word;
+//   3. after a decoupled look-back over the tile totals has given the tile's
+//      output offset, each wave builds every word's packed string (tag +
+//      v_perm-compacted bytes + count), ORs it into a 2 KiB LDS ring at its
+//      output position and streams complete 16-byte lines to memory.
+// Tiles are dealt round-robin to a persistent grid that fits on the device
+// at once, so every tile a workgroup waits on is being worked on.
+// tools/e3_model.py is this algorithm at mask level on the CPU.
+
+constexpr int kE3Waves = 4;
+constexpr int kE3Threads = 64 * kE3Waves;
+constexpr int kE3Steps = 16;                             // 64-word steps per wave
+constexpr int kE3WaveWords = 64 * kE3Steps;              // 1024
+constexpr int kE3TileWords = kE3Waves * kE3WaveWords;    // 4096
+constexpr int kE3La = 4;                                 // look-ahead steps
+constexpr int kE3Rows = kE3Waves * kE3Steps + kE3La;     // 68 step rows
+constexpr uint32_t kE3RingBytes = 2048;                  // output ring per wave
+constexpr uint32_t kE3RingLines = kE3RingBytes / 16;
+constexpr uint32_t kE3RingDw = kE3RingBytes / 4;
+// LDS byte offsets.  The tile's words stay in LDS between the phases so the
+// step loops can stay rolled (a fully unrolled tile overflows the registers
+// and the instruction cache).
+constexpr uint32_t kE3oWords = 0;                                  // u64[4096] the tile
+constexpr uint32_t kE3oLut = kE3oWords + 8 * kE3TileWords;         // u64[256]
+constexpr uint32_t kE3oRing = kE3oLut + 2048;                      // u32[waves][512]
+constexpr uint32_t kE3oTag = kE3oRing + kE3Waves * kE3RingBytes;   // u8[rows][64]
+constexpr uint32_t kE3oPs = kE3oTag + kE3Rows * 64;                // u64[rows] piece starts
+constexpr uint32_t kE3oB = kE3oPs + kE3Rows * 8;                   // u64[rows] run boundaries
+constexpr uint32_t kE3oHd = kE3oB + kE3Rows * 8;                   // u64[rows] heads
+constexpr uint32_t kE3oMb = kE3oHd + kE3Rows * 8;                  // u64[rows] run members
+constexpr uint32_t kE3oScr = kE3oMb + kE3Rows * 8;                 // int[64]
+constexpr uint32_t kE3Lds = kE3oScr + 256;
+static_assert(kE3oPs % 8 == 0 && kE3oRing % 16 == 0, "LDS alignment");
+
+#ifndef CPK_E3_WPE
+#define CPK_E3_WPE 4
+#endif
+
+// Look-back words: [63:48] launch epoch, [47:46] flag (1 aggregate,
+// 2 inclusive prefix), [45:0] value.  A word from another launch reads as
+// "not published", so the arrays need no clearing between launches.
+constexpr uint64_t kE3ValMask = (1ull << 46) - 1;
+__device__ __forceinline__ uint64_t e3_word(uint32_t ep, uint32_t flag, uint64_t v) {
+  return ((uint64_t)ep << 48) | ((uint64_t)flag << 46) | (v & kE3ValMask);
+}
+__device__ __forceinline__ uint32_t e3_flag(uint64_t w, uint32_t ep) {
+  return (uint32_t)(w >> 48) == ep ? (uint32_t)(w >> 46) & 3u : 0u;
+}
+
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// bit `lane` of a wave-uniform mask: one v_cndmask on the SGPR pair
+__device__ __forceinline__ uint32_t lanebit(uint64_t mask) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(r) : "s"(mask));
+  return r;
+}
+
+// Run state at a word position: the run the word would continue.
+//   g   0 zero run, 1 D/L stretch (words with <= 1 zero byte), 2 none
+//   len words of the run before the position (zero runs: only len mod 256
+//       matters, the 0x00 heads are every 256 words from the run start)
+//   hd  D/L stretch: words since its last 0xFF head, capped at 256; 0 = no
+//       head yet (PackedOutputStream.java:143-161: a head's run takes the
+//       next <= 255 words of the stretch)
+struct E3St {
+  int g, len, hd;
+};
+// tile exit states: [63:48] epoch, [46] valid, [33:32] g, [31:20] hd, [19:0] len
+__device__ __forceinline__ uint64_t e3_st_pack(uint32_t ep, E3St s) {
+  const uint32_t len = s.g == 0 ? (uint32_t)(s.len & 255) : (uint32_t)min(s.len, (1 << 20) - 1);
+  return ((uint64_t)ep << 48) | (1ull << 46) | ((uint64_t)(s.g & 3) << 32) |
+         ((uint64_t)(s.hd & 0xfff) << 20) | len;
+}
+__device__ __forceinline__ E3St e3_st_unpack(uint64_t w) {
+  E3St s;
+  s.g = (int)(w >> 32) & 3;
+  s.hd = (int)(w >> 20) & 0xfff;
+  s.len = (int)(w & 0xfffff);
+  return s;
+}
+
+// nonzero-byte tag of a word (PackedOutputStream.java:64-117): bit i set iff
+// byte i != 0.  SWAR: bit 7 of every byte of t = byte != 0, gathered by shifts.
+__device__ __forceinline__ uint32_t e3_tag(uint64_t v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t tl = ((lo & 0x7f7f7f7fu) + 0x7f7f7f7fu) | lo;
+  const uint32_t th = ((hi & 0x7f7f7f7fu) + 0x7f7f7f7fu) | hi;
+  const uint32_t y = ((tl >> 7) & 0x01010101u) | ((th >> 3) & 0x10101010u);
+  return (y | (y >> 7) | (y >> 14) | (y >> 21)) & 0xffu;
+}
+// 0 = Z (all-zero word), 1 = D/L (<= 1 zero byte), 2 = M
+__device__ __forceinline__ int e3_grp(uint32_t m) {
+  return m == 0 ? 0 : (__builtin_popcount(m) >= 7 ? 1 : 2);
+}
+
+// state entering tile t from tile t-1's published exit state (one wave)
+__device__ E3St e3_tile_entry(const uint64_t *tstate, uint32_t t, uint32_t ep, uint32_t *err,
+                              int lane) {
+  uint32_t spins = 0;
+  for (;;) {
+    const uint64_t v = uni64(ld_status(const_cast<uint64_t *>(&tstate[t - 1])));
+    if ((uint32_t)(v >> 48) == ep) return e3_st_unpack(v);
+    if (++spins > (1u << 22)) {  // cannot happen with a co-resident grid
+      if (lane == 0) atomicOr(err, 2u);
+      E3St s = {2, 0, 0};
+      return s;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// first D word (tag 0xff) at tile position >= x and < lim, else lim
+__device__ int e3_first_d(const uint8_t *tagrow, int x, int lim, int lane) {
+  for (int r = x >> 6; r * 64 < lim; ++r) {
+    const int p = r * 64 + lane;
+    const uint64_t b = __ballot(p >= x && p < lim && tagrow[p] == 0xffu);
+    if (b) return r * 64 + __builtin_ctzll(b);
+  }
+  return lim;
+}
+
+// State entering tile position wp (> 0, a multiple of 64): the run holding
+// word wp - 1, from the tag rows; a run reaching back to the tile's first
+// word continues from the previous tile's exit state.  All 64 lanes.
+__device__ E3St e3_state_at(const uint8_t *tagrow, const uint64_t *psrow, int wp,
+                            const uint64_t *tstate, uint32_t t, uint32_t ep, uint32_t *err,
+                            int lane) {
+  E3St s = {2, 0, 0};
+  const int g = e3_grp((uint32_t)uni((int)tagrow[wp - 1]));
+  if (g == 2) return s;
+  // run start: after the last word of another group, or at the last piece start
+  int rs = -1;
+  for (int r = (wp - 1) >> 6; r >= 0; --r) {
+    const uint64_t other = __ballot(e3_grp(tagrow[r * 64 + lane]) != g);
+    const uint64_t ps = uni64(psrow[r]);
+    int c = -1;
+    if (other) c = r * 64 + 64 - __builtin_clzll(other);
+    if (ps) c = max(c, r * 64 + 63 - __builtin_clzll(ps));
+    if (c >= 0) {
+      rs = c;
+      break;
+    }
+  }
+  bool before = false;
+  if (rs < 0) {  // reaches the tile's first word, which is no piece start
+    rs = 0;
+    if (t > 0) {
+      const E3St tin = e3_tile_entry(tstate, t, ep, err, lane);
+      if (tin.g == g) {
+        before = true;
+        s = tin;
+      }
+    }
+  }
+  if (g == 0) {
+    s.g = 0;
+    s.len = (before ? s.len : 0) + (wp - rs);
+    s.hd = 0;
+    return s;
+  }
+  // D/L stretch: its 0xFF head chain from rs (PackedOutputStream.java:143-161):
+  // the first D is a head, then the first D at least 256 words after a head
+  const int len0 = before ? s.len : 0;
+  bool hasH = before && s.hd > 0;
+  int h = hasH ? -s.hd : 0;
+  for (;;) {
+    const int from = hasH ? max(h + 256, rs) : rs;
+    if (from >= wp) break;
+    const int d = e3_first_d(tagrow, from, wp, lane);
+    if (d >= wp) break;
+    h = d;
+    hasH = true;
+  }
+  s.g = 1;
+  s.len = len0 + (wp - rs);
+  s.hd = hasH ? min(wp - h, 256) : 0;
+  return s;
+}
+
+// Decoupled look-back over the tile totals (one wave, all lanes): publishes
+// the aggregate, returns the exclusive prefix, publishes the inclusive one.
+// Each poll reads the 256 nearest predecessors.
+__device__ uint64_t e3_lookback(uint64_t *status, uint32_t t, uint64_t agg, uint32_t ep,
+                                uint32_t *err, int lane) {
+  if (lane == 0) st_status(&status[t], e3_word(ep, t == 0 ? 2u : 1u, agg));
+  if (t == 0) return 0;
+  uint64_t excl = 0;
+  int64_t top = (int64_t)t - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    uint64_t v[4];
+    uint32_t fl[4];
+    int fi = 4;  // first inclusive among this lane's four (nearest first)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t idx = top - 4 * lane - i;
+      v[i] = idx >= 0 ? ld_status(&status[idx]) : e3_word(ep, 2u, 0);
+      fl[i] = e3_flag(v[i], ep);
+    }
+#pragma unroll
+    for (int i = 3; i >= 0; --i)
+      if (fl[i] == 2) fi = i;
+    const uint64_t has = __ballot(fi < 4);
+    const int fln = has ? __builtin_ctzll(has) : 64;
+    const int firstPos = fln < 64 ? 4 * fln + __builtin_amdgcn_readlane(fi, fln) : 256;
+    bool z = false;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (4 * lane + i <= firstPos) {
+        z = z || fl[i] == 0;
+        sum += v[i] & kE3ValMask;
+      }
+    }
+    if (__ballot(z)) {
+      if (++spins > (1u << 22)) {  // cannot happen with a co-resident grid
+        if (lane == 0) atomicOr(err, 2u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    excl += sum;
+    if (firstPos < 256) break;
+    top -= 256;
+  }
+  if (lane == 0) st_status(&status[t], e3_word(ep, 2u, excl + agg));
+  return excl;
+}
+
+// bytes [j0, j1) of global line L from the ring, then clears the ring line
+__device__ __forceinline__ void e3_store_bytes(uint8_t *out, uint32_t *ring, uint64_t L, int j0,
+                                               int j1, int lane) {
+  uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kE3RingLines - 1));
+  const uint4 val = *rl;
+  if (lane >= j0 && lane < j1) {
+    const uint32_t d = (lane & 8) ? ((lane & 4) ? val.w : val.z) : ((lane & 4) ? val.y : val.x);
+    out[L * 16 + lane] = (uint8_t)(d >> (8 * (lane & 3)));
+  }
+  wave_lds_sync();
+  if (lane == 0) *rl = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// stores the complete lines [fl, upto) of the ring; bytes below `lo` belong
+// to the previous wave / tile (only the wave's first line can hold them)
+__device__ __forceinline__ void e3_flush(uint8_t *out, uint32_t *ring, uint64_t &fl, uint64_t upto,
+                                         uint64_t lo, int lane) {
+  if (fl >= upto) return;
+  if (fl * 16 < lo) {
+    e3_store_bytes(out, ring, fl, (int)(lo - fl * 16), 16, lane);
+    ++fl;
+  }
+  for (uint64_t L0 = fl; L0 < upto; L0 += 64) {
+    const uint64_t L = L0 + lane;
+    if (L < upto) {
+      uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kE3RingLines - 1));
+      const uint4 val = *rl;
+      *rl = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4 *>(out + L * 16) = val;
+    }
+  }
+  fl = upto;
+}
+
+// tfirst[t] = first piece i with swo[i] >= swo[0] + t * kE3TileWords
+// (n + 1 if none), t in [0, nt + 1], nt = min(tiles of the batch, ntb).
+// Also checks the size hint; an empty batch gets all-zero piece offsets.
+__global__ void e3_plan_kernel(const uint64_t *__restrict__ swo, uint32_t n, uint32_t ntb,
+                               uint32_t *tfirst, uint64_t *out_off, uint64_t hint, uint32_t *err) {
+  const uint64_t base = swo[0], N = swo[n];
+  uint64_t nt = (N - base + kE3TileWords - 1) / kE3TileWords;
+  if (nt > ntb) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 1u);
+    nt = ntb;
+  }
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i <= (uint64_t)n + 1;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    if (N == base) {
+      if (i <= n) out_off[i] = 0;
+      if (i <= 1) tfirst[i] = 0;
+      continue;
+    }
+    uint64_t lo = 0, hi = 0;
+    if (i > 0) {
+      const uint64_t prev = swo[i - 1];
+      lo = (prev - base) / kE3TileWords + 1;
+      hi = i <= n ? (swo[i] - base) / kE3TileWords : nt + 1;
+      if (i <= n && hint && swo[i] - prev > hint) atomicOr(err, 1u);
+    }
+    if (hi > nt + 1) hi = nt + 1;
+    for (uint64_t t = lo; t <= hi; ++t) tfirst[t] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(kE3Threads, CPK_E3_WPE) void encode3_kernel(
+    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n, uint32_t ntb,
+    const uint32_t *__restrict__ tfirst, uint8_t *__restrict__ out, uint64_t *__restrict__ out_off,
+    uint64_t *status, uint64_t *tstate, uint32_t ep, uint32_t *err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kE3oLut);
+  uint8_t *tagrow = smem + kE3oTag;
+  uint64_t *psrow = reinterpret_cast<uint64_t *>(smem + kE3oPs);
+  uint64_t *brow = reinterpret_cast<uint64_t *>(smem + kE3oB);
+  uint64_t *hdrow = reinterpret_cast<uint64_t *>(smem + kE3oHd);
+  uint64_t *mbrow = reinterpret_cast<uint64_t *>(smem + kE3oMb);
+  uint64_t *words = reinterpret_cast<uint64_t *>(smem + kE3oWords);
+  int *scr = reinterpret_cast<int *>(smem + kE3oScr);
+  // the wave index through readfirstlane: hipcc's divergence analysis treats
+  // threadIdx.x >> 6 as divergent, which would turn every wave-uniform branch
+  // below into an exec-masked one
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(wave_id());
+  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kE3oRing + w * kE3RingBytes);
+  fill_luts(lut, false);
+  for (uint32_t i = lane_id(); i < kE3RingLines; i += 64)
+    reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
+  const uint64_t base = swo[0], N = swo[n];
+  uint32_t nt = (uint32_t)((N - base + kE3TileWords - 1) / kE3TileWords);
+  if (nt > ntb) nt = ntb;  // (reported by the plan kernel)
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    // tile position of the wave's first word, opaque per tile for the same
+    // reason as the lane id below (per-step row offsets hoisted into SGPRs)
+    int wb = w * kE3WaveWords;
+    asm volatile("" : "+s"(wb));
+    // an opaque copy of the lane id per tile: hipcc otherwise hoists ~100
+    // per-lane addresses and masks out of the tile loop and spills them
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const uint64_t gtm = lane == 63 ? 0ull : (~0ull << (lane + 1));  // lanes above this one
+    const uint64_t T0 = base + (uint64_t)t * kE3TileWords;
+    const uint64_t rem = N - T0;
+    const int TW = rem < (uint64_t)kE3TileWords ? (int)rem : kE3TileWords;    // words of the tile
+    const int pN = rem < (uint64_t)(kE3Rows * 64) ? (int)rem : kE3Rows * 64;  // batch end
+    // ---- phase 0: piece-start rows, boundary rows ---------------------------
+    __syncthreads();  // the previous tile's LDS reads are done
+    if (tid < kE3Rows) {
+      psrow[tid] = 0;
+      brow[tid] = 0;
+    }
+    __syncthreads();
+    {
+      const uint32_t p0 = tfirst[t], p2 = tfirst[min(t + 2, nt + 1)];
+      for (uint32_t i = p0 + tid; i < p2; i += kE3Threads) {
+        const uint64_t k = swo[i] - T0;
+        if (k < (uint64_t)pN)
+          atomicOr(reinterpret_cast<unsigned long long *>(&psrow[k >> 6]), 1ull << (k & 63));
+      }
+      if (tid == 0 && pN < kE3Rows * 64)  // the end of the batch ends every run
+        atomicOr(reinterpret_cast<unsigned long long *>(&brow[pN >> 6]), 1ull << (pN & 63));
+    }
+    // ---- phase 1: load, tag ------------------------------------------------
+    uint32_t mlast;  // tag of the wave's last word
+    {
+      const uint64_t *src = in + T0;
+      uint64_t v[kE3Steps];
+#pragma unroll
+      for (int s = 0; s < kE3Steps; ++s) {
+        const int k = wb + 64 * s + lane;
+        const uint64_t x = src[min(k, TW - 1)];
+        v[s] = k < TW ? x : 0ull;
+      }
+#pragma unroll
+      for (int s = 0; s < kE3Steps; ++s) {
+        const uint32_t m = e3_tag(v[s]);
+        words[wb + 64 * s + lane] = v[s];
+        tagrow[wb + 64 * s + lane] = (uint8_t)m;
+        mlast = m;
+      }
+    }
+    __syncthreads();  // B1: tags and piece starts of the whole tile
+    if (w == kE3Waves - 1 && TW == kE3TileWords && pN > kE3TileWords) {
+      // look-ahead: boundaries of up to kE3La steps past the tile, until the
+      // run crossing the tile end stops (counts are capped at 255 words)
+      int gprev = e3_grp((uint32_t)__builtin_amdgcn_readlane((int)mlast, 63));
+      for (int r = 0; r < kE3La; ++r) {
+        const int k = kE3TileWords + 64 * r + lane;
+        const bool ok = k < pN;
+        const uint64_t x = in[T0 + (uint64_t)min(k, pN - 1)];
+        const int g = ok ? e3_grp(e3_tag(x)) : 3;
+        const int gp = wave_shr1(g, gprev);
+        const uint64_t ps = uni64(psrow[kE3Waves * kE3Steps + r]);
+        const uint64_t b = __ballot(ok && (g != gp || g == 2)) | ps | __ballot(k == pN);
+        if (lane == 0) brow[kE3Waves * kE3Steps + r] = b;
+        gprev = __builtin_amdgcn_readlane(g, 63);
+        if (b) break;
+      }
+    }
+    // ---- phase 2: roles and sizes ------------------------------------------
+    const bool active = wb < TW;
+    int wtot = 0;
+    if (active) {
+      E3St st = {2, 0, 0};
+      if (w == 0) {
+        if (!(uni64(psrow[0]) & 1) && t > 0) st = e3_tile_entry(tstate, t, ep, err, lane);
+      } else {
+        st = e3_state_at(tagrow, psrow, wb, tstate, t, ep, err, lane);
+      }
+#pragma unroll 1
+      for (int s = 0; s < kE3Steps; ++s) {
+        const int kb = wb + 64 * s;
+        const int k = kb + lane;
+        const bool valid = k < TW;
+        const uint32_t m = tagrow[k];
+        const uint32_t pop = (uint32_t)__builtin_popcount(m);
+        const uint64_t Z = __ballot(valid && m == 0), D = __ballot(m == 0xffu),
+                       DL = __ballot(pop >= 7), V = __ballot(valid);
+        const uint64_t PS = uni64(psrow[kb >> 6]);
+        const uint64_t M = V & ~(Z | DL);
+        const uint64_t cz = st.g == 0 ? 1ull : 0ull, cdl = st.g == 1 ? 1ull : 0ull;
+        // run boundaries: piece starts, group changes, every M word
+        const uint64_t B = (PS & V) | (Z & ~((Z << 1) | cz)) | (DL & ~((DL << 1) | cdl)) | M;
+        const uint64_t BV = B | ~V;  // (past the batch's end no run continues)
+        const int f = BV ? __builtin_ctzll(BV) : 64;  // words [0, f) continue the carried run
+        // 0x00 heads: zero-run starts, and every 256th word of the carried run (:125-127)
+        uint64_t ZH = Z & B;
+        if (st.g == 0) {
+          const int j0 = (256 - (st.len & 255)) & 255;
+          if (j0 < f) ZH |= 1ull << j0;
+        }
+        // literal-run members: a D earlier in the same D/L stretch (carry of
+        // D + DL: generate at D, propagate through D/L, killed at boundaries)
+        const uint64_t kil = ~(B >> 1);
+        const uint64_t G = D & kil, P = DL & kil;
+        const uint64_t cin = (st.g == 1 && st.hd > 0 && !(B & 1)) ? 1ull : 0ull;
+        const uint64_t cc = (G + P + cin) ^ G ^ P;
+        uint64_t MEMB = DL & cc;
+        uint64_t DH = D & ~MEMB;
+        int h1 = -1;
+        if (st.g == 1 && st.len + f > 256) {
+          // the carried stretch is longer than 256 words: members lie within
+          // 255 words of a head, the next head is the first D 256 or more
+          // words after the last (:143-161)
+          const uint64_t rng = f >= 64 ? ~0ull : ((1ull << f) - 1);
+          uint64_t mc = 0;
+          if (st.hd > 0 && st.hd <= 255) {
+            const int me = 255 - st.hd;
+            mc = me >= 63 ? ~0ull : ((2ull << me) - 1);
+          }
+          const int js = st.hd > 0 ? max(0, 256 - st.hd) : 0;
+          const uint64_t dc = js >= 64 ? 0ull : (D & rng & (~0ull << js));
+          if (dc) {
+            h1 = __builtin_ctzll(dc);
+            mc |= h1 == 63 ? 0ull : (~0ull << (h1 + 1));
+          }
+          MEMB = (MEMB & ~rng) | (mc & DL & rng);
+          DH = (DH & ~rng) | (h1 >= 0 ? (1ull << h1) : 0ull);
+        }
+        const uint64_t HD = ZH | DH;
+        const uint32_t q = 1 + pop;
+        const uint64_t q0 = __ballot(q & 1) & M, q1 = __ballot(q & 2) & M, q2 = __ballot(q & 4) & M;
+        wtot += 8 * __popcll(DL) + 2 * __popcll(HD) + __popcll(q0) + 2 * __popcll(q1) +
+                4 * __popcll(q2);
+        if (lane == 0) {
+          hdrow[kb >> 6] = HD;
+          mbrow[kb >> 6] = MEMB;
+        }
+        const uint64_t bend = __ballot(k == pN);
+        if (lane == 0) brow[kb >> 6] = B | bend;
+        // the run state entering the next step
+        if (B) {
+          const int lb = 63 - __builtin_clzll(B);
+          st.g = ((Z >> lb) & 1) ? 0 : (((DL >> lb) & 1) ? 1 : 2);
+          st.len = 64 - lb;
+          st.hd = 0;
+          if (st.g == 1) {
+            const uint64_t dd = D & (~0ull << lb);
+            st.hd = dd ? 64 - __builtin_ctzll(dd) : 0;
+          }
+        } else if (st.g != 2) {
+          st.len += 64;
+          if (st.g == 1) {
+            if (h1 >= 0) st.hd = 64 - h1;
+            else if (st.hd > 0) st.hd = min(st.hd + 64, 256);
+            else st.hd = D ? 64 - __builtin_ctzll(D) : 0;
+          }
+        }
+      }
+      // the tile's exit state, for the next tile's first run
+      if (w == kE3Waves - 1 && lane == 0) st_status(&tstate[t], e3_st_pack(ep, st));
+    }
+    if (lane == 0) scr[w] = wtot;
+    __syncthreads();  // B2: sizes and boundary rows of every wave
+    if (w == 0) {
+      uint64_t tot = 0;
+      for (int q = 0; q < kE3Waves; ++q) tot += (uint32_t)scr[q];
+      const uint64_t excl = e3_lookback(status, t, tot, ep, err, lane);
+      if (lane == 0) {
+        *reinterpret_cast<uint64_t *>(&scr[8]) = excl;
+        if (T0 + (uint64_t)TW == N)  // pieces starting at the end of the batch (and swo[n])
+          for (int64_t j = n; j >= 0 && swo[j] == N; --j) out_off[j] = excl + tot;
+      }
+    }
+    __syncthreads();  // B3: the tile's output offset
+    // ---- phase 3: packed strings -> ring -> memory -------------------------
+    if (active) {
+      uint64_t obase = *reinterpret_cast<const uint64_t *>(&scr[8]);
+      for (int q = 0; q < w; ++q) obase += (uint32_t)scr[q];
+      uint64_t rpos = obase;     // output offset of the next string
+      uint64_t fl = obase >> 4;  // first line not stored yet
+      int nbrRow = -1, nbr = 0;  // first boundary in the rows after nbrRow
+      const uint32_t pfirst = tfirst[t], plast = tfirst[t + 1];
+#pragma unroll 1
+      for (int s = 0; s < kE3Steps; ++s) {
+        const int kb = wb + 64 * s;
+        const int k = kb + lane;
+        const uint32_t m = tagrow[k];
+        const uint64_t word = words[k];
+        const uint32_t pop = (uint32_t)__builtin_popcount(m);
+        const uint32_t isDL = pop >= 7 ? 1u : 0u, isM = (m != 0 && pop < 7 && k < TW) ? 1u : 0u;
+        const uint32_t isH = lanebit(uni64(hdrow[kb >> 6]));
+        const uint32_t isMb = lanebit(uni64(mbrow[kb >> 6]));
+        // packed size: M words 1 + popcount, D/L 8, heads + 2 (Z heads 2,
+        // D heads 10; M words are never heads)
+        const uint32_t nb = ((1 + pop) & (0u - isM)) + (isDL << 3) + (isH << 1);
+        const uint64_t b0 = __ballot(nb & 1), b1 = __ballot(nb & 2), b2 = __ballot(nb & 4),
+                       b3 = __ballot(nb & 8);
+        const uint32_t o = (uint32_t)(mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2) + 8 * mbcnt(b3));
+        const uint32_t stot = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) +
+                                         8 * __popcll(b3));
+        uint32_t cnt = 0;
+        if (__ballot(isH)) {
+          // a head's count: words to the run's end, at most 255 (:123-131, :143-164)
+          const int row = kb >> 6;
+          if (nbrRow != row) {
+            nbrRow = row;
+            nbr = kE3Rows * 64;
+            for (int r = row + 1; r < kE3Rows; ++r) {
+              const uint64_t br = uni64(brow[r]);
+              if (br) {
+                nbr = r * 64 + __builtin_ctzll(br);
+                break;
+              }
+            }
+          }
+          const uint64_t bb = uni64(brow[row]) & gtm;
+          const int re = bb ? kb + __builtin_ctzll(bb) : nbr;
+          cnt = isH ? (uint32_t)min(255, re - k - 1) : 0u;
+        }
+        const uint32_t lo = (uint32_t)word, hi = (uint32_t)(word >> 32);
+        const uint64_t sel = lut[m];
+        const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
+        const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+        const uint32_t c0p = m == 0 ? cnt : c0;
+        uint32_t s0 = m | (c0p << 8);
+        uint32_t s1 = __builtin_amdgcn_alignbyte(c1, c0p, 3);
+        uint32_t s2 = __builtin_amdgcn_alignbyte(m == 0xffu ? cnt : 0u, c1, 3);
+        if (isMb) {  // literal-run member: the word verbatim (:163-171)
+          s0 = lo;
+          s1 = hi;
+          s2 = 0;
+        }
+        // OR the string into the ring at its output offset
+        const uint32_t p = (uint32_t)rpos + o;
+        const uint32_t sh = (p & 3) * 8;
+        const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
+        const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
+        const uint32_t w3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
+        const uint32_t d0 = (p >> 2) & (kE3RingDw - 1);
+        const uint32_t end = (p & 3) + nb;
+        if (nb) atomicOr(&ring[d0], (uint32_t)a01);
+        if (end > 4) {
+          uint32_t *dp = &ring[(d0 + 1) & (kE3RingDw - 1)];
+          if (end >= 8) *dp = (uint32_t)(a01 >> 32);
+          else atomicOr(dp, (uint32_t)(a01 >> 32));
+        }
+        if (end > 8) {
+          uint32_t *dp = &ring[(d0 + 2) & (kE3RingDw - 1)];
+          if (end >= 12) *dp = (uint32_t)(a12 >> 32);
+          else atomicOr(dp, (uint32_t)(a12 >> 32));
+        }
+        if (end > 12) atomicOr(&ring[(d0 + 3) & (kE3RingDw - 1)], w3);
+        // piece offsets: out_off of every piece starting at this word
+        const uint64_t ps = uni64(psrow[kb >> 6]);
+        if (ps && ((ps >> lane) & 1)) {
+          const uint64_t gk = T0 + (uint64_t)(kb + lane);
+          uint32_t lo_i = pfirst, hi_i = plast;  // first piece with swo >= gk
+          while (lo_i < hi_i) {
+            const uint32_t mid = (lo_i + hi_i) >> 1;
+            if (swo[mid] < gk) lo_i = mid + 1;
+            else hi_i = mid;
+          }
+          for (uint32_t j = lo_i; j <= n && swo[j] == gk; ++j) out_off[j] = rpos + o;
+        }
+        rpos += stot;
+        wave_lds_sync();
+        e3_flush(out, ring, fl, rpos >> 4, obase, lane);
+      }
+      // the wave's last, partial line
+      if (rpos > fl * 16) {
+        const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
+        e3_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane);
+      }
+    }
+  }
+}

@@ -1745,6 +1745,8 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
 }
 
+#include "encode_v3.hip"
+
 }  // namespace cpk
 
 // ================================================================ C ABI
@@ -1756,7 +1758,13 @@ struct cpk_ctx_s {
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
   void *plan;             // tiled encode: toff | tmap | pstatus | tstate
   uint64_t plan_cap;      // bytes
-  int encoder;            // 1: workgroup-per-piece encoder (default); 2: wave-per-tile
+  int encoder;            // 3: workgroup-per-tile encoder (default); 1, 2: earlier encoders
+  uint32_t *e3_tfirst;    // encoder v3: tile -> first piece starting in it
+  uint64_t *e3_status;    //   look-back word per tile
+  uint64_t *e3_tstate;    //   exit run state per tile
+  uint64_t e3_cap;        //   tiles the arrays hold (+2)
+  uint32_t epoch;         //   launch epoch tagging the look-back words, 1..65535
+  int e3_grid;            //   workgroups of encode3_kernel resident at once
 };
 
 namespace {
@@ -1800,6 +1808,63 @@ int ensure_plan(cpk_ctx ctx, uint64_t bytes) {
   return CPK_OK;
 }
 uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+
+// Encoder v3 (encode_v3.hip): plan kernel + persistent tile kernel.  The
+// tile count is bounded from the size hint (or read back when there is none);
+// a batch larger than the bound is reported through the error word.
+int e3_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, uint64_t hint,
+              void *d_out, uint64_t *d_out_off, hipStream_t s) {
+  const uint64_t TW = cpk::kE3TileWords;
+  uint64_t ntb;
+  if (hint) {
+    ntb = ((uint64_t)n * hint + TW - 1) / TW;
+  } else {
+    uint64_t ends[2];
+    if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return CPK_EDEVICE;
+    ntb = (ends[1] - ends[0] + TW - 1) / TW;
+  }
+  if (ntb > 0xfffffff0ull) return CPK_EUNSUPPORTED;
+  bool fresh = false;
+  if (ntb + 2 > ctx->e3_cap) {
+    if (ctx->e3_tfirst) hipFree(ctx->e3_tfirst);
+    if (ctx->e3_status) hipFree(ctx->e3_status);
+    if (ctx->e3_tstate) hipFree(ctx->e3_tstate);
+    ctx->e3_tfirst = nullptr;
+    ctx->e3_status = ctx->e3_tstate = nullptr;
+    ctx->e3_cap = 0;
+    uint64_t cap = ntb + 2 + (ntb + 2) / 4;
+    if (cap < 1024) cap = 1024;
+    if (hipMalloc(&ctx->e3_tfirst, cap * 4) != hipSuccess ||
+        hipMalloc(&ctx->e3_status, cap * 8) != hipSuccess ||
+        hipMalloc(&ctx->e3_tstate, cap * 8) != hipSuccess)
+      return CPK_ENOMEM;
+    ctx->e3_cap = cap;
+    fresh = true;
+  }
+  if (++ctx->epoch > 0xffffu) {
+    ctx->epoch = 1;
+    fresh = true;
+  }
+  if (fresh && (hipMemsetAsync(ctx->e3_status, 0, ctx->e3_cap * 8, s) != hipSuccess ||
+                hipMemsetAsync(ctx->e3_tstate, 0, ctx->e3_cap * 8, s) != hipSuccess))
+    return CPK_EDEVICE;
+  uint32_t *err = ctx->tickets + cpk::kTkErr;
+  uint64_t pb = ((uint64_t)n + 2 + 255) / 256;
+  if (pb > 4096) pb = 4096;
+  hipLaunchKernelGGL(cpk::e3_plan_kernel, dim3((unsigned)pb), dim3(256), 0, s, d_swo, n,
+                     (uint32_t)ntb, ctx->e3_tfirst, d_out_off, hint, err);
+  if (ntb == 0) return hip_ok(hipGetLastError());
+  uint64_t grid = (uint64_t)ctx->e3_grid;
+  if (grid > ntb) grid = ntb;
+  hipLaunchKernelGGL(cpk::encode3_kernel, dim3((unsigned)grid), dim3(cpk::kE3Threads), cpk::kE3Lds,
+                     s, (const uint64_t *)d_in, d_swo, n, (uint32_t)ntb,
+                     (const uint32_t *)ctx->e3_tfirst, (uint8_t *)d_out, d_out_off,
+                     ctx->e3_status, ctx->e3_tstate, ctx->epoch, err);
+  return hip_ok(hipGetLastError());
+}
 }  // namespace
 
 extern "C" {
@@ -1851,7 +1916,7 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     // CPK_ENCODER=2 selects the wave-per-tile encoder (experimental: its
     // per-1024-word look-back does not scale yet)
     const char *e = getenv("CPK_ENCODER");
-    c->encoder = (e && e[0] == '2') ? 2 : 1;
+    c->encoder = (e && e[0] == '3') ? 3 : (e && e[0] == '2') ? 2 : 1;
   }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
@@ -1867,10 +1932,25 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
       hipFuncSetAttribute((const void *)cpk::encode2_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kE2Lds) != hipSuccess ||
       hipFuncSetAttribute((const void *)cpk::decode_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess) {
+                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess ||
+      hipFuncSetAttribute((const void *)cpk::encode3_kernel,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kE3Lds) != hipSuccess) {
     hipFree(c->tickets);
     free(c);
     return CPK_EDEVICE;
+  }
+  {
+    // persistent grid of encode3_kernel: every workgroup resident at once
+    // (its look-back waits on other workgroups).  The occupancy answer can be
+    // one block per CU high for SGPR-heavy kernels (MI355X_MICROARCH.md,
+    // Residency), so one block per CU is kept in reserve.
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)cpk::encode3_kernel,
+                                                     cpk::kE3Threads, cpk::kE3Lds) != hipSuccess ||
+        occ < 1)
+      occ = 1;
+    if (occ > 1) occ -= 1;
+    c->e3_grid = occ * c->cus;
   }
   *out = c;
   return CPK_OK;
@@ -1882,6 +1962,9 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->status) hipFree(ctx->status);
   if (ctx->plan) hipFree(ctx->plan);
   if (ctx->tickets) hipFree(ctx->tickets);
+  if (ctx->e3_tfirst) hipFree(ctx->e3_tfirst);
+  if (ctx->e3_status) hipFree(ctx->e3_status);
+  if (ctx->e3_tstate) hipFree(ctx->e3_tstate);
   free(ctx);
 }
 
@@ -1894,6 +1977,7 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
+  if (ctx->encoder == 3) return e3_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
   // counters (not the error word: that is cleared by cpk_ctx_take_error)
   if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
   const bool v2 = ctx->encoder == 2;
@@ -1977,7 +2061,9 @@ int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
       hipStreamSynchronize(s) != hipSuccess)
     return CPK_EDEVICE;
   if (e && hipMemsetAsync(ctx->tickets + cpk::kTkErr, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
-  return e ? CPK_EINVAL : CPK_OK;
+  // bit 0: a piece over its size hint; bit 1: a look-back wait timed out
+  // (a grid larger than the device holds at once -- cannot happen by design)
+  return e ? ((e & 2u) ? CPK_EDEVICE : CPK_EINVAL) : CPK_OK;
 }
 
 int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off,
