@@ -37,19 +37,21 @@ constexpr int kE3Rows = kE3Waves * kE3Steps + kE3La;     // 68 step rows
 constexpr uint32_t kE3RingBytes = 2048;                  // output ring per wave
 constexpr uint32_t kE3RingLines = kE3RingBytes / 16;
 constexpr uint32_t kE3RingDw = kE3RingBytes / 4;
-// LDS byte offsets.  The tile's words stay in LDS between the phases so the
-// step loops can stay rolled (a fully unrolled tile overflows the registers
-// and the instruction cache).
-constexpr uint32_t kE3oWords = 0;                                  // u64[4096] the tile
-constexpr uint32_t kE3oLut = kE3oWords + 8 * kE3TileWords;         // u64[256]
+// LDS byte offsets.  The per-tile state (tags, step rows, wave totals) is
+// double-buffered: a workgroup builds tile i's state while it finishes tile
+// i-1 (look-back + strings), so the look-back never stalls the pipeline.
+// Phase 3 re-reads the tile's words from memory (L2 / Infinity Cache).
+constexpr uint32_t kE3oLut = 0;                                    // u64[256]
 constexpr uint32_t kE3oRing = kE3oLut + 2048;                      // u32[waves][512]
-constexpr uint32_t kE3oTag = kE3oRing + kE3Waves * kE3RingBytes;   // u8[rows][64]
-constexpr uint32_t kE3oPs = kE3oTag + kE3Rows * 64;                // u64[rows] piece starts
-constexpr uint32_t kE3oB = kE3oPs + kE3Rows * 8;                   // u64[rows] run boundaries
-constexpr uint32_t kE3oHd = kE3oB + kE3Rows * 8;                   // u64[rows] heads
-constexpr uint32_t kE3oMb = kE3oHd + kE3Rows * 8;                  // u64[rows] run members
-constexpr uint32_t kE3oScr = kE3oMb + kE3Rows * 8;                 // int[64]
-constexpr uint32_t kE3Lds = kE3oScr + 256;
+constexpr uint32_t kE3oBuf = kE3oRing + kE3Waves * kE3RingBytes;   // 2 x per-tile state
+constexpr uint32_t kE3bTag = 0;                                    // u8[rows][64]
+constexpr uint32_t kE3bPs = kE3bTag + kE3Rows * 64;                // u64[rows] piece starts
+constexpr uint32_t kE3bB = kE3bPs + kE3Rows * 8;                   // u64[rows] run boundaries
+constexpr uint32_t kE3bRole = kE3bB + kE3Rows * 8;                 // u8[rows][64] word roles
+constexpr uint32_t kE3bScr = kE3bRole + kE3Rows * 64;  // int[32]: wave totals, offset, partial sums
+constexpr uint32_t kE3BufBytes = kE3bScr + 128;
+constexpr uint32_t kE3Lds = kE3oBuf + 2 * kE3BufBytes;
+constexpr uint32_t kE3oPs = kE3oBuf + kE3bPs;  // (alignment check below)
 static_assert(kE3oPs % 8 == 0 && kE3oRing % 16 == 0, "LDS alignment");
 
 #ifndef CPK_E3_WPE
@@ -125,7 +127,7 @@ __device__ E3St e3_tile_entry(const uint64_t *tstate, uint32_t t, uint32_t ep, u
   for (;;) {
     const uint64_t v = uni64(ld_status(const_cast<uint64_t *>(&tstate[t - 1])));
     if ((uint32_t)(v >> 48) == ep) return e3_st_unpack(v);
-    if (++spins > (1u << 22)) {  // cannot happen with a co-resident grid
+    if (++spins > (1u << 16)) {  // cannot happen with a co-resident grid (~0.1 s)
       if (lane == 0) atomicOr(err, 2u);
       E3St s = {2, 0, 0};
       return s;
@@ -202,9 +204,13 @@ __device__ E3St e3_state_at(const uint8_t *tagrow, const uint64_t *psrow, int wp
   return s;
 }
 
+#ifndef CPK_E3_LBW
+#define CPK_E3_LBW 512
+#endif
+constexpr int kE3LbW = CPK_E3_LBW;  // predecessors read per look-back poll
+
 // Decoupled look-back over the tile totals (one wave, all lanes): publishes
 // the aggregate, returns the exclusive prefix, publishes the inclusive one.
-// Each poll reads the 256 nearest predecessors.
 __device__ uint64_t e3_lookback(uint64_t *status, uint32_t t, uint64_t agg, uint32_t ep,
                                 uint32_t *err, int lane) {
   if (lane == 0) st_status(&status[t], e3_word(ep, t == 0 ? 2u : 1u, agg));
@@ -213,32 +219,34 @@ __device__ uint64_t e3_lookback(uint64_t *status, uint32_t t, uint64_t agg, uint
   int64_t top = (int64_t)t - 1;
   uint32_t spins = 0;
   for (;;) {
-    uint64_t v[4];
-    uint32_t fl[4];
-    int fi = 4;  // first inclusive among this lane's four (nearest first)
+    // one poll reads the kE3LbW nearest predecessors, all loads in flight
+    // at once: with the pipelined grid the nearest inclusive prefix is about
+    // one grid's worth of tiles back
+    constexpr int kPer = kE3LbW / 64;
+    uint64_t v[kPer];
+    int fi = kPer;  // first inclusive among this lane's (nearest first)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t idx = top - 4 * lane - i;
+    for (int i = 0; i < kPer; ++i) {
+      const int64_t idx = top - kPer * lane - i;
       v[i] = idx >= 0 ? ld_status(&status[idx]) : e3_word(ep, 2u, 0);
-      fl[i] = e3_flag(v[i], ep);
     }
 #pragma unroll
-    for (int i = 3; i >= 0; --i)
-      if (fl[i] == 2) fi = i;
-    const uint64_t has = __ballot(fi < 4);
+    for (int i = kPer - 1; i >= 0; --i)
+      if (e3_flag(v[i], ep) == 2) fi = i;
+    const uint64_t has = __ballot(fi < kPer);
     const int fln = has ? __builtin_ctzll(has) : 64;
-    const int firstPos = fln < 64 ? 4 * fln + __builtin_amdgcn_readlane(fi, fln) : 256;
+    const int firstPos = fln < 64 ? kPer * fln + __builtin_amdgcn_readlane(fi, fln) : kE3LbW;
     bool z = false;
     uint64_t sum = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (4 * lane + i <= firstPos) {
-        z = z || fl[i] == 0;
+    for (int i = 0; i < kPer; ++i) {
+      if (kPer * lane + i <= firstPos) {
+        z = z || e3_flag(v[i], ep) == 0;
         sum += v[i] & kE3ValMask;
       }
     }
     if (__ballot(z)) {
-      if (++spins > (1u << 22)) {  // cannot happen with a co-resident grid
+      if (++spins > (1u << 16)) {  // cannot happen with a co-resident grid (~0.1 s)
         if (lane == 0) atomicOr(err, 2u);
         break;
       }
@@ -247,8 +255,8 @@ __device__ uint64_t e3_lookback(uint64_t *status, uint32_t t, uint64_t agg, uint
     }
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
     excl += sum;
-    if (firstPos < 256) break;
-    top -= 256;
+    if (firstPos < kE3LbW) break;
+    top -= kE3LbW;
   }
   if (lane == 0) st_status(&status[t], e3_word(ep, 2u, excl + agg));
   return excl;
@@ -318,230 +326,231 @@ __global__ void e3_plan_kernel(const uint64_t *__restrict__ swo, uint32_t n, uin
   }
 }
 
-__global__ __launch_bounds__(kE3Threads, CPK_E3_WPE) void encode3_kernel(
-    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n, uint32_t ntb,
-    const uint32_t *__restrict__ tfirst, uint8_t *__restrict__ out, uint64_t *__restrict__ out_off,
-    uint64_t *status, uint64_t *tstate, uint32_t ep, uint32_t *err) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kE3oLut);
-  uint8_t *tagrow = smem + kE3oTag;
-  uint64_t *psrow = reinterpret_cast<uint64_t *>(smem + kE3oPs);
-  uint64_t *brow = reinterpret_cast<uint64_t *>(smem + kE3oB);
-  uint64_t *hdrow = reinterpret_cast<uint64_t *>(smem + kE3oHd);
-  uint64_t *mbrow = reinterpret_cast<uint64_t *>(smem + kE3oMb);
-  uint64_t *words = reinterpret_cast<uint64_t *>(smem + kE3oWords);
-  int *scr = reinterpret_cast<int *>(smem + kE3oScr);
-  // the wave index through readfirstlane: hipcc's divergence analysis treats
-  // threadIdx.x >> 6 as divergent, which would turn every wave-uniform branch
-  // below into an exec-masked one
-  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(wave_id());
-  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kE3oRing + w * kE3RingBytes);
-  fill_luts(lut, false);
-  for (uint32_t i = lane_id(); i < kE3RingLines; i += 64)
-    reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
-  const uint64_t base = swo[0], N = swo[n];
-  uint32_t nt = (uint32_t)((N - base + kE3TileWords - 1) / kE3TileWords);
-  if (nt > ntb) nt = ntb;  // (reported by the plan kernel)
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    // tile position of the wave's first word, opaque per tile for the same
-    // reason as the lane id below (per-step row offsets hoisted into SGPRs)
-    int wb = w * kE3WaveWords;
-    asm volatile("" : "+s"(wb));
-    // an opaque copy of the lane id per tile: hipcc otherwise hoists ~100
-    // per-lane addresses and masks out of the tile loop and spills them
-    int lane = lane_id();
-    asm volatile("" : "+v"(lane));
-    const uint64_t gtm = lane == 63 ? 0ull : (~0ull << (lane + 1));  // lanes above this one
-    const uint64_t T0 = base + (uint64_t)t * kE3TileWords;
-    const uint64_t rem = N - T0;
-    const int TW = rem < (uint64_t)kE3TileWords ? (int)rem : kE3TileWords;    // words of the tile
-    const int pN = rem < (uint64_t)(kE3Rows * 64) ? (int)rem : kE3Rows * 64;  // batch end
-    // ---- phase 0: piece-start rows, boundary rows ---------------------------
-    __syncthreads();  // the previous tile's LDS reads are done
-    if (tid < kE3Rows) {
-      psrow[tid] = 0;
-      brow[tid] = 0;
-    }
-    __syncthreads();
-    {
-      const uint32_t p0 = tfirst[t], p2 = tfirst[min(t + 2, nt + 1)];
-      for (uint32_t i = p0 + tid; i < p2; i += kE3Threads) {
-        const uint64_t k = swo[i] - T0;
-        if (k < (uint64_t)pN)
-          atomicOr(reinterpret_cast<unsigned long long *>(&psrow[k >> 6]), 1ull << (k & 63));
-      }
-      if (tid == 0 && pN < kE3Rows * 64)  // the end of the batch ends every run
-        atomicOr(reinterpret_cast<unsigned long long *>(&brow[pN >> 6]), 1ull << (pN & 63));
-    }
-    // ---- phase 1: load, tag ------------------------------------------------
-    uint32_t mlast;  // tag of the wave's last word
-    {
-      const uint64_t *src = in + T0;
-      uint64_t v[kE3Steps];
+constexpr int kE3MaxPer = 5;  // tile sizes each thread sums: grids up to 1280 workgroups
+
+// Phases 0-2 of tile t into state buffer `bf` (all waves; ends with the
+// wave totals in bf's scratch and the tile's exit run state published).
+__device__ __forceinline__ void e3_front(const uint64_t *__restrict__ in,
+                                         const uint64_t *__restrict__ swo,
+                                         const uint32_t *__restrict__ tfirst, uint8_t *bf,
+                                         uint64_t *tstate, uint32_t ep, uint32_t *err, uint32_t t,
+                                         uint32_t nt, uint64_t base, uint64_t N, int w, int wb,
+                                         int lane) {
+  uint8_t *tagrow = bf + kE3bTag;
+  uint64_t *psrow = reinterpret_cast<uint64_t *>(bf + kE3bPs);
+  uint64_t *brow = reinterpret_cast<uint64_t *>(bf + kE3bB);
+  uint8_t *rolerow = bf + kE3bRole;
+  int *scr = reinterpret_cast<int *>(bf + kE3bScr);
+  const int tid = w * 64 + lane;
+  const uint64_t T0 = base + (uint64_t)t * kE3TileWords;
+  const uint64_t rem = N - T0;
+  const int TW = rem < (uint64_t)kE3TileWords ? (int)rem : kE3TileWords;    // words of the tile
+  const int pN = rem < (uint64_t)(kE3Rows * 64) ? (int)rem : kE3Rows * 64;  // batch end
+  // ---- phase 1a: the loads go out first --------------------------------------
+  const uint64_t *src = in + T0;
+  uint64_t v[kE3Steps];
 #pragma unroll
-      for (int s = 0; s < kE3Steps; ++s) {
-        const int k = wb + 64 * s + lane;
-        const uint64_t x = src[min(k, TW - 1)];
-        v[s] = k < TW ? x : 0ull;
-      }
+  for (int s = 0; s < kE3Steps; ++s) {
+    const int k = wb + 64 * s + lane;
+    const uint64_t x = src[min(k, TW - 1)];
+    v[s] = k < TW ? x : 0ull;
+  }
+  // ---- phase 0: piece-start rows, boundary rows (buffer free since the
+  // previous iteration's barrier) ----------------------------------------------
+  if (tid < kE3Rows) {
+    psrow[tid] = 0;
+    brow[tid] = 0;
+  }
+  __syncthreads();
+  {
+    const uint32_t p0 = tfirst[t], p2 = tfirst[min(t + 2, nt + 1)];
+    for (uint32_t i = p0 + tid; i < p2; i += kE3Threads) {
+      const uint64_t k = swo[i] - T0;
+      if (k < (uint64_t)pN)
+        atomicOr(reinterpret_cast<unsigned long long *>(&psrow[k >> 6]), 1ull << (k & 63));
+    }
+    if (tid == 0 && pN < kE3Rows * 64)  // the end of the batch ends every run
+      atomicOr(reinterpret_cast<unsigned long long *>(&brow[pN >> 6]), 1ull << (pN & 63));
+  }
+  // ---- phase 1b: tags ----------------------------------------------------------
+  uint32_t mlast = 0;  // tag of the wave's last word
 #pragma unroll
-      for (int s = 0; s < kE3Steps; ++s) {
-        const uint32_t m = e3_tag(v[s]);
-        words[wb + 64 * s + lane] = v[s];
-        tagrow[wb + 64 * s + lane] = (uint8_t)m;
-        mlast = m;
-      }
+  for (int s = 0; s < kE3Steps; ++s) {
+    const uint32_t m = e3_tag(v[s]);
+    tagrow[wb + 64 * s + lane] = (uint8_t)m;
+    mlast = m;
+  }
+  __syncthreads();  // B1: tags and piece starts of the whole tile
+  if (w == kE3Waves - 1 && TW == kE3TileWords && pN > kE3TileWords) {
+    // look-ahead: boundaries of up to kE3La steps past the tile, until the
+    // run crossing the tile end stops (counts are capped at 255 words)
+    int gprev = e3_grp((uint32_t)__builtin_amdgcn_readlane((int)mlast, 63));
+    for (int r = 0; r < kE3La; ++r) {
+      const int k = kE3TileWords + 64 * r + lane;
+      const bool ok = k < pN;
+      const uint64_t x = in[T0 + (uint64_t)min(k, pN - 1)];
+      const int g = ok ? e3_grp(e3_tag(x)) : 3;
+      const int gp = wave_shr1(g, gprev);
+      const uint64_t ps = uni64(psrow[kE3Waves * kE3Steps + r]);
+      const uint64_t b = __ballot(ok && (g != gp || g == 2)) | ps | __ballot(k == pN);
+      if (lane == 0) brow[kE3Waves * kE3Steps + r] = b;
+      gprev = __builtin_amdgcn_readlane(g, 63);
+      if (b) break;
     }
-    __syncthreads();  // B1: tags and piece starts of the whole tile
-    if (w == kE3Waves - 1 && TW == kE3TileWords && pN > kE3TileWords) {
-      // look-ahead: boundaries of up to kE3La steps past the tile, until the
-      // run crossing the tile end stops (counts are capped at 255 words)
-      int gprev = e3_grp((uint32_t)__builtin_amdgcn_readlane((int)mlast, 63));
-      for (int r = 0; r < kE3La; ++r) {
-        const int k = kE3TileWords + 64 * r + lane;
-        const bool ok = k < pN;
-        const uint64_t x = in[T0 + (uint64_t)min(k, pN - 1)];
-        const int g = ok ? e3_grp(e3_tag(x)) : 3;
-        const int gp = wave_shr1(g, gprev);
-        const uint64_t ps = uni64(psrow[kE3Waves * kE3Steps + r]);
-        const uint64_t b = __ballot(ok && (g != gp || g == 2)) | ps | __ballot(k == pN);
-        if (lane == 0) brow[kE3Waves * kE3Steps + r] = b;
-        gprev = __builtin_amdgcn_readlane(g, 63);
-        if (b) break;
-      }
-    }
-    // ---- phase 2: roles and sizes ------------------------------------------
-    const bool active = wb < TW;
-    int wtot = 0;
-    if (active) {
-      E3St st = {2, 0, 0};
-      if (w == 0) {
-        if (!(uni64(psrow[0]) & 1) && t > 0) st = e3_tile_entry(tstate, t, ep, err, lane);
-      } else {
-        st = e3_state_at(tagrow, psrow, wb, tstate, t, ep, err, lane);
-      }
-#pragma unroll 1
-      for (int s = 0; s < kE3Steps; ++s) {
-        const int kb = wb + 64 * s;
-        const int k = kb + lane;
-        const bool valid = k < TW;
-        const uint32_t m = tagrow[k];
-        const uint32_t pop = (uint32_t)__builtin_popcount(m);
-        const uint64_t Z = __ballot(valid && m == 0), D = __ballot(m == 0xffu),
-                       DL = __ballot(pop >= 7), V = __ballot(valid);
-        const uint64_t PS = uni64(psrow[kb >> 6]);
-        const uint64_t M = V & ~(Z | DL);
-        const uint64_t cz = st.g == 0 ? 1ull : 0ull, cdl = st.g == 1 ? 1ull : 0ull;
-        // run boundaries: piece starts, group changes, every M word
-        const uint64_t B = (PS & V) | (Z & ~((Z << 1) | cz)) | (DL & ~((DL << 1) | cdl)) | M;
-        const uint64_t BV = B | ~V;  // (past the batch's end no run continues)
-        const int f = BV ? __builtin_ctzll(BV) : 64;  // words [0, f) continue the carried run
-        // 0x00 heads: zero-run starts, and every 256th word of the carried run (:125-127)
-        uint64_t ZH = Z & B;
-        if (st.g == 0) {
-          const int j0 = (256 - (st.len & 255)) & 255;
-          if (j0 < f) ZH |= 1ull << j0;
-        }
-        // literal-run members: a D earlier in the same D/L stretch (carry of
-        // D + DL: generate at D, propagate through D/L, killed at boundaries)
-        const uint64_t kil = ~(B >> 1);
-        const uint64_t G = D & kil, P = DL & kil;
-        const uint64_t cin = (st.g == 1 && st.hd > 0 && !(B & 1)) ? 1ull : 0ull;
-        const uint64_t cc = (G + P + cin) ^ G ^ P;
-        uint64_t MEMB = DL & cc;
-        uint64_t DH = D & ~MEMB;
-        int h1 = -1;
-        if (st.g == 1 && st.len + f > 256) {
-          // the carried stretch is longer than 256 words: members lie within
-          // 255 words of a head, the next head is the first D 256 or more
-          // words after the last (:143-161)
-          const uint64_t rng = f >= 64 ? ~0ull : ((1ull << f) - 1);
-          uint64_t mc = 0;
-          if (st.hd > 0 && st.hd <= 255) {
-            const int me = 255 - st.hd;
-            mc = me >= 63 ? ~0ull : ((2ull << me) - 1);
-          }
-          const int js = st.hd > 0 ? max(0, 256 - st.hd) : 0;
-          const uint64_t dc = js >= 64 ? 0ull : (D & rng & (~0ull << js));
-          if (dc) {
-            h1 = __builtin_ctzll(dc);
-            mc |= h1 == 63 ? 0ull : (~0ull << (h1 + 1));
-          }
-          MEMB = (MEMB & ~rng) | (mc & DL & rng);
-          DH = (DH & ~rng) | (h1 >= 0 ? (1ull << h1) : 0ull);
-        }
-        const uint64_t HD = ZH | DH;
-        const uint32_t q = 1 + pop;
-        const uint64_t q0 = __ballot(q & 1) & M, q1 = __ballot(q & 2) & M, q2 = __ballot(q & 4) & M;
-        wtot += 8 * __popcll(DL) + 2 * __popcll(HD) + __popcll(q0) + 2 * __popcll(q1) +
-                4 * __popcll(q2);
-        if (lane == 0) {
-          hdrow[kb >> 6] = HD;
-          mbrow[kb >> 6] = MEMB;
-        }
-        const uint64_t bend = __ballot(k == pN);
-        if (lane == 0) brow[kb >> 6] = B | bend;
-        // the run state entering the next step
-        if (B) {
-          const int lb = 63 - __builtin_clzll(B);
-          st.g = ((Z >> lb) & 1) ? 0 : (((DL >> lb) & 1) ? 1 : 2);
-          st.len = 64 - lb;
-          st.hd = 0;
-          if (st.g == 1) {
-            const uint64_t dd = D & (~0ull << lb);
-            st.hd = dd ? 64 - __builtin_ctzll(dd) : 0;
-          }
-        } else if (st.g != 2) {
-          st.len += 64;
-          if (st.g == 1) {
-            if (h1 >= 0) st.hd = 64 - h1;
-            else if (st.hd > 0) st.hd = min(st.hd + 64, 256);
-            else st.hd = D ? 64 - __builtin_ctzll(D) : 0;
-          }
-        }
-      }
-      // the tile's exit state, for the next tile's first run
-      if (w == kE3Waves - 1 && lane == 0) st_status(&tstate[t], e3_st_pack(ep, st));
-    }
-    if (lane == 0) scr[w] = wtot;
-    __syncthreads();  // B2: sizes and boundary rows of every wave
+  }
+  // ---- phase 2: roles and sizes ------------------------------------------------
+  int wtot = 0;
+  if (wb < TW) {
+    E3St st = {2, 0, 0};
     if (w == 0) {
-      uint64_t tot = 0;
-      for (int q = 0; q < kE3Waves; ++q) tot += (uint32_t)scr[q];
-      const uint64_t excl = e3_lookback(status, t, tot, ep, err, lane);
-      if (lane == 0) {
-        *reinterpret_cast<uint64_t *>(&scr[8]) = excl;
-        if (T0 + (uint64_t)TW == N)  // pieces starting at the end of the batch (and swo[n])
-          for (int64_t j = n; j >= 0 && swo[j] == N; --j) out_off[j] = excl + tot;
+      if (!(uni64(psrow[0]) & 1) && t > 0) st = e3_tile_entry(tstate, t, ep, err, lane);
+    } else {
+      st = e3_state_at(tagrow, psrow, wb, tstate, t, ep, err, lane);
+    }
+    const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);  // lanes <= this one
+    uint32_t acc = 0;  // this lane's packed bytes over the steps
+#pragma unroll 1
+    for (int s = 0; s < kE3Steps; ++s) {
+      const int kb = wb + 64 * s;
+      const int k = kb + lane;
+      const bool valid = k < TW;
+      const uint32_t m = tagrow[k];
+      const uint32_t pop = (uint32_t)__builtin_popcount(m);
+      const uint64_t PS = uni64(psrow[kb >> 6]);
+      // run boundaries (piece starts, group changes, every M word), per lane
+      const int g = !valid ? 3 : (m == 0 ? 0 : (pop >= 7 ? 1 : 2));
+      const int gp = wave_shr1(g, st.g);
+      const bool isB = valid && (lanebit(PS) || g != gp || g == 2);
+      const uint64_t B = __ballot(isB), D = __ballot(m == 0xffu), DL = __ballot(g == 1);
+      // this lane's run start (step-relative; the carried run started st.len
+      // words before the step) and the last D before it
+      const uint64_t bl = B & lem;
+      const int rs = bl ? 63 - __builtin_clzll(bl) : -st.len;
+      const uint64_t dl = D & (lem >> 1);
+      const int lastD = dl ? 63 - __builtin_clzll(dl) : (st.hd > 0 ? -st.hd : -(1 << 30));
+      // 0x00 heads every 256 words of a zero run from its start (:119-131);
+      // literal-run members: a D earlier in the same D/L stretch (:133-161,
+      // exact for stretches of <= 256 words; longer ones below)
+      uint32_t zh = (g == 0 && ((lane - rs) & 255) == 0) ? 1u : 0u;
+      uint32_t memb = (g == 1 && lastD >= rs) ? 1u : 0u;
+      uint32_t dh = (m == 0xffu && !memb) ? 1u : 0u;
+      const uint64_t BV = B | __ballot(!valid);  // (past the batch's end no run continues)
+      const int f = BV ? __builtin_ctzll(BV) : 64;  // words [0, f) continue the carried run
+      int h1 = -1;
+      if (st.g == 1 && st.len + f > 256) {
+        // the carried stretch is longer than 256 words: members lie within
+        // 255 words of a head, the next head is the first D 256 or more
+        // words after the last (:143-161)
+        const uint64_t rng = f >= 64 ? ~0ull : ((1ull << f) - 1);
+        uint64_t mc = 0;
+        if (st.hd > 0 && st.hd <= 255) {
+          const int me = 255 - st.hd;
+          mc = me >= 63 ? ~0ull : ((2ull << me) - 1);
+        }
+        const int js = st.hd > 0 ? max(0, 256 - st.hd) : 0;
+        const uint64_t dc = js >= 64 ? 0ull : (D & rng & (~0ull << js));
+        if (dc) {
+          h1 = __builtin_ctzll(dc);
+          mc |= h1 == 63 ? 0ull : (~0ull << (h1 + 1));
+        }
+        if ((rng >> lane) & 1) {
+          memb = ((mc & DL) >> lane) & 1;
+          dh = (h1 == lane) ? 1u : 0u;
+        }
+      }
+      const uint32_t isH = zh | dh;
+      // packed bytes: M words 1 + popcount, D/L 8 (+2 for a 0xFF head), 0x00 heads 2
+      const uint32_t nb = !valid ? 0u : (g == 2 ? 1 + pop : (g == 1 ? 8 + 2 * dh : 2 * zh));
+      acc += nb;
+      rolerow[k] = (uint8_t)(nb | (memb << 4) | (isH << 5));
+      const uint64_t bend = __ballot(k == pN);
+      if (lane == 0) brow[kb >> 6] = B | bend;
+      // the run state entering the next step
+      if (B) {
+        const int lb = 63 - __builtin_clzll(B);
+        const int g63 = __builtin_amdgcn_readlane(g, 63);
+        st.g = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
+        st.len = 64 - lb;
+        st.hd = 0;
+        if (st.g == 1) {
+          const uint64_t dd = D & (~0ull << lb);
+          st.hd = dd ? 64 - __builtin_ctzll(dd) : 0;
+        }
+      } else if (st.g != 2) {
+        st.len += 64;
+        if (st.g == 1) {
+          if (h1 >= 0) st.hd = 64 - h1;
+          else if (st.hd > 0) st.hd = min(st.hd + 64, 256);
+          else st.hd = D ? 64 - __builtin_ctzll(D) : 0;
+        }
       }
     }
-    __syncthreads();  // B3: the tile's output offset
-    // ---- phase 3: packed strings -> ring -> memory -------------------------
-    if (active) {
-      uint64_t obase = *reinterpret_cast<const uint64_t *>(&scr[8]);
-      for (int q = 0; q < w; ++q) obase += (uint32_t)scr[q];
-      uint64_t rpos = obase;     // output offset of the next string
-      uint64_t fl = obase >> 4;  // first line not stored yet
-      int nbrRow = -1, nbr = 0;  // first boundary in the rows after nbrRow
-      const uint32_t pfirst = tfirst[t], plast = tfirst[t + 1];
-#pragma unroll 1
+    wtot = wave_incl_add((int)acc);
+    wtot = __builtin_amdgcn_readlane(wtot, 63);
+    // the tile's exit state, for the next tile's first run
+    if (w == kE3Waves - 1 && lane == 0) st_status(&tstate[t], e3_st_pack(ep, st));
+  }
+  if (lane == 0) scr[w] = wtot;
+}
+
+// Look-back of tile t from state buffer `bf` (wave 0): the tile's output
+// offset into the buffer's scratch.
+__device__ __forceinline__ void e3_tile_offset(const uint64_t *__restrict__ swo, uint32_t n,
+                                               uint64_t *__restrict__ out_off, uint8_t *bf,
+                                               uint64_t *status, uint32_t ep, uint32_t *err,
+                                               uint32_t t, uint64_t base, uint64_t N, int w,
+                                               int lane) {
+  int *scr = reinterpret_cast<int *>(bf + kE3bScr);
+  const uint64_t T0 = base + (uint64_t)t * kE3TileWords;
+  const uint64_t rem = N - T0;
+  const int TW = rem < (uint64_t)kE3TileWords ? (int)rem : kE3TileWords;
+  if (w == 0) {
+    uint64_t tot = 0;
+    for (int q = 0; q < kE3Waves; ++q) tot += (uint32_t)scr[q];
+    const uint64_t excl = e3_lookback(status, t, tot, ep, err, lane);
+    if (lane == 0) {
+      *reinterpret_cast<uint64_t *>(&scr[8]) = excl;
+      if (T0 + (uint64_t)TW == N)  // pieces starting at the end of the batch (and swo[n])
+        for (int64_t j = n; j >= 0 && swo[j] == N; --j) out_off[j] = excl + tot;
+    }
+  }
+}
+
+// Phase 3 of tile t after its look-back (all waves).
+__device__ __forceinline__ void e3_strings(const uint64_t *__restrict__ in,
+                                           const uint64_t *__restrict__ swo, uint32_t n,
+                                           const uint32_t *__restrict__ tfirst,
+                                           uint8_t *__restrict__ out,
+                                           uint64_t *__restrict__ out_off, const uint64_t *lut,
+                                           uint32_t *ring, uint8_t *bf, uint32_t t, uint64_t base,
+                                           uint64_t N, int w, int wb, int lane,
+                                           const uint64_t (&v)[kE3Steps]) {
+  uint64_t *psrow = reinterpret_cast<uint64_t *>(bf + kE3bPs);
+  uint64_t *brow = reinterpret_cast<uint64_t *>(bf + kE3bB);
+  const uint8_t *rolerow = bf + kE3bRole;
+  int *scr = reinterpret_cast<int *>(bf + kE3bScr);
+  const uint64_t gtm = lane == 63 ? 0ull : (~0ull << (lane + 1));  // lanes above this one
+  const uint64_t T0 = base + (uint64_t)t * kE3TileWords;
+  const uint64_t rem = N - T0;
+  const int TW = rem < (uint64_t)kE3TileWords ? (int)rem : kE3TileWords;
+  if (wb < TW) {
+    uint64_t obase = *reinterpret_cast<const uint64_t *>(&scr[8]);
+    for (int q = 0; q < w; ++q) obase += (uint32_t)scr[q];
+    uint64_t rpos = obase;     // output offset of the next string
+    uint64_t fl = obase >> 4;  // first line not stored yet
+    int nbrRow = -1, nbr = 0;  // first boundary in the rows after nbrRow
+    const uint32_t pfirst = tfirst[t], plast = tfirst[t + 1];
+#pragma unroll
       for (int s = 0; s < kE3Steps; ++s) {
         const int kb = wb + 64 * s;
         const int k = kb + lane;
-        const uint32_t m = tagrow[k];
-        const uint64_t word = words[k];
-        const uint32_t pop = (uint32_t)__builtin_popcount(m);
-        const uint32_t isDL = pop >= 7 ? 1u : 0u, isM = (m != 0 && pop < 7 && k < TW) ? 1u : 0u;
-        const uint32_t isH = lanebit(uni64(hdrow[kb >> 6]));
-        const uint32_t isMb = lanebit(uni64(mbrow[kb >> 6]));
-        // packed size: M words 1 + popcount, D/L 8, heads + 2 (Z heads 2,
-        // D heads 10; M words are never heads)
-        const uint32_t nb = ((1 + pop) & (0u - isM)) + (isDL << 3) + (isH << 1);
-        const uint64_t b0 = __ballot(nb & 1), b1 = __ballot(nb & 2), b2 = __ballot(nb & 4),
-                       b3 = __ballot(nb & 8);
-        const uint32_t o = (uint32_t)(mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2) + 8 * mbcnt(b3));
-        const uint32_t stot = (uint32_t)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) +
-                                         8 * __popcll(b3));
+        const uint64_t word = v[s];
+        const uint32_t m = e3_tag(word);
+        const uint32_t role = rolerow[k];
+        const uint32_t nb = role & 15u, isMb = (role >> 4) & 1u, isH = (role >> 5) & 1u;
+        const int incl = wave_incl_add((int)nb);
+        const uint32_t o = (uint32_t)incl - nb;
+        const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
         uint32_t cnt = 0;
         if (__ballot(isH)) {
           // a head's count: words to the run's end, at most 255 (:123-131, :143-164)
@@ -610,11 +619,135 @@ __global__ __launch_bounds__(kE3Threads, CPK_E3_WPE) void encode3_kernel(
         wave_lds_sync();
         e3_flush(out, ring, fl, rpos >> 4, obase, lane);
       }
-      // the wave's last, partial line
-      if (rpos > fl * 16) {
-        const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
-        e3_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane);
-      }
+
+    // the wave's last, partial line
+    if (rpos > fl * 16) {
+      const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
+      e3_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane);
     }
   }
+}
+
+__global__ __launch_bounds__(kE3Threads, CPK_E3_WPE) void encode3_kernel(
+    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n, uint32_t ntb,
+    const uint32_t *__restrict__ tfirst, uint8_t *__restrict__ out, uint64_t *__restrict__ out_off,
+    uint64_t *status, uint64_t *rbase, uint64_t *tstate, uint32_t ep, uint32_t *err) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint64_t *lut = reinterpret_cast<const uint64_t *>(smem + kE3oLut);
+  // the wave index through readfirstlane: hipcc's divergence analysis treats
+  // threadIdx.x >> 6 as divergent, which would turn every wave-uniform branch
+  // below into an exec-masked one
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kE3oRing + w * kE3RingBytes);
+  fill_luts(reinterpret_cast<uint64_t *>(smem + kE3oLut), false);
+  for (uint32_t i = lane_id(); i < kE3RingLines; i += 64)
+    reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
+  const uint64_t base = swo[0], N = swo[n];
+  uint32_t nt = (uint32_t)((N - base + kE3TileWords - 1) / kE3TileWords);
+  if (nt > ntb) nt = ntb;  // (reported by the plan kernel)
+  __syncthreads();
+  WPH_INIT
+  const int tid = threadIdx.x;
+  const uint32_t G = gridDim.x, g = blockIdx.x;
+  // Two-stage pipeline over this workgroup's tiles t_i = g + i G ("round" i):
+  // iteration i builds t_i's roles and publishes its packed size (front),
+  // then finishes t_{i-1} (back).  t_{i-1}'s output offset is the base of
+  // round i-1 (published by that round's last workgroup in its back stage)
+  // plus the sizes of the round's g tiles before it (all published an
+  // iteration ago): loads issued before the front, summed after it.
+  for (uint32_t i = 0;; ++i) {
+    const uint32_t t = g + i * G;
+    uint64_t la[kE3MaxPer], lrb = 0;
+    if (i > 0) {
+      const uint32_t r0 = (i - 1) * G;  // first tile of round i-1
+#pragma unroll
+      for (int j = 0; j < kE3MaxPer; ++j) {
+        const uint32_t q = tid + kE3Threads * j;
+        la[j] = q < g ? ld_status(&status[r0 + q]) : e3_word(ep, 1u, 0);
+      }
+      lrb = i > 1 ? ld_status(&rbase[i - 1]) : e3_word(ep, 1u, 0);
+    }
+    // opaque per iteration: hipcc otherwise hoists ~100 per-lane addresses
+    // and per-step row offsets out of the loop and spills them
+    int wb = w * kE3WaveWords;
+    asm volatile("" : "+s"(wb));
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    uint8_t *bcur = smem + kE3oBuf + (i & 1) * kE3BufBytes;
+    uint8_t *bprev = smem + kE3oBuf + ((i & 1) ^ 1) * kE3BufBytes;
+    if (t < nt) e3_front(in, swo, tfirst, bcur, tstate, ep, err, t, nt, base, N, w, wb, lane);
+    WPH(0)
+    __syncthreads();  // B2: t's totals and rows; t_{i-1}'s buffer is complete too
+    WPH(1)
+    if (t < nt && tid == 0) {  // t's packed size for the next round's offsets
+      const int *sc = reinterpret_cast<const int *>(bcur + kE3bScr);
+      uint64_t tot = 0;
+      for (int q = 0; q < kE3Waves; ++q) tot += (uint32_t)sc[q];
+      st_status(&status[t], e3_word(ep, 1u, tot));
+    }
+    if (i > 0) {
+      // t_{i-1}'s words again (L2 / Infinity Cache), all in flight across the
+      // look-back wait and ahead of any store of phase 3
+      const uint32_t tp = t - gridDim.x;
+      const uint64_t T0p = base + (uint64_t)tp * kE3TileWords;
+      const int TWp = N - T0p < (uint64_t)kE3TileWords ? (int)(N - T0p) : kE3TileWords;
+      uint64_t v[kE3Steps];
+#pragma unroll
+      for (int s = 0; s < kE3Steps; ++s) {
+        const int k = wb + 64 * s + lane;
+        const uint64_t x = in[T0p + (uint64_t)min(k, TWp - 1)];
+        v[s] = k < TWp ? x : 0ull;
+      }
+      {
+        // t_{i-1}'s offset: check the loads issued before the front (re-poll
+        // what was not published yet: a lagging workgroup), sum them
+        const uint32_t r0 = (i - 1) * G;
+        uint32_t spins = 0;
+        for (;;) {
+          bool miss = e3_flag(lrb, ep) == 0;
+#pragma unroll
+          for (int j = 0; j < kE3MaxPer; ++j) miss = miss || e3_flag(la[j], ep) == 0;
+          if (!__syncthreads_or(miss)) break;
+          if (++spins > (1u << 16)) {  // cannot happen with a co-resident grid
+            if (tid == 0) atomicOr(err, 2u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+          for (int j = 0; j < kE3MaxPer; ++j) {
+            const uint32_t q = tid + kE3Threads * j;
+            if (q < g && e3_flag(la[j], ep) == 0) la[j] = ld_status(&status[r0 + q]);
+          }
+          if (e3_flag(lrb, ep) == 0) lrb = ld_status(&rbase[i - 1]);
+        }
+        uint64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < kE3MaxPer; ++j) sum += la[j] & kE3ValMask;
+        for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+        uint64_t *ps = reinterpret_cast<uint64_t *>(bprev + kE3bScr + 64);
+        if (lane == 0) ps[w] = sum;
+        __syncthreads();
+        int *sc = reinterpret_cast<int *>(bprev + kE3bScr);
+        const uint64_t excl = (lrb & kE3ValMask) + ps[0] + ps[1] + ps[2] + ps[3];
+        uint64_t tot = 0;
+        for (int q = 0; q < kE3Waves; ++q) tot += (uint32_t)sc[q];
+        if (tid == 0) {
+          *reinterpret_cast<uint64_t *>(&sc[8]) = excl;
+          if (g == G - 1) st_status(&rbase[i], e3_word(ep, 1u, excl + tot));  // next round's base
+          const uint64_t T0 = base + (uint64_t)tp * kE3TileWords;
+          if (T0 + (uint64_t)TWp == N)  // pieces starting at the end of the batch (and swo[n])
+            for (int64_t j = n; j >= 0 && swo[j] == N; --j) out_off[j] = excl + tot;
+        }
+      }
+      WPH(2)
+      __syncthreads();  // B3: the tile's output offset
+      WPH(3)
+      e3_strings(in, swo, n, tfirst, out, out_off, lut, ring, bprev, tp, base, N, w, wb, lane, v);
+    }
+    WPH(4)
+    if (t >= nt) break;
+    __syncthreads();  // bprev is free for the next iteration's front
+    WPH(5)
+  }
+  WPH_FLUSH(40)
 }

@@ -1838,7 +1838,7 @@ int e3_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
     uint64_t cap = ntb + 2 + (ntb + 2) / 4;
     if (cap < 1024) cap = 1024;
     if (hipMalloc(&ctx->e3_tfirst, cap * 4) != hipSuccess ||
-        hipMalloc(&ctx->e3_status, cap * 8) != hipSuccess ||
+        hipMalloc(&ctx->e3_status, cap * 16) != hipSuccess ||  // tile sizes | round bases
         hipMalloc(&ctx->e3_tstate, cap * 8) != hipSuccess)
       return CPK_ENOMEM;
     ctx->e3_cap = cap;
@@ -1848,7 +1848,7 @@ int e3_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
     ctx->epoch = 1;
     fresh = true;
   }
-  if (fresh && (hipMemsetAsync(ctx->e3_status, 0, ctx->e3_cap * 8, s) != hipSuccess ||
+  if (fresh && (hipMemsetAsync(ctx->e3_status, 0, ctx->e3_cap * 16, s) != hipSuccess ||
                 hipMemsetAsync(ctx->e3_tstate, 0, ctx->e3_cap * 8, s) != hipSuccess))
     return CPK_EDEVICE;
   uint32_t *err = ctx->tickets + cpk::kTkErr;
@@ -1858,11 +1858,13 @@ int e3_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
                      (uint32_t)ntb, ctx->e3_tfirst, d_out_off, hint, err);
   if (ntb == 0) return hip_ok(hipGetLastError());
   uint64_t grid = (uint64_t)ctx->e3_grid;
+  if (grid > (uint64_t)cpk::kE3Threads * cpk::kE3MaxPer) grid = (uint64_t)cpk::kE3Threads * cpk::kE3MaxPer;
   if (grid > ntb) grid = ntb;
   hipLaunchKernelGGL(cpk::encode3_kernel, dim3((unsigned)grid), dim3(cpk::kE3Threads), cpk::kE3Lds,
                      s, (const uint64_t *)d_in, d_swo, n, (uint32_t)ntb,
                      (const uint32_t *)ctx->e3_tfirst, (uint8_t *)d_out, d_out_off,
-                     ctx->e3_status, ctx->e3_tstate, ctx->epoch, err);
+                     ctx->e3_status, ctx->e3_status + ctx->e3_cap, ctx->e3_tstate, ctx->epoch,
+                     err);
   return hip_ok(hipGetLastError());
 }
 }  // namespace
@@ -1949,7 +1951,9 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
                                                      cpk::kE3Threads, cpk::kE3Lds) != hipSuccess ||
         occ < 1)
       occ = 1;
-    if (occ > 1) occ -= 1;
+    const char *rs = getenv("CPK_E3_RESERVE");  // blocks per CU kept in reserve (tuning)
+    const int reserve = rs ? atoi(rs) : 1;
+    if (occ > reserve) occ -= reserve;
     c->e3_grid = occ * c->cus;
   }
   *out = c;

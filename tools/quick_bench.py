@@ -24,33 +24,38 @@ handles = []
 import os
 for spec in libs:
     # "lib.so@1": context created with CPK_ENCODER=1 (workgroup-per-piece encoder)
+    # "lib.so@3:CPK_E3_RESERVE=0,CPK_DECODER=3": encoder 3 plus env knobs read at ctx creation
     lp, _, enc = spec.partition("@")
+    enc, _, envs = enc.partition(":")
     os.environ["CPK_ENCODER"] = enc or "1"
+    for kv in filter(None, envs.split(",")):
+        k, _, v = kv.partition("=")
+        os.environ[k] = v
     cp._lib = None
     L = cp.load(Path(lp), strict=False)
     ctx = cp.Context(0)
-    handles.append((Path(lp).name + (f"@{enc}" if enc else ""), L, ctx))
+    handles.append((spec.split("/")[-1], L, ctx))
 for cfg in cfgs:
     cp._lib = handles[0][1]
     handles[0][2].generate(cp.preset(cfg), d_swo, d_in)
     torch.cuda.synchronize()
-    res = {h[0]: ([], []) for h in handles}
-    for rnd in range(6):
-        for name, L, ctx in handles:
-            cp._lib = L
-            ctx._lib = L
+    U = n * 65536
+    print(f"config {cfg}: n={n}", flush=True)
+    for name, L, ctx in handles:
+        cp._lib = L
+        ctx._lib = L
+        te, td = [], []
+        for rnd in range(6):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            ctx._lib = L
             e[0].record(); ctx.encode_batch(d_in, d_swo, hint, d_pk, d_off); e[1].record()
             ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st); e[2].record()
             torch.cuda.synchronize()
             if rnd:
-                res[name][0].append(e[0].elapsed_time(e[1])); res[name][1].append(e[1].elapsed_time(e[2]))
-    U = n * 65536
-    P = int(d_off[-1].item())
-    cnt.zero_(); handles[-1][2].count_mismatch(d_in, d_out, n * 8192, cnt)
-    print(f"config {cfg}: n={n} P/U={P / U:.4f} mismatch={int(cnt.item())} badst={int((d_st != 0).sum().item())}")
-    for name, (te, td) in res.items():
+                te.append(e[0].elapsed_time(e[1])); td.append(e[1].elapsed_time(e[2]))
+        err = ctx.take_error() if hasattr(L, "cpk_ctx_take_error") else 0
+        cnt.zero_(); ctx.count_mismatch(d_in, d_out, n * 8192, cnt)
+        P = int(d_off[-1].item())
         me, md = np.median(te), np.median(td)
-        print(f"  {name:36s} enc {me:8.3f} ms ({U / me / 1e6:7.1f} GB/s)  dec {md:8.3f} ms ({U / md / 1e6:7.1f} GB/s)"
-              f"  rt {U / (me + md) / 1e6 / 1.073741824:7.1f} GiB/s")
+        print(f"  {name:44s} enc {me:8.3f} ms ({U / me / 1e6:7.1f} GB/s)  dec {md:8.3f} ms ({U / md / 1e6:7.1f} GB/s)"
+              f"  rt {U / (me + md) / 1e6 / 1.073741824:7.1f} GiB/s  P/U={P / U:.4f} mism={int(cnt.item())}"
+              f" bad={int((d_st != 0).sum().item())} err={err}", flush=True)
