@@ -128,7 +128,7 @@ __device__ E3St e3_tile_entry(const uint64_t *tstate, uint32_t t, uint32_t ep, u
     const uint64_t v = uni64(ld_status(const_cast<uint64_t *>(&tstate[t - 1])));
     if ((uint32_t)(v >> 48) == ep) return e3_st_unpack(v);
     if (++spins > (1u << 16)) {  // cannot happen with a co-resident grid (~0.1 s)
-      if (lane == 0) atomicOr(err, 2u);
+      if (lane == 0) atomicOr(err, 4u);
       E3St s = {2, 0, 0};
       return s;
     }
@@ -247,7 +247,7 @@ __device__ uint64_t e3_lookback(uint64_t *status, uint32_t t, uint64_t agg, uint
     }
     if (__ballot(z)) {
       if (++spins > (1u << 16)) {  // cannot happen with a co-resident grid (~0.1 s)
-        if (lane == 0) atomicOr(err, 2u);
+        if (lane == 0) atomicOr(err, 4u);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(kE3Threads, CPK_E3_WPE) void encode3_kernel(
           for (int j = 0; j < kE3MaxPer; ++j) miss = miss || e3_flag(la[j], ep) == 0;
           if (!__syncthreads_or(miss)) break;
           if (++spins > (1u << 16)) {  // cannot happen with a co-resident grid
-            if (tid == 0) atomicOr(err, 2u);
+            if (tid == 0) atomicOr(err, 4u);
             break;
           }
           __builtin_amdgcn_s_sleep(2);

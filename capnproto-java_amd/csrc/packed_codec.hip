@@ -1367,18 +1367,24 @@ __device__ __forceinline__ int wave_min(int v) {
   return v;
 }
 
-// record length in bytes of the record whose tag is at piece position q
-__device__ __forceinline__ uint32_t rec_len(const uint8_t *pkw, uint32_t q) {
-  const uint32_t tag = pkw[q];
-  if (tag == 0) return 2;
-  if (tag == 0xffu) return 10 + 8u * pkw[q + 9];
-  return 1 + __builtin_popcount(tag);
+// The record whose tag is at piece position q: its byte length and output
+// words (PackedInputStream.java:82-134).  The tag and both possible count
+// bytes are read together: one LDS round trip per record on the walks.
+struct DecRec {
+  uint32_t len, nw;
+};
+__device__ __forceinline__ DecRec rec_at(const uint8_t *pkw, uint32_t q) {
+  const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+  DecRec r;
+  r.len = tag == 0 ? 2u : (tag == 0xffu ? 10u + 8u * c9 : 1u + __builtin_popcount(tag));
+  r.nw = 1u + (tag == 0 ? c1 : (tag == 0xffu ? c9 : 0u));
+  return r;
 }
 
 // 8 bytes at piece position x: from the LDS window when loaded, otherwise
 // (tail of a literal run reaching past the window) straight from memory
 __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32_t lend,
-                                         const uint8_t *gpiece) {
+                                         const uint8_t *gpiece, uint32_t glim) {
   uint32_t d0, d1, d2, sh;
   if (x + 12 <= lend) {
     // piece-relative dword grid (the LDS copy may sit at any byte phase)
@@ -1388,13 +1394,16 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
     d1 = p[1];
     d2 = p[2];
   } else {
-    // address-aligned dwords of the packed buffer
+    // address-aligned dwords of the packed buffer, none at or past the
+    // readable limit glim (piece-relative: the piece's end rounded up to a
+    // 16-byte line; bytes there are never part of a valid record)
     const uintptr_t g = reinterpret_cast<uintptr_t>(gpiece + x);
     const uint32_t *p = reinterpret_cast<const uint32_t *>(g & ~(uintptr_t)3);
     sh = (uint32_t)(g & 3);
-    d0 = p[0];
-    d1 = p[1];
-    d2 = sh ? p[2] : 0u;
+    const int64_t xa = (int64_t)x - sh;  // piece position of p[0] (>= -3: the
+    d0 = xa < glim ? p[0] : 0u;           // bytes before the piece are the buffer's)
+    d1 = xa + 4 < glim ? p[1] : 0u;
+    d2 = (sh && xa + 8 < glim) ? p[2] : 0u;
   }
   const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
   const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
@@ -1453,6 +1462,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       continue;
     }
     const uint8_t *gp = packed + a;
+    const uint32_t glim = (uint32_t)(((a + P + 15) & ~15ull) - a);  // readable bytes
     uint64_t *dst = out + w0;
     int st = CPK_OK;
     uint32_t e = 0;  // true tag position (piece-relative)
@@ -1484,64 +1494,72 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       // ---- 1: speculative chunk walks --------------------------------------
       const uint32_t cb = e + 32 * lane;
       const uint32_t ce = min(cb + 32, wend);
-      uint32_t vis = 0, X = cb;
+      uint32_t vis = 0, X = cb, wt = 0;  // wt: output words of the walk
       if (cb < wend) {
         uint32_t pos = cb;
         while (pos < ce) {
           vis |= 1u << (pos - cb);
-          pos += rec_len(pkw, pos);
+          const DecRec r = rec_at(pkw, pos);
+          wt += r.nw;
+          pos += r.len;
         }
         X = pos;
       }
       visa[lane] = vis;
       wave_lds_sync();
       // ---- 2: walk on until landing on a visited position -------------------
-      uint32_t S = X;
+      uint32_t S = X, lw = 0;  // lw: output words of the landing walk
       if (cb < wend) {
         while (S < wend) {
           const uint32_t r = S - e;
           if ((visa[r >> 5] >> (r & 31)) & 1) break;
-          S += rec_len(pkw, S);
+          const DecRec rr = rec_at(pkw, S);
+          lw += rr.nw;
+          S += rr.len;
         }
       }
       WPH(2)
-      // ---- 3: true chain over lanes (scalar) --------------------------------
-      uint64_t onmask = 0;
-      uint32_t entry = e;
-      uint32_t enext;
-      {
-        int cur = 0;
-        for (;;) {
-          onmask |= 1ull << cur;
-          const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)S, cur);
-          if (s >= wend) {
-            enext = s;
-            break;
-          }
-          const int nx = (int)((s - e) >> 5);
-          if (lane == nx) entry = s;
-          cur = nx;
+      // ---- 3: true chain over lanes -----------------------------------------
+      // lane j's successor is the owner of its landing point (always a later
+      // lane); the true records are on the lanes reachable from lane 0, found
+      // by pointer doubling (6 rounds cover a chain of 64)
+      int nx = (cb < wend && S < wend) ? (int)((S - e) >> 5) : 64;
+      uint64_t R = 1ull << lane;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const int src = (nx & 63) << 2;
+        const uint32_t rlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)R);
+        const uint32_t rhi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(R >> 32));
+        const int nn = __builtin_amdgcn_ds_bpermute(src, nx);
+        if (nx < 64) {
+          R |= ((uint64_t)rhi << 32) | rlo;
+          nx = nn;
         }
       }
+      const uint64_t onmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)R, 0)) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(R >> 32), 0) << 32);
+      const uint32_t enext =
+          (uint32_t)__builtin_amdgcn_readlane((int)S, 63 - __builtin_clzll(onmask));
+      // each on-path lane hands its landing point to its successor
+      wave_lds_sync();  // (phase 2's reads of visa are done)
+      if (((onmask >> lane) & 1) && S < wend) visa[(S - e) >> 5] = S;
+      wave_lds_sync();
+      const uint32_t entry = lane == 0 ? e : visa[lane];
       const bool on = (onmask >> lane) & 1;
       WPH(3)
       // ---- 4: output words of each lane's true records ----------------------
+      // [entry, S) = the walk's records from entry (a position the walk
+      // visited) plus the landing walk: the walk's words minus those before
+      // entry (usually one or two records of a false start)
       int myw = 0;
       if (on) {
-        for (uint32_t q = entry; q < S;) {
-          const uint32_t tag = pkw[q];
-          if (tag == 0) {
-            myw += 1 + pkw[q + 1];
-            q += 2;
-          } else if (tag == 0xffu) {
-            const uint32_t rn = pkw[q + 9];
-            myw += 1 + (int)rn;
-            q += 10 + 8 * rn;
-          } else {
-            myw += 1;
-            q += 1 + __builtin_popcount(tag);
-          }
+        uint32_t pre = 0;
+        for (uint32_t q = cb; q < entry;) {
+          const DecRec r = rec_at(pkw, q);
+          pre += r.nw;
+          q += r.len;
         }
+        myw = (int)(wt - pre + lw);
       }
       const int inc = wave_incl_add(myw);
       const int T = readlane(inc, 63);
@@ -1550,24 +1568,20 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       // ---- 5: error checks, block map, expansion (rounds of 2048 words) -----
       bool failed = false;
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
+      // errors and the filling record can only occur in a window reaching the
+      // piece's last word or within one window plus one record of its end
+      const bool chk = (ow + T >= W) || (P - e < 3 * kWin);
       for (int rb = 0; rb < T; rb += kRound) {
         int err = 0x7fffffff;
         if (on) {
           int o = o0;
           for (uint32_t q = entry; q < S;) {
-            const uint32_t tag = pkw[q];
+            const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
             const uint32_t ntag = 1 + __builtin_popcount(tag);
-            int nw = 1;
-            uint32_t adv = ntag;
-            if (tag == 0) {
-              nw = 1 + pkw[q + 1];
-              adv = 2;
-            } else if (tag == 0xffu) {
-              nw = 1 + pkw[q + 9];
-              adv = 10 + 8 * (uint32_t)(nw - 1);
-            }
+            const int nw = 1 + (int)(tag == 0 ? c1 : (tag == 0xffu ? c9 : 0u));
+            const uint32_t adv = tag == 0 ? 2u : (tag == 0xffu ? 10u + 8u * c9 : ntag);
             const int oo = ow + o;
-            if (rb == 0 && oo < W && err == 0x7fffffff) {
+            if (chk && rb == 0 && oo < W && err == 0x7fffffff) {
               // PackedInputStream.java:53-138: truncated tag bytes / count /
               // literal run -> EOF DecodeException; run past the piece ->
               // DecodeException / BufferOverflowException
@@ -1625,9 +1639,9 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
               const uint32_t rn = pkw[q + 9];
               nw = 1 + (int)rn;
               adv = 10 + 8 * rn;
-              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp);
+              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim);
             } else {
-              const uint64_t raw = read8(pkw, q + 1, lend, gp);
+              const uint64_t raw = read8(pkw, q + 1, lend, gp, glim);
               const uint64_t sel = lut[tag];
               const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
               const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
@@ -2065,9 +2079,10 @@ int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
       hipStreamSynchronize(s) != hipSuccess)
     return CPK_EDEVICE;
   if (e && hipMemsetAsync(ctx->tickets + cpk::kTkErr, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
-  // bit 0: a piece over its size hint; bit 1: a look-back wait timed out
-  // (a grid larger than the device holds at once -- cannot happen by design)
-  return e ? ((e & 2u) ? CPK_EDEVICE : CPK_EINVAL) : CPK_OK;
+  // bits 0, 1: a piece over its size hint (encoder / tile plan); bit 2: a
+  // cross-workgroup wait timed out (a grid larger than the device holds at
+  // once -- cannot happen by design)
+  return e ? ((e & 4u) ? CPK_EDEVICE : CPK_EINVAL) : CPK_OK;
 }
 
 int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off,

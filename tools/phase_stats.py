@@ -1,5 +1,5 @@
 """Per-phase cycle shares of the codec kernels (diagnostic stats build).
-Usage: python tools/phase_stats.py [config] [segments]"""
+Usage: python tools/phase_stats.py [config] [segments] [lib]"""
 import ctypes, sys
 from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
@@ -9,7 +9,7 @@ import capnp_packed as cp
 
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
-L = cp.load(REPO / "capnproto-java_amd" / "lib" / "libcapnp_packed_hip_stats.so")
+L = cp.load(Path(sys.argv[3]) if len(sys.argv) > 3 else REPO / "build" / "variants" / "stats.so")
 L.cpk_debug_phase_stats.argtypes = [ctypes.c_void_p]
 ctx = cp.Context(0)
 swo = np.arange(0, (n + 1) * 8192, 8192, dtype=np.uint64)
