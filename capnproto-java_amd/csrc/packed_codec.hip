@@ -1384,12 +1384,13 @@ __device__ __forceinline__ DecRec rec_at(const uint8_t *pkw, uint32_t q) {
 // 8 bytes at piece position x: from the LDS window when loaded, otherwise
 // (tail of a literal run reaching past the window) straight from memory
 __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32_t lend,
-                                         const uint8_t *gpiece, uint32_t glim) {
+                                         const uint8_t *gpiece, uint32_t glim, uint32_t ph) {
   uint32_t d0, d1, d2, sh;
   if (x + 12 <= lend) {
-    // piece-relative dword grid (the LDS copy may sit at any byte phase)
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(pkw + (x & ~3u));
-    sh = x & 3;
+    // LDS-aligned dwords: piece position x sits at byte phase (x + ph) & 3
+    // of the 16-byte aligned window buffer
+    sh = (x + ph) & 3;
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(pkw + (x - sh));
     d0 = p[0];
     d1 = p[1];
     d2 = p[2];
@@ -1488,6 +1489,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       // pkw[q] = packed byte q (signed 64-bit offset: ebase is negative when
       // the piece starts mid-line)
       const uint8_t *pkw = wbuf + (int64_t)padw - (int64_t)e;
+      const uint32_t ph = (padw - e) & 3;  // LDS byte phase of piece position 0
       wave_lds_sync();
 
       WPH(1)
@@ -1639,9 +1641,9 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
               const uint32_t rn = pkw[q + 9];
               nw = 1 + (int)rn;
               adv = 10 + 8 * rn;
-              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim);
+              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph);
             } else {
-              const uint64_t raw = read8(pkw, q + 1, lend, gp, glim);
+              const uint64_t raw = read8(pkw, q + 1, lend, gp, glim, ph);
               const uint64_t sel = lut[tag];
               const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
               const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
