@@ -271,7 +271,7 @@ __device__ __forceinline__ void e3_store_bytes(uint8_t *out, uint32_t *ring, uin
     const uint32_t d = (lane & 8) ? ((lane & 4) ? val.w : val.z) : ((lane & 4) ? val.y : val.x);
     out[L * 16 + lane] = (uint8_t)(d >> (8 * (lane & 3)));
   }
-  wave_lds_sync();
+  wave_lds_order();
   if (lane == 0) *rl = make_uint4(0u, 0u, 0u, 0u);
 }
 
@@ -616,7 +616,7 @@ __device__ __forceinline__ void e3_strings(const uint64_t *__restrict__ in,
           for (uint32_t j = lo_i; j <= n && swo[j] == gk; ++j) out_off[j] = rpos + o;
         }
         rpos += stot;
-        wave_lds_sync();
+        wave_lds_order();
         e3_flush(out, ring, fl, rpos >> 4, obase, lane);
       }
 

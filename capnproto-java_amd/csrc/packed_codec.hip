@@ -204,6 +204,13 @@ __device__ void fill_luts(uint64_t *lut, bool expand) {
   }
 }
 
+// Orders this wave's LDS accesses without waiting for them: DS instructions
+// of one wave execute in issue order, so a later read sees earlier writes
+// and atomics of every lane; only the compiler must not reorder across.
+__device__ __forceinline__ void wave_lds_order() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ void wave_lds_sync() {
   // DS ops of one wave complete in order; this only stops the compiler
   // moving LDS accesses across the point and drains this lane's queue.
@@ -1350,8 +1357,14 @@ __global__ __launch_bounds__(kPlanThreads) void tile_plan_kernel(
 //      gather-expand the blocks (PackedInputStream.java:82-134 per word).
 // No barriers: 32 pieces in flight per CU hide every LDS / HBM latency.
 constexpr int kDecThreads = 256;               // 4 independent waves
-constexpr uint32_t kWin = 2048;                // packed bytes resolved per window
-constexpr uint32_t kWinBuf = 2112;             // + pad (<= 15) + 64 read slack
+#ifndef CPK_DEC_CHUNK
+#define CPK_DEC_CHUNK 32
+#endif
+// Lane chunks of 28 bytes (7 dwords): the 64 walks start on 64 different LDS
+// banks (a 32-byte chunk put 8 lanes on every bank: 8-way conflicts)
+constexpr uint32_t kDecChunk = CPK_DEC_CHUNK;
+constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per window
+constexpr uint32_t kWinBuf = (kWin + 15 + 32 + 16 + 15) & ~15u;  // + pad, look-ahead, slack
 constexpr int kRound = 2048;                   // output words expanded per round
 constexpr uint32_t kDecWaveLds = kWinBuf + 4 * (kRound / 8) + 256;  // 3392
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;                // 15,616
@@ -1480,7 +1493,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       // ---- window load: LDS byte x <-> packed[(a + e) & ~15 + x] ----------
       const uint32_t padw = (uint32_t)((a + e) & 15);
       const uint32_t ebase = e - padw;  // piece position of wbuf[0]
-      const uint32_t need = min(e + kWin + 32, P) - ebase;  // <= 2095 bytes
+      const uint32_t need = min(e + kWin + 32, P) - ebase;  // <= kWin + 47 bytes
       const uint32_t lines = (need + 15) >> 4;
       const uint4 *gsrc = reinterpret_cast<const uint4 *>(gp - padw + e);
       for (uint32_t L = lane; L < lines; L += 64)
@@ -1490,12 +1503,12 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       // the piece starts mid-line)
       const uint8_t *pkw = wbuf + (int64_t)padw - (int64_t)e;
       const uint32_t ph = (padw - e) & 3;  // LDS byte phase of piece position 0
-      wave_lds_sync();
+      wave_lds_order();
 
       WPH(1)
       // ---- 1: speculative chunk walks --------------------------------------
-      const uint32_t cb = e + 32 * lane;
-      const uint32_t ce = min(cb + 32, wend);
+      const uint32_t cb = e + kDecChunk * lane;
+      const uint32_t ce = min(cb + kDecChunk, wend);
       uint32_t vis = 0, X = cb, wt = 0;  // wt: output words of the walk
       if (cb < wend) {
         uint32_t pos = cb;
@@ -1508,13 +1521,14 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
         X = pos;
       }
       visa[lane] = vis;
-      wave_lds_sync();
+      wave_lds_order();
       // ---- 2: walk on until landing on a visited position -------------------
       uint32_t S = X, lw = 0;  // lw: output words of the landing walk
       if (cb < wend) {
         while (S < wend) {
           const uint32_t r = S - e;
-          if ((visa[r >> 5] >> (r & 31)) & 1) break;
+          const uint32_t ow_ = r / kDecChunk;
+          if ((visa[ow_] >> (r - ow_ * kDecChunk)) & 1) break;
           const DecRec rr = rec_at(pkw, S);
           lw += rr.nw;
           S += rr.len;
@@ -1525,7 +1539,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       // lane j's successor is the owner of its landing point (always a later
       // lane); the true records are on the lanes reachable from lane 0, found
       // by pointer doubling (6 rounds cover a chain of 64)
-      int nx = (cb < wend && S < wend) ? (int)((S - e) >> 5) : 64;
+      int nx = (cb < wend && S < wend) ? (int)((S - e) / kDecChunk) : 64;
       uint64_t R = 1ull << lane;
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
@@ -1543,9 +1557,9 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       const uint32_t enext =
           (uint32_t)__builtin_amdgcn_readlane((int)S, 63 - __builtin_clzll(onmask));
       // each on-path lane hands its landing point to its successor
-      wave_lds_sync();  // (phase 2's reads of visa are done)
-      if (((onmask >> lane) & 1) && S < wend) visa[(S - e) >> 5] = S;
-      wave_lds_sync();
+      wave_lds_order();  // (phase 2's reads of visa are done)
+      if (((onmask >> lane) & 1) && S < wend) visa[(S - e) / kDecChunk] = S;
+      wave_lds_order();
       const uint32_t entry = lane == 0 ? e : visa[lane];
       const bool on = (onmask >> lane) & 1;
       WPH(3)
@@ -1616,7 +1630,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
           }
           fin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u(fin));
         }
-        wave_lds_sync();
+        wave_lds_order();
         WPH(5)
         const int nb = (min(min(kRound, T - rb), W - ow - rb) + 7) >> 3;
         for (int b = lane; b < nb; b += 64) {
@@ -1677,7 +1691,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
               if (i < kw) d[i] = words[i];
           }
         }
-        wave_lds_sync();  // blk reused by the next round
+        wave_lds_order();  // blk reused by the next round
         WPH(6)
       }
       if (failed) break;

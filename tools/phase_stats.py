@@ -31,6 +31,12 @@ ctx.encode_batch(d_in, d_swo, 8192, d_pk, d_off)
 ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
 torch.cuda.synchronize()
 L.cpk_debug_phase_stats(buf.ctypes.data)
+e1names = ["ticket", "load+classify", "roles", "long stretches", "bytes+zero stage", "strings to LDS", "look-back", "store"]
+v = buf[0:len(e1names)].astype(float)
+tot = v.sum()
+print(f"encode (v1, wave 0 of each workgroup): total {tot / 1e6:.1f} Mcycles; per piece {tot / n:.0f} cyc")
+for nm, x in zip(e1names, v):
+    print(f"   {nm:22s} {100 * x / max(tot, 1):6.2f} %   {x / n:8.0f} cyc/piece")
 e2names = ["ticket+setup", "load+classify", "exit/entry state", "roles", "look-back", "strings+store"]
 v = buf[32:32 + len(e2names)].astype(float)
 tot = v.sum()
