@@ -39,7 +39,7 @@ constexpr int kTileWords = kWaves * kWaveWords; // 8192
 constexpr int kBig = 0x3fffffff;
 // encoder geometry: 1024 threads, 8 words per lane (2 chunks of 4)
 #ifndef CPK_ENC_WPE
-#define CPK_ENC_WPE 4  // waves per SIMD the encoder's registers must allow
+#define CPK_ENC_WPE 8  // waves per SIMD the encoder's registers must allow (2 workgroups per CU)
 #endif
 constexpr int kEncThreads = 1024;
 constexpr int kEncWaves = kEncThreads / 64;                 // 16
@@ -892,17 +892,12 @@ __global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
       const uint64_t lo64 = s01 << sh;
       const uint64_t hi64 = ((uint64_t)d2 << sh) | (sh ? (s01 >> (64 - sh)) : 0ull);
       uint32_t *dst = stage32 + (o >> 2);
-      const int end = (o & 3) + (int)nb;  // bytes covered from dst[0]
+      // four unconditional ORs into the zeroed stage (the bytes past the
+      // string are zero): no exec-mask branches around the LDS ops
       atomicOr(&dst[0], (uint32_t)lo64);
-      if (end > 4) {
-        if (end >= 8) dst[1] = (uint32_t)(lo64 >> 32);
-        else atomicOr(&dst[1], (uint32_t)(lo64 >> 32));
-      }
-      if (end > 8) {
-        if (end >= 12) dst[2] = (uint32_t)hi64;
-        else atomicOr(&dst[2], (uint32_t)hi64);
-      }
-      if (end > 12) atomicOr(&dst[3], (uint32_t)(hi64 >> 32));
+      atomicOr(&dst[1], (uint32_t)(lo64 >> 32));
+      atomicOr(&dst[2], (uint32_t)hi64);
+      atomicOr(&dst[3], (uint32_t)(hi64 >> 32));
       __builtin_amdgcn_sched_barrier(0);  // one step at a time: bounds VGPRs
     }
     PH(5)
@@ -1397,23 +1392,24 @@ __device__ __forceinline__ DecRec rec_at(const uint8_t *pkw, uint32_t q) {
 // 8 bytes at piece position x: from the LDS window when loaded, otherwise
 // (tail of a literal run reaching past the window) straight from memory
 __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32_t lend,
-                                         const uint8_t *gpiece, uint32_t glim, uint32_t ph) {
-  uint32_t d0, d1, d2, sh;
-  if (x + 12 <= lend) {
-    // LDS-aligned dwords: piece position x sits at byte phase (x + ph) & 3
-    // of the 16-byte aligned window buffer
-    sh = (x + ph) & 3;
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(pkw + (x - sh));
-    d0 = p[0];
-    d1 = p[1];
-    d2 = p[2];
-  } else {
+                                         const uint8_t *gpiece, uint32_t glim, uint32_t ph,
+                                         uint32_t e) {
+  // The LDS read is unconditional (position clamped to the window start e,
+  // which has 12 buffer bytes after it whatever the window's size): with
+  // both reads under one branch hipcc merged them into flat loads.
+  // LDS-aligned dwords: piece position x sits at byte phase (x + ph) & 3 of
+  // the 16-byte aligned window buffer.
+  const bool inw = x + 12 <= lend;
+  const uint32_t xl = inw ? x : e;
+  uint32_t sh = (xl + ph) & 3;
+  const uint32_t *pl = reinterpret_cast<const uint32_t *>(pkw + ((int64_t)xl - sh));  // (signed: xl < sh)
+  uint32_t d0 = pl[0], d1 = pl[1], d2 = pl[2];
+  if (!inw) {
     // address-aligned dwords of the packed buffer, none at or past the
     // readable limit glim (piece-relative: the piece's end rounded up to a
     // 16-byte line; bytes there are never part of a valid record)
-    const uintptr_t g = reinterpret_cast<uintptr_t>(gpiece + x);
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(g & ~(uintptr_t)3);
-    sh = (uint32_t)(g & 3);
+    sh = (uint32_t)(reinterpret_cast<uintptr_t>(gpiece + x) & 3);
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(gpiece + ((int64_t)x - sh));  // (stays global)
     const int64_t xa = (int64_t)x - sh;  // piece position of p[0] (>= -3: the
     d0 = xa < glim ? p[0] : 0u;           // bytes before the piece are the buffer's)
     d1 = xa + 4 < glim ? p[1] : 0u;
@@ -1655,9 +1651,9 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
               const uint32_t rn = pkw[q + 9];
               nw = 1 + (int)rn;
               adv = 10 + 8 * rn;
-              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph);
+              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
             } else {
-              const uint64_t raw = read8(pkw, q + 1, lend, gp, glim, ph);
+              const uint64_t raw = read8(pkw, q + 1, lend, gp, glim, ph, e);
               const uint64_t sel = lut[tag];
               const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
               const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
