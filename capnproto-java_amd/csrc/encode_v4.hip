@@ -1,0 +1,410 @@
+// Encoder v4: one wave per piece, two streaming passes, no cross-workgroup
+// waits.  Included from packed_codec.hip (namespace cpk).
+//
+//   e4_size_kernel   each wave takes pieces from per-XCD tickets and walks
+//                    its piece in 64-word steps (lane = word), carrying the
+//                    run state in SGPRs from step to step: word class, run
+//                    boundaries, the roles of PackedOutputStream.java:64-193
+//                    per word, and the packed size of the piece;
+//   e4_scan_*        exclusive scan of the sizes -> out_off[0..n];
+//   e4_emit_kernel   the same walk again, now with the piece's output offset
+//                    known: every word's packed string (tag, v_perm-compacted
+//                    bytes, count) is OR-ed into a 2 KiB LDS ring at its byte
+//                    position and complete 16-byte lines stream to memory.
+//                    A head's count needs the end of its run, at most 256
+//                    words on: the emit walk classifies 4 steps ahead.
+// Traffic: U + (U + P) instead of U + P, in exchange for no barriers, no
+// look-back and every wave independent (both passes are pure streams).
+
+constexpr int kE4Waves = 4;
+constexpr int kE4Threads = 64 * kE4Waves;
+constexpr uint32_t kE4RingBytes = 2048;  // output ring per wave (<= 41 live lines)
+constexpr uint32_t kE4oLut = 0;                                   // u64[256]
+constexpr uint32_t kE4oRing = 2048;                               // u32[waves][512]
+constexpr uint32_t kE4Lds = kE4oRing + kE4Waves * kE4RingBytes;   // 10 KiB
+static_assert(kE4RingBytes == kE3RingBytes, "the v3 ring helpers are reused");
+
+#ifndef CPK_E4_WPE
+#define CPK_E4_WPE 8
+#endif
+
+// Run state entering a step (wave-uniform): g 0 zero run, 1 D/L stretch,
+// 2 none (piece start or after an M word); len: words of the run before the
+// step; hd: D/L stretch only, words since its last 0xFF head (capped at 256),
+// 0 = no head yet (PackedOutputStream.java:143-161).
+struct E4St {
+  int g, len, hd;
+};
+
+// Classification of one step: run boundaries B (a word whose run starts
+// there: group change, every M word, the piece's first word), D words
+// (tag 0xff), D/L words, and BV = B plus the words past the piece's end.
+struct E4Cls {
+  uint64_t B, D, DL, BV;
+};
+
+__device__ __forceinline__ int e4_group(uint32_t m, bool valid) {
+  return !valid ? 3 : (m == 0 ? 0 : (__builtin_popcount(m) >= 7 ? 1 : 2));
+}
+
+// gl: group of the word before the step (2 at the piece start); updated to
+// the group of the step's last word (2 for M or past the end)
+__device__ __forceinline__ E4Cls e4_classify(uint64_t word, bool valid, int &gl) {
+  const uint32_t m = e3_tag(word);
+  const int g = e4_group(m, valid);
+  const int gp = wave_shr1(g, gl);
+  E4Cls c;
+  c.B = __ballot(valid && (g != gp || g == 2));
+  c.D = __ballot(valid && m == 0xffu);
+  c.DL = __ballot(g == 1);
+  c.BV = c.B | __ballot(!valid);
+  const int g63 = __builtin_amdgcn_readlane(g, 63);
+  gl = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
+  return c;
+}
+
+// Roles of one step's words (lane = word; PackedOutputStream.java:119-193
+// restated per word, as encode_kernel's pass 2):
+//   Z word: a 0x00 head every 256 words from its zero run's start (2 bytes);
+//   M word: 1 + popcount bytes;
+//   D/L word: a member of the 0xFF run of the stretch's last head (8 bytes
+//   verbatim) if one lies within 255 words before it, else a head (D: 10
+//   bytes with the count, L: 8).
+// nb = packed bytes, memb / head flags; st advances to the next step.
+struct E4Role {
+  uint32_t nb, memb, head;
+};
+__device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &c, E4St &st,
+                                           int lane, uint64_t lem) {
+  const int g = e4_group(m, valid);
+  // this lane's run start (step-relative; the carried run started st.len
+  // words before the step) and the last D before this lane
+  const uint64_t bl = c.B & lem;
+  const int rs = bl ? 63 - __builtin_clzll(bl) : -st.len;
+  const uint64_t dl = c.D & (lem >> 1);
+  const int lastD = dl ? 63 - __builtin_clzll(dl) : (st.hd > 0 ? -st.hd : -(1 << 30));
+  const uint32_t zh = (g == 0 && ((lane - rs) & 255) == 0) ? 1u : 0u;
+  uint32_t memb = (g == 1 && lastD >= rs) ? 1u : 0u;
+  uint32_t dh = (valid && m == 0xffu && !memb) ? 1u : 0u;
+  const int f = c.BV ? __builtin_ctzll(c.BV) : 64;  // words [0, f) continue the carried run
+  int h1 = -1;
+  if (st.g == 1 && st.len + f > 256) {
+    // the carried stretch is longer than 256 words: members lie within 255
+    // words after a head, the next head is the first D 256 or more words
+    // after the last (:143-161)
+    const uint64_t rng = f >= 64 ? ~0ull : ((1ull << f) - 1);
+    uint64_t mc = 0;
+    if (st.hd > 0 && st.hd <= 255) {
+      const int me = 255 - st.hd;
+      mc = me >= 63 ? ~0ull : ((2ull << me) - 1);
+    }
+    const int js = st.hd > 0 ? max(0, 256 - st.hd) : 0;
+    const uint64_t dc = js >= 64 ? 0ull : (c.D & rng & (~0ull << js));
+    if (dc) {
+      h1 = __builtin_ctzll(dc);
+      mc |= h1 == 63 ? 0ull : (~0ull << (h1 + 1));
+    }
+    if ((rng >> lane) & 1) {
+      memb = ((mc & c.DL) >> lane) & 1;
+      dh = (h1 == lane) ? 1u : 0u;
+    }
+  }
+  E4Role r;
+  r.nb = !valid ? 0u : (g == 2 ? 1 + __builtin_popcount(m) : (g == 1 ? 8 + 2 * dh : 2 * zh));
+  r.memb = memb;
+  r.head = zh | dh;
+  // the run state entering the next step
+  if (c.B) {
+    const int lb = 63 - __builtin_clzll(c.B);
+    const int g63 = __builtin_amdgcn_readlane(g, 63);
+    st.g = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
+    st.len = 64 - lb;
+    st.hd = 0;
+    if (st.g == 1) {
+      const uint64_t dd = c.D & (~0ull << lb);
+      st.hd = dd ? 64 - __builtin_ctzll(dd) : 0;
+    }
+  } else if (st.g != 2) {
+    st.len += 64;
+    if (st.g == 1) {
+      if (h1 >= 0) st.hd = 64 - h1;
+      else if (st.hd > 0) st.hd = min(st.hd + 64, 256);
+      else st.hd = c.D ? 64 - __builtin_ctzll(c.D) : 0;
+    }
+  }
+  return r;
+}
+
+// next piece for this wave from the per-XCD counters (as the decoder)
+__device__ __forceinline__ uint32_t e4_next_piece(uint32_t *ticket, int &xq, int &dry, uint32_t n) {
+  uint32_t seg;
+  for (;;) {
+    seg = take_ticket(ticket, xq);
+    if (seg < n || ++dry >= 8) break;
+    xq = (xq + 1) & 7;
+  }
+  return seg;
+}
+
+// ---- pass 1: packed size of every piece --------------------------------------
+__global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
+    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
+    uint64_t *__restrict__ sizes, uint32_t *ticket, uint64_t hint, uint32_t *err) {
+  const int lane = lane_id();
+  const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  int xq = xcc_id(), dry = 0;
+  for (;;) {
+    const uint32_t seg = e4_next_piece(ticket, xq, dry, n);
+    if (seg >= n) break;
+    const uint64_t w0 = swo[seg];
+    const uint64_t W = swo[seg + 1] - w0;
+    if (hint && W > hint && lane == 0) atomicOr(err, 1u);
+    const uint64_t *src = in + w0;
+    E4St st = {2, 0, 0};
+    int gl = 2;
+    uint32_t acc = 0;
+    const uint64_t nsteps = (W + 63) >> 6;
+    for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
+      // four steps' loads in flight at once
+      uint64_t v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t k = ((s0 + j) << 6) + lane;
+        v[j] = k < W ? src[k] : 0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (s0 + j >= nsteps) break;
+        const uint64_t k = ((s0 + j) << 6) + lane;
+        const bool valid = k < W;
+        const E4Cls c = e4_classify(v[j], valid, gl);
+        const E4Role r = e4_roles(e3_tag(v[j]), valid, c, st, lane, lem);
+        acc += r.nb;
+      }
+    }
+    // wave sum in two 16-bit halves (a piece's packed size may pass 2^31)
+    const uint32_t thi = (uint32_t)wave_incl_add((int)(acc >> 16));
+    const uint32_t tlo = (uint32_t)wave_incl_add((int)(acc & 0xffffu));
+    if (lane == 63) sizes[seg] = ((uint64_t)thi << 16) + tlo;
+  }
+}
+
+// ---- exclusive scan of the sizes -> out_off[0..n] ------------------------------
+constexpr int kE4ScanThreads = 1024;
+constexpr int kE4ScanPer = 4;  // sizes per thread per block
+constexpr int kE4ScanBlock = kE4ScanThreads * kE4ScanPer;
+
+__device__ __forceinline__ uint64_t e4_block_scan(uint64_t x, uint64_t *sh, uint64_t &total) {
+  // inclusive scan over the block's 1024 threads (wave scans + one LDS pass)
+  const int lane = lane_id(), w = wave_id();
+  uint64_t v = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(v, d, 64);
+    if (lane >= d) v += y;
+  }
+  if (lane == 63) sh[w] = v;
+  __syncthreads();
+  if (w == 0) {
+    uint64_t t = lane < kE4ScanThreads / 64 ? sh[lane] : 0;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const uint64_t y = __shfl_up(t, d, 64);
+      if (lane >= d) t += y;
+    }
+    if (lane < kE4ScanThreads / 64) sh[16 + lane] = t;
+  }
+  __syncthreads();
+  total = sh[16 + kE4ScanThreads / 64 - 1];
+  const uint64_t r = v + (w ? sh[16 + w - 1] : 0);
+  __syncthreads();
+  return r;
+}
+
+// block sums of kE4ScanBlock sizes each
+__global__ __launch_bounds__(kE4ScanThreads) void e4_scan_reduce(const uint64_t *__restrict__ sizes,
+                                                                 uint32_t n, uint64_t *bsum) {
+  __shared__ uint64_t sh[32];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kE4ScanBlock;
+  uint64_t x = 0;
+#pragma unroll
+  for (int j = 0; j < kE4ScanPer; ++j) {
+    const uint64_t i = b0 + (uint64_t)j * kE4ScanThreads + threadIdx.x;
+    x += i < n ? sizes[i] : 0;
+  }
+  uint64_t total;
+  e4_block_scan(x, sh, total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// exclusive scan of the block sums in place (one block; nb <= 1024 * 16)
+__global__ __launch_bounds__(kE4ScanThreads) void e4_scan_top(uint64_t *bsum, uint32_t nb) {
+  __shared__ uint64_t sh[32];
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += kE4ScanThreads) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint64_t x = i < nb ? bsum[i] : 0;
+    uint64_t total;
+    const uint64_t inc = e4_block_scan(x, sh, total);
+    if (i < nb) bsum[i] = carry + inc - x;
+    carry += total;
+  }
+}
+
+// out_off[i] = exclusive prefix of sizes, out_off[n] = total
+__global__ __launch_bounds__(kE4ScanThreads) void e4_scan_down(const uint64_t *__restrict__ sizes,
+                                                               uint32_t n, const uint64_t *bsum,
+                                                               uint64_t *__restrict__ out_off) {
+  __shared__ uint64_t sh[32];
+  // thread t owns sizes b0 + t*kE4ScanPer .. +kE4ScanPer-1 (contiguous)
+  const uint64_t b0 = (uint64_t)blockIdx.x * kE4ScanBlock;
+  const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kE4ScanPer;
+  uint64_t x[kE4ScanPer], s = 0;
+#pragma unroll
+  for (int j = 0; j < kE4ScanPer; ++j) {
+    x[j] = i0 + j < n ? sizes[i0 + j] : 0;
+    s += x[j];
+  }
+  uint64_t total;
+  const uint64_t inc = e4_block_scan(s, sh, total);
+  uint64_t o = bsum[blockIdx.x] + inc - s;
+#pragma unroll
+  for (int j = 0; j < kE4ScanPer; ++j) {
+    if (i0 + j < n) out_off[i0 + j] = o;
+    o += x[j];
+    if (i0 + j + 1 == n) out_off[n] = o;
+  }
+}
+
+// ---- pass 2: the packed bytes ----------------------------------------------------
+// One step of the emit walk.  c[0] is this step's classification, bv1..bv4
+// the boundaries of the next four steps (for the counts of heads whose run
+// reaches past this step).
+__device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, const E4Cls &c,
+                                             uint64_t bv1, uint64_t bv2, uint64_t bv3,
+                                             uint64_t bv4, E4St &st, int lane, uint64_t lem,
+                                             const uint64_t *lut, uint32_t *ring, uint8_t *out,
+                                             uint64_t &rpos, uint64_t &fl, uint64_t obase) {
+  const uint32_t m = e3_tag(word);
+  const E4Role r = e4_roles(m, valid, c, st, lane, lem);
+  // a head's count: words to its run's end, at most 255 (:123-131, :143-164)
+  uint32_t cnt = 0;
+  if (__ballot(r.head)) {
+    const uint64_t gtm = lane == 63 ? 0ull : (~0ull << (lane + 1));
+    const uint64_t bb = c.BV & gtm;
+    const int nbr = bv1 ? 64 + __builtin_ctzll(bv1)
+                        : bv2 ? 128 + __builtin_ctzll(bv2)
+                              : bv3 ? 192 + __builtin_ctzll(bv3)
+                                    : bv4 ? 256 + __builtin_ctzll(bv4) : 320;
+    const int re = bb ? __builtin_ctzll(bb) : nbr;
+    cnt = r.head ? (uint32_t)min(255, re - lane - 1) : 0u;
+  }
+  // the string: tag, the nonzero bytes (v_perm with the compaction LUT), the
+  // count after a 0x00 / 0xFF tag; a literal-run member is its 8 bytes (:163-171)
+  const uint32_t lo = (uint32_t)word, hi = (uint32_t)(word >> 32);
+  const uint64_t sel = lut[m];
+  const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
+  const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+  const uint32_t c0p = m == 0 ? cnt : c0;
+  uint32_t s0 = m | (c0p << 8);
+  uint32_t s1 = __builtin_amdgcn_alignbyte(c1, c0p, 3);
+  uint32_t s2 = __builtin_amdgcn_alignbyte(m == 0xffu ? cnt : 0u, c1, 3);
+  if (r.memb) {
+    s0 = lo;
+    s1 = hi;
+    s2 = 0;
+  }
+  const uint32_t nb = r.nb;
+  const int incl = wave_incl_add((int)nb);
+  const uint32_t o = (uint32_t)incl - nb;
+  const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+  if (stot) {
+    // OR the string into the ring at its output position (the ring's lines
+    // are zero until written; bytes past a string are zero)
+    const uint32_t p = (uint32_t)rpos + o;
+    const uint32_t sh = (p & 3) * 8;
+    const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
+    const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
+    const uint32_t w3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
+    const uint32_t d0 = (p >> 2) & (kE3RingDw - 1);
+    if (nb) {
+      atomicOr(&ring[d0], (uint32_t)a01);
+      atomicOr(&ring[(d0 + 1) & (kE3RingDw - 1)], (uint32_t)(a01 >> 32));
+      atomicOr(&ring[(d0 + 2) & (kE3RingDw - 1)], (uint32_t)(a12 >> 32));
+      atomicOr(&ring[(d0 + 3) & (kE3RingDw - 1)], w3);
+    }
+    rpos += stot;
+    wave_lds_order();
+    e3_flush(out, ring, fl, rpos >> 4, obase, lane);
+  }
+}
+
+__global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
+    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
+    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint32_t *ticket) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint64_t *lut = reinterpret_cast<const uint64_t *>(smem + kE4oLut);
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kE4oRing + w * kE4RingBytes);
+  fill_luts(reinterpret_cast<uint64_t *>(smem + kE4oLut), false);
+  for (uint32_t i = lane; i < kE3RingLines; i += 64)
+    reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  int xq = xcc_id(), dry = 0;
+  for (;;) {
+    const uint32_t seg = e4_next_piece(ticket, xq, dry, n);
+    if (seg >= n) break;
+    const uint64_t w0 = swo[seg];
+    const uint64_t W = swo[seg + 1] - w0;
+    const uint64_t *src = in + w0;
+    const uint64_t obase = out_off[seg];
+    uint64_t rpos = obase, fl = obase >> 4;
+    E4St st = {2, 0, 0};
+    int gl = 2;
+    const uint64_t nsteps = (W + 63) >> 6;
+    // three groups of four steps in the pipeline: cur (emitted now), nxt
+    // (classified: the look-ahead of cur's heads), ld (loading)
+    uint64_t vc[4], vn[4], vl[4];
+    E4Cls cc[4], cn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t k = ((uint64_t)j << 6) + lane, k2 = ((uint64_t)(4 + j) << 6) + lane;
+      vc[j] = k < W ? src[k] : 0ull;
+      vn[j] = k2 < W ? src[k2] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cc[j] = e4_classify(vc[j], ((uint64_t)j << 6) + lane < W, gl);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cn[j] = e4_classify(vn[j], ((uint64_t)(4 + j) << 6) + lane < W, gl);
+    for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t k = ((s0 + 8 + j) << 6) + lane;
+        vl[j] = k < W ? src[k] : 0ull;
+      }
+      const uint64_t bvx[8] = {cc[0].BV, cc[1].BV, cc[2].BV, cc[3].BV,
+                               cn[0].BV, cn[1].BV, cn[2].BV, cn[3].BV};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (s0 + j < nsteps)
+          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W, cc[j], bvx[j + 1], bvx[j + 2],
+                       bvx[j + 3], bvx[j + 4], st, lane, lem, lut, ring, out, rpos, fl, obase);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vc[j] = vn[j];
+        cc[j] = cn[j];
+        vn[j] = vl[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cn[j] = e4_classify(vn[j], ((s0 + 8 + j) << 6) + lane < W, gl);
+    }
+    // the piece's last, partial line
+    if (rpos > fl * 16) {
+      const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
+      e3_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane);
+    }
+  }
+}

@@ -1772,6 +1772,7 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 }
 
 #include "encode_v3.hip"
+#include "encode_v4.hip"
 
 }  // namespace cpk
 
@@ -1944,7 +1945,7 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     // CPK_ENCODER=2 selects the wave-per-tile encoder (experimental: its
     // per-1024-word look-back does not scale yet)
     const char *e = getenv("CPK_ENCODER");
-    c->encoder = (e && e[0] == '3') ? 3 : (e && e[0] == '2') ? 2 : 1;
+    c->encoder = (e && e[0] == '4') ? 4 : (e && e[0] == '3') ? 3 : (e && e[0] == '2') ? 2 : 1;
   }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
@@ -2000,6 +2001,31 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
 
 int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
 
+// Encoder v4 (encode_v4.hip): size pass, scan, emit pass.  Pieces of any
+// size; the hint is only checked.
+int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, uint64_t hint,
+              void *d_out, uint64_t *d_out_off, hipStream_t s) {
+  const uint32_t nb = (uint32_t)((n + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
+  int rc = ensure_status(ctx, (uint64_t)n + nb + 1);
+  if (rc) return rc;
+  uint64_t *sizes = ctx->status, *bsum = ctx->status + n;
+  if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
+  unsigned grid = (unsigned)(8 * ctx->cus);
+  if (grid > (n + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (n + cpk::kE4Waves - 1) / cpk::kE4Waves;
+  hipLaunchKernelGGL(cpk::e4_size_kernel, dim3(grid), dim3(cpk::kE4Threads), 0, s,
+                     (const uint64_t *)d_in, d_swo, n, sizes, ctx->tickets + cpk::kTkEnc, hint,
+                     ctx->tickets + cpk::kTkErr);
+  hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
+                     (const uint64_t *)sizes, n, bsum);
+  hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bsum, nb);
+  hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
+                     (const uint64_t *)sizes, n, (const uint64_t *)bsum, d_out_off);
+  hipLaunchKernelGGL(cpk::e4_emit_kernel, dim3(grid), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
+                     (const uint64_t *)d_in, d_swo, n, (const uint64_t *)d_out_off,
+                     (uint8_t *)d_out, ctx->tickets + cpk::kTkDec);
+  return hip_ok(hipGetLastError());
+}
+
 int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n,
                      uint64_t max_seg_words, void *d_out, uint64_t *d_out_off, void *stream) {
   if (!ctx || (!d_swo && n) || !d_out_off) return CPK_EINVAL;
@@ -2008,6 +2034,7 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
   if (ctx->encoder == 3) return e3_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
+  if (ctx->encoder == 4) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
   // counters (not the error word: that is cleared by cpk_ctx_take_error)
   if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
   const bool v2 = ctx->encoder == 2;
