@@ -36,11 +36,12 @@ struct E4St {
   int g, len, hd;
 };
 
-// Classification of one step: run boundaries B (a word whose run starts
-// there: group change, every M word, the piece's first word), D words
-// (tag 0xff), D/L words, and BV = B plus the words past the piece's end.
+// Classification of one step: BV = run boundaries (a word whose run starts
+// there: group change, every M word, the piece's first word) plus the words
+// past the piece's end, and the D words (tag 0xff).  (A valid word's masks
+// below it never hold a past-the-end word, so BV serves as the boundaries.)
 struct E4Cls {
-  uint64_t B, D, DL, BV;
+  uint64_t D, BV;
 };
 
 __device__ __forceinline__ int e4_group(uint32_t m, bool valid) {
@@ -54,10 +55,8 @@ __device__ __forceinline__ E4Cls e4_classify(uint64_t word, bool valid, int &gl)
   const int g = e4_group(m, valid);
   const int gp = wave_shr1(g, gl);
   E4Cls c;
-  c.B = __ballot(valid && (g != gp || g == 2));
+  c.BV = __ballot(!valid || g != gp || g == 2);
   c.D = __ballot(valid && m == 0xffu);
-  c.DL = __ballot(g == 1);
-  c.BV = c.B | __ballot(!valid);
   const int g63 = __builtin_amdgcn_readlane(g, 63);
   gl = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
   return c;
@@ -79,7 +78,7 @@ __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &
   const int g = e4_group(m, valid);
   // this lane's run start (step-relative; the carried run started st.len
   // words before the step) and the last D before this lane
-  const uint64_t bl = c.B & lem;
+  const uint64_t bl = c.BV & lem;
   const int rs = bl ? 63 - __builtin_clzll(bl) : -st.len;
   const uint64_t dl = c.D & (lem >> 1);
   const int lastD = dl ? 63 - __builtin_clzll(dl) : (st.hd > 0 ? -st.hd : -(1 << 30));
@@ -104,8 +103,8 @@ __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &
       h1 = __builtin_ctzll(dc);
       mc |= h1 == 63 ? 0ull : (~0ull << (h1 + 1));
     }
-    if ((rng >> lane) & 1) {
-      memb = ((mc & c.DL) >> lane) & 1;
+    if ((rng >> lane) & 1) {  // (words of the carried stretch: all D/L)
+      memb = (mc >> lane) & 1;
       dh = (h1 == lane) ? 1u : 0u;
     }
   }
@@ -113,9 +112,9 @@ __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &
   r.nb = !valid ? 0u : (g == 2 ? 1 + __builtin_popcount(m) : (g == 1 ? 8 + 2 * dh : 2 * zh));
   r.memb = memb;
   r.head = zh | dh;
-  // the run state entering the next step
-  if (c.B) {
-    const int lb = 63 - __builtin_clzll(c.B);
+  // the run state entering the next step (past the piece's end: unused)
+  if (c.BV) {
+    const int lb = 63 - __builtin_clzll(c.BV);
     const int g63 = __builtin_amdgcn_readlane(g, 63);
     st.g = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
     st.len = 64 - lb;
@@ -164,23 +163,32 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     int gl = 2;
     uint32_t acc = 0;
     const uint64_t nsteps = (W + 63) >> 6;
+    // software pipeline: the next four steps' loads are in flight while
+    // these four are classified
+    uint64_t v[4], vn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t k = ((uint64_t)j << 6) + lane;
+      v[j] = k < W ? src[k] : 0ull;
+    }
     for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
-      // four steps' loads in flight at once
-      uint64_t v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint64_t k = ((s0 + j) << 6) + lane;
-        v[j] = k < W ? src[k] : 0ull;
+        const uint64_t k = ((s0 + 4 + j) << 6) + lane;
+        vn[j] = k < W ? src[k] : 0ull;
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (s0 + j >= nsteps) break;
         const uint64_t k = ((s0 + j) << 6) + lane;
         const bool valid = k < W;
-        const E4Cls c = e4_classify(v[j], valid, gl);
-        const E4Role r = e4_roles(e3_tag(v[j]), valid, c, st, lane, lem);
-        acc += r.nb;
+        if (s0 + j < nsteps) {
+          const E4Cls c = e4_classify(v[j], valid, gl);
+          const E4Role r = e4_roles(e3_tag(v[j]), valid, c, st, lane, lem);
+          acc += r.nb;
+        }
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = vn[j];
     }
     // wave sum in two 16-bit halves (a piece's packed size may pass 2^31)
     const uint32_t thi = (uint32_t)wave_incl_add((int)(acc >> 16));

@@ -341,3 +341,33 @@ def test_short_stretch_after_long(ctx, oracle):
             pieces.append(np.concatenate(p))
     data = np.concatenate(pieces)
     _check_batch(ctx, oracle, data, _swo([len(p) // 8 for p in pieces]))
+
+
+@pytest.mark.parametrize("enc", ["1", "2", "3", "4"])
+def test_every_encoder_matches_oracle(oracle, enc, monkeypatch):
+    """The opt-in encoders (CPK_ENCODER=1 workgroup per piece, 2 wave per
+    tile, 3 workgroup per 4096-word tile) and the default (4, size + emit
+    passes) on one mixed batch: pieces of 0..20000 words, long D/L stretches,
+    long zero runs."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    import capnp_packed as cp
+    monkeypatch.setenv("CPK_ENCODER", enc)
+    c = cp.Context(0)
+    try:
+        rng = np.random.default_rng(1234)
+        sizes = [0, 1, 63, 64, 65, 255, 256, 257, 8191, 8192, 8193, 20000] + \
+            list(rng.integers(0, 3000, size=24))
+        parts = []
+        for i, n in enumerate(sizes):
+            probs = [[.25, .25, .25, .25], [.01, .7, .285, .005], [.9, .04, .03, .03]][i % 3]
+            w = _random_words(rng, int(n), probs).reshape(-1, 8)
+            if i % 4 == 1 and n > 800:  # a D/L stretch of 600 words
+                w[100:700] = rng.integers(1, 256, size=(600, 8), dtype=np.uint8)
+                w[100:700:7, 3] = 0
+            parts.append(w.reshape(-1))
+        data = np.concatenate(parts)
+        _check_batch(c, oracle, data, _swo(sizes))
+    finally:
+        c.close()

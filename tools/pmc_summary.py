@@ -17,11 +17,14 @@ for f in sorted(root.glob("*/*_counter_collection.csv")):
     with open(f) as fh:
         for r in csv.DictReader(fh):
             k = r["Kernel_Name"]
-            short = ("encode_kernel" if "encode_kernel" in k else "decode_kernel" if "decode_kernel" in k
+            short = ("e4_size_kernel" if "e4_size_kernel" in k else "e4_emit_kernel" if "e4_emit_kernel" in k
+                     else "encode_kernel" if "encode_kernel" in k else "decode_kernel" if "decode_kernel" in k
+                     else "encode3_kernel" if "encode3_kernel" in k else "encode2_kernel" if "encode2_kernel" in k
                      else k.split("(")[0][-40:])
             vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
-for kern in ("encode_kernel", "decode_kernel"):
+for kern in ("encode_kernel", "encode2_kernel", "encode3_kernel", "e4_size_kernel", "e4_emit_kernel",
+                 "decode_kernel"):
     if kern not in vals:
         continue
     d = {c: sum(v) / len(v) for c, v in vals[kern].items()}
@@ -40,6 +43,10 @@ for kern in ("encode_kernel", "decode_kernel"):
                 print(f"  {c:22s} {100 * d[c] / wc:6.1f} % of wave cycles")
 if len(sys.argv) > 3 and sys.argv[2] == "--json":
     traffic = {}
+    # the v4 encode stage = size pass + emit pass: their traffic adds up
+    if "e4_size_kernel" in out and "e4_emit_kernel" in out:
+        out["encode_kernel"] = {c: out["e4_size_kernel"].get(c, 0) + out["e4_emit_kernel"].get(c, 0)
+                                for c in ("FETCH_SIZE", "WRITE_SIZE")}
     for kern, key in (("encode_kernel", "encode"), ("decode_kernel", "decode")):
         d = out.get(kern, {})
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
