@@ -42,6 +42,7 @@ struct E4St {
 // below it never hold a past-the-end word, so BV serves as the boundaries.)
 struct E4Cls {
   uint64_t D, BV;
+  int gl;  // group of the step's last word (2: M, or past the end)
 };
 
 __device__ __forceinline__ int e4_group(uint32_t m, bool valid) {
@@ -59,6 +60,7 @@ __device__ __forceinline__ E4Cls e4_classify(uint64_t word, bool valid, int &gl)
   c.D = __ballot(valid && m == 0xffu);
   const int g63 = __builtin_amdgcn_readlane(g, 63);
   gl = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
+  c.gl = gl;
   return c;
 }
 
@@ -78,15 +80,18 @@ __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &
   const int g = e4_group(m, valid);
   // this lane's run start (step-relative; the carried run started st.len
   // words before the step) and the last D before this lane
-  const uint64_t bl = c.BV & lem;
-  const int rs = bl ? 63 - __builtin_clzll(bl) : -st.len;
-  const uint64_t dl = c.D & (lem >> 1);
-  const int lastD = dl ? 63 - __builtin_clzll(dl) : (st.hd > 0 ? -st.hd : -(1 << 30));
+  // (__clzll(0) = 64: the highest set bit is -1 for an empty mask; plain
+  // selects on it, no exec-mask branches)
+  const int hb = 63 - __clzll((long long)(c.BV & lem));
+  const int rs = hb >= 0 ? hb : -st.len;
+  const int hd = 63 - __clzll((long long)(c.D & (lem >> 1)));
+  const int lastD = hd >= 0 ? hd : (st.hd > 0 ? -st.hd : -(1 << 30));
   const uint32_t zh = (g == 0 && ((lane - rs) & 255) == 0) ? 1u : 0u;
   uint32_t memb = (g == 1 && lastD >= rs) ? 1u : 0u;
   uint32_t dh = (valid && m == 0xffu && !memb) ? 1u : 0u;
-  const int f = c.BV ? __builtin_ctzll(c.BV) : 64;  // words [0, f) continue the carried run
   int h1 = -1;
+  // (st.len + f > 256 needs st.len > 192: f, the first boundary, is <= 64)
+  const int f = st.g == 1 && st.len > 192 && c.BV ? __builtin_ctzll(c.BV) : 64;
   if (st.g == 1 && st.len + f > 256) {
     // the carried stretch is longer than 256 words: members lie within 255
     // words after a head, the next head is the first D 256 or more words
@@ -103,26 +108,24 @@ __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &
       h1 = __builtin_ctzll(dc);
       mc |= h1 == 63 ? 0ull : (~0ull << (h1 + 1));
     }
-    if ((rng >> lane) & 1) {  // (words of the carried stretch: all D/L)
-      memb = (mc >> lane) & 1;
-      dh = (h1 == lane) ? 1u : 0u;
-    }
+    // (words of the carried stretch, all D/L; selects, not a branch)
+    const bool inr = (rng >> lane) & 1;
+    memb = inr ? (uint32_t)((mc >> lane) & 1) : memb;
+    dh = inr ? (h1 == lane ? 1u : 0u) : dh;
   }
   E4Role r;
-  r.nb = !valid ? 0u : (g == 2 ? 1 + __builtin_popcount(m) : (g == 1 ? 8 + 2 * dh : 2 * zh));
+  // (a sum of selects: nested per-lane ternaries become branches)
+  r.nb = (g == 2 ? 1u + __builtin_popcount(m) : 0u) + (g == 1 ? 8u + 2u * dh : 0u) +
+         (g == 0 ? 2u * zh : 0u);
   r.memb = memb;
   r.head = zh | dh;
   // the run state entering the next step (past the piece's end: unused)
   if (c.BV) {
     const int lb = 63 - __builtin_clzll(c.BV);
-    const int g63 = __builtin_amdgcn_readlane(g, 63);
-    st.g = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
+    st.g = c.gl;
     st.len = 64 - lb;
-    st.hd = 0;
-    if (st.g == 1) {
-      const uint64_t dd = c.D & (~0ull << lb);
-      st.hd = dd ? 64 - __builtin_ctzll(dd) : 0;
-    }
+    const uint64_t dd = c.D & (~0ull << lb);  // (a D there means a D/L run)
+    st.hd = dd ? 64 - __builtin_ctzll(dd) : 0;
   } else if (st.g != 2) {
     st.len += 64;
     if (st.g == 1) {
@@ -158,6 +161,10 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     const uint64_t w0 = swo[seg];
     const uint64_t W = swo[seg + 1] - w0;
     if (hint && W > hint && lane == 0) atomicOr(err, 1u);
+    if (W == 0) {  // an empty piece: no bytes (and no loads: it may sit at the end)
+      if (lane == 0) sizes[seg] = 0;
+      continue;
+    }
     const uint64_t *src = in + w0;
     E4St st = {2, 0, 0};
     int gl = 2;
@@ -166,17 +173,14 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     // software pipeline: the next four steps' loads are in flight while
     // these four are classified
     uint64_t v[4], vn[4];
+    // loads clamped to the piece's last word, not predicated (no exec-mask
+    // branches around them); words past the end are masked by `valid`
+    const uint64_t kl = W ? W - 1 : 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint64_t k = ((uint64_t)j << 6) + lane;
-      v[j] = k < W ? src[k] : 0ull;
-    }
+    for (int j = 0; j < 4; ++j) v[j] = src[min(((uint64_t)j << 6) + lane, kl)];
     for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint64_t k = ((s0 + 4 + j) << 6) + lane;
-        vn[j] = k < W ? src[k] : 0ull;
-      }
+      for (int j = 0; j < 4; ++j) vn[j] = src[min(((s0 + 4 + j) << 6) + lane, kl)];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint64_t k = ((s0 + j) << 6) + lane;
@@ -366,6 +370,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     if (seg >= n) break;
     const uint64_t w0 = swo[seg];
     const uint64_t W = swo[seg + 1] - w0;
+    if (W == 0) continue;  // no bytes; no loads (it may sit at the end of the input)
     const uint64_t *src = in + w0;
     const uint64_t obase = out_off[seg];
     uint64_t rpos = obase, fl = obase >> 4;
@@ -376,11 +381,11 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     // (classified: the look-ahead of cur's heads), ld (loading)
     uint64_t vc[4], vn[4], vl[4];
     E4Cls cc[4], cn[4];
+    const uint64_t kl = W ? W - 1 : 0;  // loads clamped, not predicated
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint64_t k = ((uint64_t)j << 6) + lane, k2 = ((uint64_t)(4 + j) << 6) + lane;
-      vc[j] = k < W ? src[k] : 0ull;
-      vn[j] = k2 < W ? src[k2] : 0ull;
+      vc[j] = src[min(((uint64_t)j << 6) + lane, kl)];
+      vn[j] = src[min(((uint64_t)(4 + j) << 6) + lane, kl)];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) cc[j] = e4_classify(vc[j], ((uint64_t)j << 6) + lane < W, gl);
@@ -388,10 +393,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     for (int j = 0; j < 4; ++j) cn[j] = e4_classify(vn[j], ((uint64_t)(4 + j) << 6) + lane < W, gl);
     for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint64_t k = ((s0 + 8 + j) << 6) + lane;
-        vl[j] = k < W ? src[k] : 0ull;
-      }
+      for (int j = 0; j < 4; ++j) vl[j] = src[min(((s0 + 8 + j) << 6) + lane, kl)];
       const uint64_t bvx[8] = {cc[0].BV, cc[1].BV, cc[2].BV, cc[3].BV,
                                cn[0].BV, cn[1].BV, cn[2].BV, cn[3].BV};
 #pragma unroll
