@@ -1361,7 +1361,11 @@ constexpr uint32_t kDecChunk = CPK_DEC_CHUNK;
 constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per window
 constexpr uint32_t kWinBuf = (kWin + 15 + 32 + 16 + 15) & ~15u;  // + pad, look-ahead, slack
 constexpr int kRound = 2048;                   // output words expanded per round
-constexpr uint32_t kDecWaveLds = kWinBuf + 4 * (kRound / 8) + 256;  // 3392
+#ifndef CPK_DEC_BLK
+#define CPK_DEC_BLK 4  // (4: 64 lanes cover a window's blocks in fewer, fuller passes; measured faster than 8)
+#endif
+constexpr int kBlk = CPK_DEC_BLK;  // output words per expansion block
+constexpr uint32_t kDecWaveLds = kWinBuf + 4 * (kRound / kBlk) + 256;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;                // 15,616
 
 __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
@@ -1438,7 +1442,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
   uint8_t *wl = smem + 2048 + w * kDecWaveLds;
   uint8_t *wbuf = wl;                                            // window bytes
   uint32_t *blk = reinterpret_cast<uint32_t *>(wl + kWinBuf);    // [256]
-  uint32_t *visa = blk + kRound / 8;                             // [64]
+  uint32_t *visa = blk + kRound / kBlk;                          // [64]
   fill_luts(lut, true);
   __syncthreads();  // the only block-wide barrier: LUT ready
   if (kStream && (blockIdx.x != 0 || w != 0)) return;
@@ -1611,8 +1615,8 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
             // blocks of this round whose first word this record covers
             const int lo = max(o, rb), hi = min(o + nw, rb + kRound);
             // window-relative record position (< 2 KiB) | offset in the run
-            for (int bb = (lo + 7) & ~7; bb < hi; bb += 8)
-              blk[(bb - rb) >> 3] = (q - e) | ((uint32_t)(bb - o) << 16);
+            for (int bb = (lo + kBlk - 1) & ~(kBlk - 1); bb < hi; bb += kBlk)
+              blk[(bb - rb) / kBlk] = (q - e) | ((uint32_t)(bb - o) << 16);
             o += nw;
             q += adv;
           }
@@ -1628,27 +1632,28 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
         }
         wave_lds_order();
         WPH(5)
-        const int nb = (min(min(kRound, T - rb), W - ow - rb) + 7) >> 3;
+        const int nb = (min(min(kRound, T - rb), W - ow - rb) + kBlk - 1) / kBlk;
         for (int b = lane; b < nb; b += 64) {
           const uint32_t v = blk[b];
           uint32_t q = e + (v & 0xffffu);
           int ofs = (int)(v >> 16);
-          const int wbase = ow + rb + 8 * b;  // piece word of the block's first word
-          uint64_t words[8];
+          const int wbase = ow + rb + kBlk * b;  // piece word of the block's first word
+          uint64_t words[kBlk];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
+          for (int i = 0; i < kBlk; ++i) {
             // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
             // run (tag word, then the counted words), or a tagged word
-            const uint32_t tag = pkw[q];
+            // (the count bytes are read with the tag: one LDS round trip)
+            const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
             uint64_t x;
             int nw;
             uint32_t adv;
             if (tag == 0) {
               x = 0;
-              nw = 1 + pkw[q + 1];
+              nw = 1 + c1;
               adv = 2;
             } else if (tag == 0xffu) {
-              const uint32_t rn = pkw[q + 9];
+              const uint32_t rn = c9;
               nw = 1 + (int)rn;
               adv = 10 + 8 * rn;
               x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
@@ -1669,11 +1674,11 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
               ofs = 0;
             }
           }
-          const int kw = min(8, min(ow + T, W) - wbase);
+          const int kw = min(kBlk, min(ow + T, W) - wbase);
           uint64_t *d = dst + wbase;
-          if (kw == 8 && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
+          if (kw == kBlk && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
 #pragma unroll
-            for (int i = 0; i < 8; i += 2) {
+            for (int i = 0; i < kBlk; i += 2) {
               uint4 v4;
               v4.x = (uint32_t)words[i];
               v4.y = (uint32_t)(words[i] >> 32);
@@ -1683,7 +1688,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
             }
           } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+            for (int i = 0; i < kBlk; ++i)
               if (i < kw) d[i] = words[i];
           }
         }
