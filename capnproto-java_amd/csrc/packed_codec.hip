@@ -1496,8 +1496,19 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       const uint32_t need = min(e + kWin + 32, P) - ebase;  // <= kWin + 47 bytes
       const uint32_t lines = (need + 15) >> 4;
       const uint4 *gsrc = reinterpret_cast<const uint4 *>(gp - padw + e);
-      for (uint32_t L = lane; L < lines; L += 64)
-        reinterpret_cast<uint4 *>(wbuf)[L] = gsrc[L];
+      // all of a lane's lines (<= 3) in flight at once, then the LDS writes:
+      // one memory latency per window instead of one per line
+      static_assert((kWin + 47 + 15) / 16 <= 3 * 64, "three lines per lane");
+      {
+        const uint32_t L0 = lane, L1 = lane + 64, L2 = lane + 128;
+        uint4 l0 = make_uint4(0u, 0u, 0u, 0u), l1 = l0, l2 = l0;
+        if (L0 < lines) l0 = gsrc[L0];
+        if (L1 < lines) l1 = gsrc[L1];
+        if (L2 < lines) l2 = gsrc[L2];
+        if (L0 < lines) reinterpret_cast<uint4 *>(wbuf)[L0] = l0;
+        if (L1 < lines) reinterpret_cast<uint4 *>(wbuf)[L1] = l1;
+        if (L2 < lines) reinterpret_cast<uint4 *>(wbuf)[L2] = l2;
+      }
       const uint32_t lend = ebase + 16 * lines;  // loaded piece positions < lend
       // pkw[q] = packed byte q (signed 64-bit offset: ebase is negative when
       // the piece starts mid-line)
