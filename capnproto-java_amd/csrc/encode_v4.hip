@@ -292,12 +292,22 @@ __global__ __launch_bounds__(kE4ScanThreads) void e4_scan_down(const uint64_t *_
 // One step of the emit walk.  c[0] is this step's classification, bv1..bv4
 // the boundaries of the next four steps (for the counts of heads whose run
 // reaches past this step).
-__device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, const E4Cls &c,
+__device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t bv0,
                                              uint64_t bv1, uint64_t bv2, uint64_t bv3,
                                              uint64_t bv4, E4St &st, int lane, uint64_t lem,
                                              const uint64_t *lut, uint32_t *ring, uint8_t *out,
                                              uint64_t &rpos, uint64_t &fl, uint64_t obase) {
   const uint32_t m = e3_tag(word);
+  // this step's classification: the boundaries came with the look-ahead
+  // (only they are kept for 4 steps: SGPR pressure), D and the last group
+  // are recomputed here
+  E4Cls c;
+  c.BV = bv0;
+  c.D = __ballot(valid && m == 0xffu);
+  {
+    const int g63 = __builtin_amdgcn_readlane(e4_group(m, valid), 63);
+    c.gl = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
+  }
   const E4Role r = e4_roles(m, valid, c, st, lane, lem);
   // a head's count: words to its run's end, at most 255 (:123-131, :143-164)
   uint32_t cnt = 0;
@@ -380,7 +390,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     // three groups of four steps in the pipeline: cur (emitted now), nxt
     // (classified: the look-ahead of cur's heads), ld (loading)
     uint64_t vc[4], vn[4], vl[4];
-    E4Cls cc[4], cn[4];
+    uint64_t cc[4], cn[4];  // boundaries (BV) of the cur / nxt steps
     const uint64_t kl = W ? W - 1 : 0;  // loads clamped, not predicated
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -388,19 +398,24 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
       vn[j] = src[min(((uint64_t)(4 + j) << 6) + lane, kl)];
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cc[j] = e4_classify(vc[j], ((uint64_t)j << 6) + lane < W, gl);
+    for (int j = 0; j < 4; ++j) cc[j] = e4_classify(vc[j], ((uint64_t)j << 6) + lane < W, gl).BV;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cn[j] = e4_classify(vn[j], ((uint64_t)(4 + j) << 6) + lane < W, gl);
+    for (int j = 0; j < 4; ++j)
+      cn[j] = e4_classify(vn[j], ((uint64_t)(4 + j) << 6) + lane < W, gl).BV;
     for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) vl[j] = src[min(((s0 + 8 + j) << 6) + lane, kl)];
-      const uint64_t bvx[8] = {cc[0].BV, cc[1].BV, cc[2].BV, cc[3].BV,
-                               cn[0].BV, cn[1].BV, cn[2].BV, cn[3].BV};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        // boundaries of steps j .. j+4 of this group and the next
+        const uint64_t b0 = cc[j];
+        const uint64_t b1 = j + 1 < 4 ? cc[(j + 1) & 3] : cn[(j + 1) & 3];
+        const uint64_t b2 = j + 2 < 4 ? cc[(j + 2) & 3] : cn[(j + 2) & 3];
+        const uint64_t b3 = j + 3 < 4 ? cc[(j + 3) & 3] : cn[(j + 3) & 3];
+        const uint64_t b4 = cn[j];
         if (s0 + j < nsteps)
-          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W, cc[j], bvx[j + 1], bvx[j + 2],
-                       bvx[j + 3], bvx[j + 4], st, lane, lem, lut, ring, out, rpos, fl, obase);
+          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W, b0, b1, b2, b3, b4, st, lane, lem, lut,
+                       ring, out, rpos, fl, obase);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -409,7 +424,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
         vn[j] = vl[j];
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cn[j] = e4_classify(vn[j], ((s0 + 8 + j) << 6) + lane < W, gl);
+      for (int j = 0; j < 4; ++j) cn[j] = e4_classify(vn[j], ((s0 + 8 + j) << 6) + lane < W, gl).BV;
     }
     // the piece's last, partial line
     if (rpos > fl * 16) {
