@@ -75,24 +75,31 @@ __device__ __forceinline__ E4Cls e4_classify(uint64_t word, bool valid, int &gl)
 struct E4Role {
   uint32_t nb, memb, head;
 };
+// per lane: mask bit set ? b : a, as one v_cndmask
+__device__ __forceinline__ int e4_vsel(int a, int b, uint64_t mask) {
+  int r;
+  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
+  return r;
+}
 __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &c, E4St &st,
                                            int lane, uint64_t lem) {
   const int g = e4_group(m, valid);
   // this lane's run start (step-relative; the carried run started st.len
   // words before the step) and the last D before this lane
-  // (__clzll(0) = 64: the highest set bit is -1 for an empty mask; plain
-  // selects on it, no exec-mask branches)
-  const int hb = 63 - __clzll((long long)(c.BV & lem));
-  const int rs = hb >= 0 ? hb : -st.len;
-  const int hd = 63 - __clzll((long long)(c.D & (lem >> 1)));
-  const int lastD = hd >= 0 ? hd : (st.hd > 0 ? -st.hd : -(1 << 30));
+  // (__clzll(0) = 64: the highest set bit is -1 for an empty mask; the
+  // selects are forced v_cndmasks: hipcc otherwise branches on the mask)
+  const uint64_t bl = c.BV & lem, dl = c.D & (lem >> 1);
+  const int rs = e4_vsel(63 - __clzll((long long)bl), -st.len, __ballot(bl == 0));
+  const int lastD = e4_vsel(63 - __clzll((long long)dl), st.hd > 0 ? -st.hd : -(1 << 30),
+                            __ballot(dl == 0));
   const uint32_t zh = (g == 0 && ((lane - rs) & 255) == 0) ? 1u : 0u;
   uint32_t memb = (g == 1 && lastD >= rs) ? 1u : 0u;
   uint32_t dh = (valid && m == 0xffu && !memb) ? 1u : 0u;
   int h1 = -1;
   // (st.len + f > 256 needs st.len > 192: f, the first boundary, is <= 64)
-  const int f = st.g == 1 && st.len > 192 && c.BV ? __builtin_ctzll(c.BV) : 64;
-  if (st.g == 1 && st.len + f > 256) {
+  if (st.g == 1 && st.len > 192) {
+   const int f = c.BV ? __builtin_ctzll(c.BV) : 64;  // words [0, f) continue the carried run
+   if (st.len + f > 256) {
     // the carried stretch is longer than 256 words: members lie within 255
     // words after a head, the next head is the first D 256 or more words
     // after the last (:143-161)
@@ -112,6 +119,7 @@ __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &
     const bool inr = (rng >> lane) & 1;
     memb = inr ? (uint32_t)((mc >> lane) & 1) : memb;
     dh = inr ? (h1 == lane ? 1u : 0u) : dh;
+   }
   }
   E4Role r;
   // (a sum of selects: nested per-lane ternaries become branches)
