@@ -1387,9 +1387,11 @@ struct DecRec {
 };
 __device__ __forceinline__ DecRec rec_at(const uint8_t *pkw, uint32_t q) {
   const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+  // masks, not nested selects (hipcc turns those into exec-mask branches)
+  const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
   DecRec r;
-  r.len = tag == 0 ? 2u : (tag == 0xffu ? 10u + 8u * c9 : 1u + __builtin_popcount(tag));
-  r.nw = 1u + (tag == 0 ? c1 : (tag == 0xffu ? c9 : 0u));
+  r.len = 1u + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
+  r.nw = 1u + (zm & c1) + (fm & c9);
   return r;
 }
 
@@ -1605,8 +1607,9 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
           for (uint32_t q = entry; q < S;) {
             const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
             const uint32_t ntag = 1 + __builtin_popcount(tag);
-            const int nw = 1 + (int)(tag == 0 ? c1 : (tag == 0xffu ? c9 : 0u));
-            const uint32_t adv = tag == 0 ? 2u : (tag == 0xffu ? 10u + 8u * c9 : ntag);
+            const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+            const int nw = 1 + (int)((zm & c1) + (fm & c9));
+            const uint32_t adv = ntag + (zm & 1u) + (fm & (8u * c9 + 1u));
             const int oo = ow + o;
             if (chk && rb == 0 && oo < W && err == 0x7fffffff) {
               // PackedInputStream.java:53-138: truncated tag bytes / count /
