@@ -20,6 +20,7 @@
 //                  pointer-doubling validation, then a gather-expand of every
 //                  8-word output block from its covering record.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1337,26 +1338,28 @@ __global__ __launch_bounds__(kPlanThreads) void tile_plan_kernel(
 
 // ------------------------------------------------------------ decoder
 // Wave-per-piece decoder.  Each wave owns one piece at a time and consumes
-// its packed bytes in windows of 2 KiB starting at a known tag position e:
-//   1. lane l walks its 32-byte chunk [e + 32l, e + 32l + 32) from the
-//      chunk start, speculatively treating it as a tag; visited positions
-//      form a 32-bit mask per lane;
-//   2. from its exit, each lane walks on until it lands on a position some
-//      lane visited (the two walks coincide from there: the tag chain is a
+// its packed bytes in windows of 64 chunks starting at a known tag position e:
+//   1. lane l walks its chunk [e + Cl, e + Cl + C) from the chunk start,
+//      speculatively treating it as a tag; visited positions form a bit mask
+//      per lane, and the walk tallies its output words;
+//   2. from its exit, each lane walks on until it lands on a position its
+//      owner visited (the two walks coincide from there: the tag chain is a
 //      function of the position);
-//   3. starting from lane 0 (whose chunk starts at the true tag e) the lane
-//      chain lane -> owner of its landing point gives every true record;
-//   4. on-path lanes re-walk their true records, count output words (wave
-//      scan), check the reference's error conditions, and write, for every
-//      8-word output block, the record covering it; all 64 lanes then
+//   3. the lanes reachable from lane 0 (whose chunk starts at the true tag e)
+//      under "lane -> owner of its landing point" hold every true record
+//      (pointer doubling);
+//   4. on-path lanes' word counts -> wave scan; they re-walk their true
+//      records to check the reference's error conditions and write, for
+//      every 4-word output block, the record covering it; all 64 lanes then
 //      gather-expand the blocks (PackedInputStream.java:82-134 per word).
-// No barriers: 32 pieces in flight per CU hide every LDS / HBM latency.
+// No barriers: up to 32 pieces in flight per CU.
 constexpr int kDecThreads = 256;               // 4 independent waves
 #ifndef CPK_DEC_CHUNK
-#define CPK_DEC_CHUNK 32
+#define CPK_DEC_CHUNK 48
 #endif
-// Lane chunks of 28 bytes (7 dwords): the 64 walks start on 64 different LDS
-// banks (a 32-byte chunk put 8 lanes on every bank: 8-way conflicts)
+// Lane chunks C of 48 bytes (3 KiB windows, 6 workgroups per CU by LDS):
+// measured against 28 / 32 / 64 at 131,072 pieces, 48 is fastest on configs
+// 2 and 3 (config 2 decode 5.07 -> 4.82 ms), 6 % slower on the sparse config 4
 constexpr uint32_t kDecChunk = CPK_DEC_CHUNK;
 constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per window
 constexpr uint32_t kWinBuf = (kWin + 15 + 32 + 16 + 15) & ~15u;  // + pad, look-ahead, slack
@@ -1365,7 +1368,11 @@ constexpr int kRound = 2048;                   // output words expanded per roun
 #define CPK_DEC_BLK 4  // (4: 64 lanes cover a window's blocks in fewer, fuller passes; measured faster than 8)
 #endif
 constexpr int kBlk = CPK_DEC_BLK;  // output words per expansion block
-constexpr uint32_t kDecWaveLds = kWinBuf + 4 * (kRound / kBlk) + 256;
+// a lane's visited positions: one bit per chunk byte
+typedef std::conditional<(kDecChunk <= 32), uint32_t, uint64_t>::type VisMask;
+static_assert(kDecChunk <= 64, "visited mask bits");
+constexpr uint32_t kDecWaveLds = kWinBuf + 4 * (kRound / kBlk) + 64 * sizeof(VisMask);
+constexpr int kWinLinesPerLane = (int)((kWin + 47 + 15) / 16 + 63) / 64;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;                // 15,616
 
 __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
@@ -1444,7 +1451,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
   uint8_t *wl = smem + 2048 + w * kDecWaveLds;
   uint8_t *wbuf = wl;                                            // window bytes
   uint32_t *blk = reinterpret_cast<uint32_t *>(wl + kWinBuf);    // [256]
-  uint32_t *visa = blk + kRound / kBlk;                          // [64]
+  VisMask *visa = reinterpret_cast<VisMask *>(blk + kRound / kBlk);  // [64]
   fill_luts(lut, true);
   __syncthreads();  // the only block-wide barrier: LUT ready
   if (kStream && (blockIdx.x != 0 || w != 0)) return;
@@ -1500,16 +1507,18 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       const uint4 *gsrc = reinterpret_cast<const uint4 *>(gp - padw + e);
       // all of a lane's lines (<= 3) in flight at once, then the LDS writes:
       // one memory latency per window instead of one per line
-      static_assert((kWin + 47 + 15) / 16 <= 3 * 64, "three lines per lane");
       {
-        const uint32_t L0 = lane, L1 = lane + 64, L2 = lane + 128;
-        uint4 l0 = make_uint4(0u, 0u, 0u, 0u), l1 = l0, l2 = l0;
-        if (L0 < lines) l0 = gsrc[L0];
-        if (L1 < lines) l1 = gsrc[L1];
-        if (L2 < lines) l2 = gsrc[L2];
-        if (L0 < lines) reinterpret_cast<uint4 *>(wbuf)[L0] = l0;
-        if (L1 < lines) reinterpret_cast<uint4 *>(wbuf)[L1] = l1;
-        if (L2 < lines) reinterpret_cast<uint4 *>(wbuf)[L2] = l2;
+        uint4 l[kWinLinesPerLane];
+#pragma unroll
+        for (int j = 0; j < kWinLinesPerLane; ++j) {
+          const uint32_t L = lane + 64 * j;
+          l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < kWinLinesPerLane; ++j) {
+          const uint32_t L = lane + 64 * j;
+          if (L < lines) reinterpret_cast<uint4 *>(wbuf)[L] = l[j];
+        }
       }
       const uint32_t lend = ebase + 16 * lines;  // loaded piece positions < lend
       // pkw[q] = packed byte q (signed 64-bit offset: ebase is negative when
@@ -1522,11 +1531,12 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       // ---- 1: speculative chunk walks --------------------------------------
       const uint32_t cb = e + kDecChunk * lane;
       const uint32_t ce = min(cb + kDecChunk, wend);
-      uint32_t vis = 0, X = cb, wt = 0;  // wt: output words of the walk
+      VisMask vis = 0;
+      uint32_t X = cb, wt = 0;  // wt: output words of the walk
       if (cb < wend) {
         uint32_t pos = cb;
         while (pos < ce) {
-          vis |= 1u << (pos - cb);
+          vis |= (VisMask)1 << (pos - cb);
           const DecRec r = rec_at(pkw, pos);
           wt += r.nw;
           pos += r.len;
@@ -1571,9 +1581,9 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
           (uint32_t)__builtin_amdgcn_readlane((int)S, 63 - __builtin_clzll(onmask));
       // each on-path lane hands its landing point to its successor
       wave_lds_order();  // (phase 2's reads of visa are done)
-      if (((onmask >> lane) & 1) && S < wend) visa[(S - e) / kDecChunk] = S;
+      if (((onmask >> lane) & 1) && S < wend) visa[(S - e) / kDecChunk] = (VisMask)S;
       wave_lds_order();
-      const uint32_t entry = lane == 0 ? e : visa[lane];
+      const uint32_t entry = lane == 0 ? e : (uint32_t)visa[lane];
       const bool on = (onmask >> lane) & 1;
       WPH(3)
       // ---- 4: output words of each lane's true records ----------------------
@@ -2153,8 +2163,10 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
     return CPK_EDEVICE;
-  // persistent: 8 blocks of 4 independent waves per CU (32 pieces in flight)
-  unsigned grid = (unsigned)(8 * ctx->cus);
+  // persistent: up to 8 blocks of 4 independent waves per CU (32 pieces in
+  // flight), as many as the LDS holds
+  const unsigned per_cu = (unsigned)min(8u, 160u * 1024u / cpk::kDecLds);
+  unsigned grid = per_cu * (unsigned)ctx->cus;
   if (grid > (n + 3) / 4) grid = (n + 3) / 4;
   hipLaunchKernelGGL(cpk::decode_kernel<false>, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
                      (const uint8_t *)d_packed, const_cast<uint64_t *>(d_in_off), d_swo, n,
