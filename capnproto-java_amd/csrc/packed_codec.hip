@@ -1363,7 +1363,10 @@ constexpr int kDecThreads = 256;               // 4 independent waves
 constexpr uint32_t kDecChunk = CPK_DEC_CHUNK;
 constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per window
 constexpr uint32_t kWinBuf = (kWin + 15 + 32 + 16 + 15) & ~15u;  // + pad, look-ahead, slack
-constexpr int kRound = 2048;                   // output words expanded per round
+#ifndef CPK_DEC_ROUND
+#define CPK_DEC_ROUND 1536  // (7 workgroups per CU with 48-byte chunks; 2048: 6, 1024: more rounds)
+#endif
+constexpr int kRound = CPK_DEC_ROUND;  // output words expanded per round
 #ifndef CPK_DEC_BLK
 #define CPK_DEC_BLK 4  // (4: 64 lanes cover a window's blocks in fewer, fuller passes; measured faster than 8)
 #endif
