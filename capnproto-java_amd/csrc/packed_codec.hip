@@ -1364,7 +1364,7 @@ constexpr uint32_t kDecChunk = CPK_DEC_CHUNK;
 constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per window
 constexpr uint32_t kWinBuf = (kWin + 15 + 32 + 16 + 15) & ~15u;  // + pad, look-ahead, slack
 #ifndef CPK_DEC_ROUND
-#define CPK_DEC_ROUND 1536  // (7 workgroups per CU with 48-byte chunks; 2048: 6, 1024: more rounds)
+#define CPK_DEC_ROUND 1280  // (8 workgroups per CU with 48-byte chunks; larger rounds cost occupancy)
 #endif
 constexpr int kRound = CPK_DEC_ROUND;  // output words expanded per round
 #ifndef CPK_DEC_BLK
@@ -1374,7 +1374,10 @@ constexpr int kBlk = CPK_DEC_BLK;  // output words per expansion block
 // a lane's visited positions: one bit per chunk byte
 typedef std::conditional<(kDecChunk <= 32), uint32_t, uint64_t>::type VisMask;
 static_assert(kDecChunk <= 64, "visited mask bits");
-constexpr uint32_t kDecWaveLds = kWinBuf + 4 * (kRound / kBlk) + 64 * sizeof(VisMask);
+// the visited masks (phases 1-3) and the block map (phase 5) share LDS
+constexpr uint32_t kDecWaveLds = kWinBuf + (4 * (kRound / kBlk) > 64 * sizeof(VisMask)
+                                                ? 4 * (kRound / kBlk)
+                                                : 64 * sizeof(VisMask));
 constexpr int kWinLinesPerLane = (int)((kWin + 47 + 15) / 16 + 63) / 64;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;                // 15,616
 
@@ -1454,7 +1457,7 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
   uint8_t *wl = smem + 2048 + w * kDecWaveLds;
   uint8_t *wbuf = wl;                                            // window bytes
   uint32_t *blk = reinterpret_cast<uint32_t *>(wl + kWinBuf);    // [256]
-  VisMask *visa = reinterpret_cast<VisMask *>(blk + kRound / kBlk);  // [64]
+  VisMask *visa = reinterpret_cast<VisMask *>(blk);  // [64], over the block map
   fill_luts(lut, true);
   __syncthreads();  // the only block-wide barrier: LUT ready
   if (kStream && (blockIdx.x != 0 || w != 0)) return;
