@@ -159,7 +159,8 @@ __device__ __forceinline__ uint32_t e4_next_piece(uint32_t *ticket, int &xq, int
 // ---- pass 1: packed size of every piece --------------------------------------
 __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
-    uint64_t *__restrict__ sizes, uint32_t *ticket, uint64_t hint, uint32_t *err) {
+    uint64_t *__restrict__ sizes, uint32_t *ticket, uint64_t hint, uint32_t *err,
+    uint64_t *__restrict__ bvbuf, uint64_t stride) {
   const int lane = lane_id();
   const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
   int xq = xcc_id(), dry = 0;
@@ -174,6 +175,11 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
       continue;
     }
     const uint64_t *src = in + w0;
+    // this piece's step rows in bvbuf: `stride` rows per piece when the
+    // size hint bounds them, else packed by word offset (disjoint: a piece
+    // adds at most one partial step)
+    uint64_t *bvp = bvbuf + (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
+    const uint64_t rows = stride ? stride : ~0ull;  // (a piece over the hint: error, no rows)
     E4St st = {2, 0, 0};
     int gl = 2;
     uint32_t acc = 0;
@@ -197,6 +203,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
           const E4Cls c = e4_classify(v[j], valid, gl);
           const E4Role r = e4_roles(e3_tag(v[j]), valid, c, st, lane, lem);
           acc += r.nb;
+          if (lane == 0 && s0 + j < rows) bvp[s0 + j] = c.BV;  // the emit pass's look-ahead
         }
       }
 #pragma unroll
@@ -376,7 +383,8 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
 
 __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
-    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint32_t *ticket) {
+    const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint32_t *ticket,
+    const uint64_t *__restrict__ bvbuf, uint64_t stride) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint64_t *lut = reinterpret_cast<const uint64_t *>(smem + kE4oLut);
   const int lane = lane_id();
@@ -398,46 +406,30 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     const uint64_t obase = out_off[seg];
     uint64_t rpos = obase, fl = obase >> 4;
     E4St st = {2, 0, 0};
-    int gl = 2;
+    // the boundaries of every step come from the size pass (bvbuf); past
+    // the piece every word is a boundary.  Words: this group of four steps
+    // and the next one's loads in flight.
     const uint64_t nsteps = (W + 63) >> 6;
-    // three groups of four steps in the pipeline: cur (emitted now), nxt
-    // (classified: the look-ahead of cur's heads), ld (loading)
-    uint64_t vc[4], vn[4], vl[4];
-    uint64_t cc[4], cn[4];  // boundaries (BV) of the cur / nxt steps
+    if (stride && nsteps > stride) continue;  // over the size hint: reported, output undefined
+    const uint64_t *bvp = bvbuf + (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
+    uint64_t vc[4], vl[4];
     const uint64_t kl = W ? W - 1 : 0;  // loads clamped, not predicated
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      vc[j] = src[min(((uint64_t)j << 6) + lane, kl)];
-      vn[j] = src[min(((uint64_t)(4 + j) << 6) + lane, kl)];
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cc[j] = e4_classify(vc[j], ((uint64_t)j << 6) + lane < W, gl).BV;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      cn[j] = e4_classify(vn[j], ((uint64_t)(4 + j) << 6) + lane < W, gl).BV;
+    for (int j = 0; j < 4; ++j) vc[j] = src[min(((uint64_t)j << 6) + lane, kl)];
     for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) vl[j] = src[min(((s0 + 8 + j) << 6) + lane, kl)];
+      for (int j = 0; j < 4; ++j) vl[j] = src[min(((s0 + 4 + j) << 6) + lane, kl)];
+      uint64_t bv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bv[j] = s0 + j < nsteps ? bvp[s0 + j] : ~0ull;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        // boundaries of steps j .. j+4 of this group and the next
-        const uint64_t b0 = cc[j];
-        const uint64_t b1 = j + 1 < 4 ? cc[(j + 1) & 3] : cn[(j + 1) & 3];
-        const uint64_t b2 = j + 2 < 4 ? cc[(j + 2) & 3] : cn[(j + 2) & 3];
-        const uint64_t b3 = j + 3 < 4 ? cc[(j + 3) & 3] : cn[(j + 3) & 3];
-        const uint64_t b4 = cn[j];
         if (s0 + j < nsteps)
-          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W, b0, b1, b2, b3, b4, st, lane, lem, lut,
-                       ring, out, rpos, fl, obase);
+          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W, bv[j], bv[j + 1], bv[j + 2], bv[j + 3],
+                       bv[j + 4], st, lane, lem, lut, ring, out, rpos, fl, obase);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        vc[j] = vn[j];
-        cc[j] = cn[j];
-        vn[j] = vl[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cn[j] = e4_classify(vn[j], ((s0 + 8 + j) << 6) + lane < W, gl).BV;
+      for (int j = 0; j < 4; ++j) vc[j] = vl[j];
     }
     wave_lds_order();
     e3_flush(out, ring, fl, rpos >> 4, obase, lane);

@@ -1827,6 +1827,8 @@ struct cpk_ctx_s {
   uint64_t e3_cap;        //   tiles the arrays hold (+2)
   uint32_t epoch;         //   launch epoch tagging the look-back words, 1..65535
   int e3_grid;            //   workgroups of encode3_kernel resident at once
+  uint64_t *e4_bv;        // encoder v4: run boundaries per 64-word step
+  uint64_t e4_bv_cap;     //   entries
 };
 
 namespace {
@@ -2031,25 +2033,49 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->e3_tfirst) hipFree(ctx->e3_tfirst);
   if (ctx->e3_status) hipFree(ctx->e3_status);
   if (ctx->e3_tstate) hipFree(ctx->e3_tstate);
+  if (ctx->e4_bv) hipFree(ctx->e4_bv);
   free(ctx);
 }
 
 int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
 
 // Encoder v4 (encode_v4.hip): size pass, scan, emit pass.  Pieces of any
-// size; the hint is only checked.
+// size; a piece over the hint is reported (output undefined).  The size pass
+// leaves each 64-word step's run boundaries for the emit pass: `stride` rows
+// per piece from the hint, or packed by word offset when there is no hint (the
+// batch's word count is then read back, synchronising the stream).
 int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, uint64_t hint,
               void *d_out, uint64_t *d_out_off, hipStream_t s) {
   const uint32_t nb = (uint32_t)((n + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
   int rc = ensure_status(ctx, (uint64_t)n + nb + 1);
   if (rc) return rc;
+  uint64_t stride = hint ? (hint + 63) / 64 : 0, rows;
+  if (stride && (uint64_t)n * stride > (1ull << 29)) stride = 0;  // (> 4 GiB of rows: pack them)
+  if (stride) {
+    rows = (uint64_t)n * stride;
+  } else {
+    uint64_t ends[2];
+    if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return CPK_EDEVICE;
+    rows = (ends[1] - ends[0]) / 64 + n + 1;
+  }
+  if (rows > ctx->e4_bv_cap) {
+    if (ctx->e4_bv) hipFree(ctx->e4_bv);
+    ctx->e4_bv = nullptr;
+    ctx->e4_bv_cap = 0;
+    const uint64_t cap = rows + rows / 4;
+    if (hipMalloc(&ctx->e4_bv, cap * 8) != hipSuccess) return CPK_ENOMEM;
+    ctx->e4_bv_cap = cap;
+  }
   uint64_t *sizes = ctx->status, *bsum = ctx->status + n;
   if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (n + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (n + cpk::kE4Waves - 1) / cpk::kE4Waves;
   hipLaunchKernelGGL(cpk::e4_size_kernel, dim3(grid), dim3(cpk::kE4Threads), 0, s,
                      (const uint64_t *)d_in, d_swo, n, sizes, ctx->tickets + cpk::kTkEnc, hint,
-                     ctx->tickets + cpk::kTkErr);
+                     ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride);
   hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
                      (const uint64_t *)sizes, n, bsum);
   hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bsum, nb);
@@ -2057,7 +2083,8 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
                      (const uint64_t *)sizes, n, (const uint64_t *)bsum, d_out_off);
   hipLaunchKernelGGL(cpk::e4_emit_kernel, dim3(grid), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
                      (const uint64_t *)d_in, d_swo, n, (const uint64_t *)d_out_off,
-                     (uint8_t *)d_out, ctx->tickets + cpk::kTkDec);
+                     (uint8_t *)d_out, ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv,
+                     stride);
   return hip_ok(hipGetLastError());
 }
 

@@ -83,12 +83,11 @@ int cpk_ctx_device(cpk_ctx ctx);
  *   d_in            : 8-byte aligned words; piece i is words
  *                     [d_seg_word_off[i], d_seg_word_off[i+1]).
  *   d_seg_word_off  : uint64[n+1], device.
- *   max_seg_words   : host bound on every piece's size in words, 0 = unknown.
- *                     A piece larger than a nonzero bound is reported by
- *                     cpk_ctx_take_error.  (The workgroup-per-piece encoder,
- *                     CPK_ENCODER=1, uses it to choose its tiled form and may
- *                     then read d_seg_word_off[0], [n] back, synchronising
- *                     `stream`; its output is undefined for such a piece.)
+ *   max_seg_words   : host bound on every piece's size in words, 0 = unknown
+ *                     (the call then reads d_seg_word_off[0], [n] back,
+ *                     synchronising `stream`).  A piece larger than a nonzero
+ *                     bound is reported by cpk_ctx_take_error (output
+ *                     undefined for that piece).
  *   d_out           : 16-byte aligned, capacity cpk_batch_packed_capacity().
  *   d_out_off       : uint64[n+1], device, written: piece i's packed bytes
  *                     are d_out[d_out_off[i] .. d_out_off[i+1]), contiguous
