@@ -195,6 +195,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) vn[j] = src[min(((s0 + 4 + j) << 6) + lane, kl)];
+      uint64_t bvg[4] = {~0ull, ~0ull, ~0ull, ~0ull};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint64_t k = ((s0 + j) << 6) + lane;
@@ -203,8 +204,13 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
           const E4Cls c = e4_classify(v[j], valid, gl);
           const E4Role r = e4_roles(e3_tag(v[j]), valid, c, st, lane, lem);
           acc += r.nb;
-          if (lane == 0 && s0 + j < rows) bvp[s0 + j] = c.BV;  // the emit pass's look-ahead
+          bvg[j] = c.BV;
         }
+      }
+      // the group's boundary rows for the emit pass: lanes 0-3, one store
+      {
+        const uint64_t x = lane == 0 ? bvg[0] : lane == 1 ? bvg[1] : lane == 2 ? bvg[2] : bvg[3];
+        if (lane < 4 && s0 + lane < nsteps && s0 + lane < rows) bvp[s0 + lane] = x;
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = vn[j];
