@@ -59,7 +59,7 @@ __device__ __forceinline__ E4Cls e4_classify(uint64_t word, bool valid, int &gl)
   c.BV = __ballot(!valid || g != gp || g == 2);
   c.D = __ballot(valid && m == 0xffu);
   const int g63 = __builtin_amdgcn_readlane(g, 63);
-  gl = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
+  gl = min(g63, 2);  // (3, past the end, counts as 2)
   c.gl = gl;
   return c;
 }
@@ -327,7 +327,7 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
   c.D = __ballot(valid && m == 0xffu);
   {
     const int g63 = __builtin_amdgcn_readlane(e4_group(m, valid), 63);
-    c.gl = g63 == 0 ? 0 : (g63 == 1 ? 1 : 2);
+    c.gl = min(g63, 2);
   }
   const E4Role r = e4_roles(m, valid, c, st, lane, lem);
   // a head's count: words to its run's end, at most 255 (:123-131, :143-164)
