@@ -1618,7 +1618,8 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       const bool chk = (ow + T >= W) || (P - e < 3 * kWin);
       for (int rb = 0; rb < T; rb += kRound) {
         int err = 0x7fffffff;
-        if (on) {
+        // after the first round only the lanes whose output meets this round
+        if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
           int o = o0;
           for (uint32_t q = entry; q < S;) {
             const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
