@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     if (seg >= n) break;
     const uint64_t w0 = swo[seg];
     const uint64_t W = swo[seg + 1] - w0;
-    if (hint && W > hint && lane == 0) atomicOr(err, 1u);
+    if (((hint && W > hint) || W >= (1ull << 31)) && lane == 0) atomicOr(err, 1u);
     if (W == 0) {  // an empty piece: no bytes (and no loads: it may sit at the end)
       if (lane == 0) sizes[seg] = 0;
       continue;
@@ -183,23 +183,25 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     E4St st = {2, 0, 0};
     int gl = 2;
     uint32_t acc = 0;
-    const uint64_t nsteps = (W + 63) >> 6;
+    // (32-bit step / word indices: a piece is at most 2^31 words, Serialize
+    // limits segments to 2^29 - 1, Serialize.java:45-53)
+    const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;
     // software pipeline: the next four steps' loads are in flight while
     // these four are classified
     uint64_t v[4], vn[4];
     // loads clamped to the piece's last word, not predicated (no exec-mask
     // branches around them); words past the end are masked by `valid`
-    const uint64_t kl = W ? W - 1 : 0;
+    const uint32_t kl = W32 - 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = src[min(((uint64_t)j << 6) + lane, kl)];
-    for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
+    for (int j = 0; j < 4; ++j) v[j] = src[min(((uint32_t)j << 6) + lane, kl)];
+    for (uint32_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) vn[j] = src[min(((s0 + 4 + j) << 6) + lane, kl)];
       uint64_t bvg[4] = {~0ull, ~0ull, ~0ull, ~0ull};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint64_t k = ((s0 + j) << 6) + lane;
-        const bool valid = k < W;
+        const uint32_t k = ((s0 + j) << 6) + lane;
+        const bool valid = k < W32;
         if (s0 + j < nsteps) {
           const E4Cls c = e4_classify(v[j], valid, gl);
           const E4Role r = e4_roles(e3_tag(v[j]), valid, c, st, lane, lem);
@@ -415,14 +417,14 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     // the boundaries of every step come from the size pass (bvbuf); past
     // the piece every word is a boundary.  Words: this group of four steps
     // and the next one's loads in flight.
-    const uint64_t nsteps = (W + 63) >> 6;
+    const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;  // (pieces < 2^31 words)
     if (stride && nsteps > stride) continue;  // over the size hint: reported, output undefined
     const uint64_t *bvp = bvbuf + (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
     uint64_t vc[4], vl[4];
-    const uint64_t kl = W ? W - 1 : 0;  // loads clamped, not predicated
+    const uint32_t kl = W32 - 1;  // loads clamped, not predicated
 #pragma unroll
-    for (int j = 0; j < 4; ++j) vc[j] = src[min(((uint64_t)j << 6) + lane, kl)];
-    for (uint64_t s0 = 0; s0 < nsteps; s0 += 4) {
+    for (int j = 0; j < 4; ++j) vc[j] = src[min(((uint32_t)j << 6) + lane, kl)];
+    for (uint32_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) vl[j] = src[min(((s0 + 4 + j) << 6) + lane, kl)];
       uint64_t bv[8];
@@ -431,7 +433,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (s0 + j < nsteps)
-          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W, bv[j], bv[j + 1], bv[j + 2], bv[j + 3],
+          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W32, bv[j], bv[j + 1], bv[j + 2], bv[j + 3],
                        bv[j + 4], st, lane, lem, lut, ring, out, rpos, fl, obase);
       }
 #pragma unroll
