@@ -382,7 +382,7 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
     // complete lines go out 64 at a time (one full-wave store: flushing
     // every step's few lines cost 8 % more time); the ring holds at most
     // 63 + 41 lines
-    if ((rpos >> 4) >= fl + 64) {
+    if ((uint32_t)(rpos >> 4) - (uint32_t)fl >= 64u) {  // (32-bit: a 64-bit < is VALU work)
       wave_lds_order();
       e3_flush(out, ring, fl, fl + 64, obase, lane);
     }
