@@ -16,6 +16,9 @@
  * Threading: reentrant; a context may be used from one host thread at a time,
  * different contexts concurrently.  All *_batch calls are asynchronous on the
  * given stream (hipStream_t passed as void*; NULL = the device's null stream).
+ * Calls on one context share its device workspace (counters, piece sizes,
+ * step boundaries): issue them on one stream, or order the streams, so that
+ * they do not run at the same time.
  */
 #ifndef CAPNP_PACKED_H
 #define CAPNP_PACKED_H
