@@ -371,3 +371,16 @@ def test_every_encoder_matches_oracle(oracle, enc, monkeypatch):
         _check_batch(c, oracle, data, _swo(sizes))
     finally:
         c.close()
+
+
+def test_large_single_pieces(ctx, oracle):
+    """Pieces of 2^21 and 3 * 2^20 + 17 words (the default encoder walks a
+    piece with one wave; its step / word indices are 32-bit) and the decoder's
+    many windows per piece."""
+    rng = np.random.default_rng(77)
+    sizes = [1 << 21, 3 * (1 << 20) + 17, 5]
+    parts = []
+    for i, n in enumerate(sizes):
+        probs = [[.5, .2, .2, .1], [.05, .6, .3, .05], [.9, .04, .03, .03]][i % 3]
+        parts.append(_random_words(rng, n, probs))
+    _check_batch(ctx, oracle, np.concatenate(parts), _swo(sizes))
