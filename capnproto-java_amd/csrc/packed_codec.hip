@@ -2051,7 +2051,7 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
   int rc = ensure_status(ctx, (uint64_t)n + nb + 1);
   if (rc) return rc;
   uint64_t stride = hint ? (hint + 63) / 64 : 0, rows;
-  if (stride && (uint64_t)n * stride > (1ull << 29)) stride = 0;  // (> 4 GiB of rows: pack them)
+  if (stride && stride > (1ull << 29) / n) stride = 0;  // (> 4 GiB of rows: pack them; no overflow)
   if (stride) {
     rows = (uint64_t)n * stride;
   } else {
