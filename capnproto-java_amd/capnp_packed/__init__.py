@@ -173,26 +173,35 @@ class Context:
                "cpk_count_mismatch")
 
     # ---- host-memory forms (numpy) -----------------------------------------
-    def encode_host(self, data: np.ndarray, seg_word_off: np.ndarray):
-        """-> (packed bytes as uint8 array, out_off uint64[n+1])."""
+    def encode_host(self, data: np.ndarray, seg_word_off: np.ndarray, out: np.ndarray = None):
+        """-> (packed bytes as uint8 array, out_off uint64[n+1]).  `out`: a
+        reusable uint8 buffer of at least batch_capacity() bytes."""
         swo = np.ascontiguousarray(seg_word_off, dtype=np.uint64)
         n = len(swo) - 1
         data = np.ascontiguousarray(data, dtype=np.uint8)
         cap = batch_capacity(swo)
-        out = np.zeros(cap, dtype=np.uint8)
+        if out is None:
+            out = np.zeros(cap, dtype=np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < cap:
+            raise ValueError("out: contiguous uint8, at least batch_capacity() bytes")
         off = np.zeros(n + 1, dtype=np.uint64)
         rc = self._lib.cpk_encode_host(self.handle, data.ctypes.data if data.size else None,
                                        swo.ctypes.data, n, out.ctypes.data, cap, off.ctypes.data)
         _check(rc, "cpk_encode_host")
         return out[: int(off[-1])], off
 
-    def decode_host(self, packed: np.ndarray, in_off: np.ndarray, seg_word_off: np.ndarray):
-        """-> (decoded uint8 array, status int32[n]).  Never raises on bad data."""
+    def decode_host(self, packed: np.ndarray, in_off: np.ndarray, seg_word_off: np.ndarray,
+                    out: np.ndarray = None):
+        """-> (decoded uint8 array, status int32[n]).  Never raises on bad data.
+        `out`: a reusable uint8 buffer of at least 8 * seg_word_off[-1] bytes."""
         swo = np.ascontiguousarray(seg_word_off, dtype=np.uint64)
         io = np.ascontiguousarray(in_off, dtype=np.uint64)
         n = len(swo) - 1
         pk = np.ascontiguousarray(packed, dtype=np.uint8)
-        out = np.zeros(int(8 * swo[-1]) + 8, dtype=np.uint8)
+        if out is None:
+            out = np.zeros(int(8 * swo[-1]) + 8, dtype=np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < int(8 * swo[-1]):
+            raise ValueError("out: contiguous uint8, at least 8 * seg_word_off[-1] bytes")
         st = np.zeros(max(n, 1), dtype=np.int32)
         rc = self._lib.cpk_decode_host(self.handle, pk.ctypes.data if pk.size else None,
                                        io.ctypes.data, swo.ctypes.data, n, out.ctypes.data,

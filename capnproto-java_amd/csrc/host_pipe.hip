@@ -1,0 +1,369 @@
+// Host-memory forms of the batch codec (cpk_encode_host / cpk_decode_host):
+// the socket/file ByteBuffer path of SerializePacked.java:75-96, :119-134.
+// Included from packed_codec.hip.
+//
+// The batch is cut into chunks of whole pieces (~CPK_HOST_CHUNK_MB of
+// unpacked words each) that flow through two staging slots, each a pinned
+// host buffer pair and a device buffer pair:
+//
+//   host threads   copy-in(k) ............ copy-out(k-2)
+//   copy stream    H2D(k)
+//   codec stream          kernels(k) + its offsets / statuses
+//   copy stream 2                   D2H(k-1)
+//
+// Pageable hipMemcpy moves 9-14 GiB/s host->device on the box; pinned DMA
+// runs at 53 GiB/s each way (full duplex) and a threaded memcpy into pinned
+// memory at 80-100 GiB/s (tools/host_copy_probe.cpp), so the pipeline is
+// bounded by the DMA of the larger side.  Kernels of consecutive chunks run
+// in order on one stream (they share the context's workspace).
+
+struct HostSlot {
+  void *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+  uint64_t *pin_meta = nullptr, *d_meta = nullptr;
+  hipEvent_t eh = nullptr, ek = nullptr, ed = nullptr;  // H2D done, kernels done, D2H done
+};
+
+struct HostPipe {
+  hipStream_t sh = nullptr, sk = nullptr, sd = nullptr;
+  HostSlot slot[2];
+  uint64_t cap_in = 0, cap_out = 0, cap_meta = 0;  // bytes, bytes, u64 entries
+  bool ok = false;
+};
+
+namespace {
+
+int host_threads() {
+  const char *e = getenv("CPK_HOST_THREADS");
+  const int t = e ? atoi(e) : 8;
+  return t < 1 ? 1 : (t > 64 ? 64 : t);
+}
+
+uint64_t host_chunk_bytes() {
+  // (CPK_HOST_CHUNK_KB: small chunks for tests)
+  if (const char *k = getenv("CPK_HOST_CHUNK_KB")) return (uint64_t)atoll(k) << 10 ?: 1;
+  const char *e = getenv("CPK_HOST_CHUNK_MB");
+  return (uint64_t)(e ? atoll(e) : 256) << 20 ?: 1;
+}
+
+// memcpy over host threads (page-aligned parts)
+void par_copy(void *dst, const void *src, uint64_t bytes) {
+  const int nt = host_threads();
+  if (bytes < (4u << 20) || nt == 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  const uint64_t per = ((bytes + nt - 1) / nt + 4095) & ~4095ull;
+  std::vector<std::thread> ts;
+  for (int i = 1; i < nt; ++i) {
+    const uint64_t a = per * i;
+    if (a >= bytes) break;
+    const uint64_t b = a + per < bytes ? a + per : bytes;
+    ts.emplace_back([=] { memcpy((char *)dst + a, (const char *)src + a, b - a); });
+  }
+  memcpy(dst, src, per < bytes ? per : bytes);
+  for (auto &t : ts) t.join();
+}
+
+void pipe_free_buffers(HostPipe *p) {
+  for (HostSlot &s : p->slot) {
+    if (s.pin_in) hipHostFree(s.pin_in);
+    if (s.pin_out) hipHostFree(s.pin_out);
+    if (s.pin_meta) hipHostFree(s.pin_meta);
+    if (s.d_in) hipFree(s.d_in);
+    if (s.d_out) hipFree(s.d_out);
+    if (s.d_meta) hipFree(s.d_meta);
+    s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
+    s.pin_meta = s.d_meta = nullptr;
+  }
+  p->cap_in = p->cap_out = p->cap_meta = 0;
+}
+
+void pipe_destroy(HostPipe *p) {
+  if (!p) return;
+  if (p->sh) hipStreamSynchronize(p->sh);
+  if (p->sk) hipStreamSynchronize(p->sk);
+  if (p->sd) hipStreamSynchronize(p->sd);
+  pipe_free_buffers(p);
+  for (HostSlot &s : p->slot) {
+    if (s.eh) hipEventDestroy(s.eh);
+    if (s.ek) hipEventDestroy(s.ek);
+    if (s.ed) hipEventDestroy(s.ed);
+  }
+  if (p->sh) hipStreamDestroy(p->sh);
+  if (p->sk) hipStreamDestroy(p->sk);
+  if (p->sd) hipStreamDestroy(p->sd);
+  delete p;
+}
+
+// the context's pipe with staging of at least the given sizes (grow-only)
+int pipe_get(cpk_ctx ctx, uint64_t in_bytes, uint64_t out_bytes, uint64_t meta, HostPipe **out) {
+  HostPipe *p = ctx->pipe;
+  if (!p) {
+    p = new HostPipe();
+    ctx->pipe = p;
+    bool ok = hipStreamCreateWithFlags(&p->sh, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&p->sk, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&p->sd, hipStreamNonBlocking) == hipSuccess;
+    for (HostSlot &s : p->slot)
+      ok = ok && hipEventCreateWithFlags(&s.eh, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&s.ek, hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&s.ed, hipEventDisableTiming) == hipSuccess;
+    p->ok = ok;
+  }
+  if (!p->ok) return CPK_EDEVICE;
+  in_bytes = (in_bytes + 64 + 4095) & ~4095ull;  // (+ the decoder's zero read slack)
+  out_bytes = (out_bytes + 64 + 4095) & ~4095ull;
+  if (in_bytes > p->cap_in || out_bytes > p->cap_out || meta > p->cap_meta) {
+    const uint64_t ci = in_bytes > p->cap_in ? in_bytes : p->cap_in;
+    const uint64_t co = out_bytes > p->cap_out ? out_bytes : p->cap_out;
+    const uint64_t cm = meta > p->cap_meta ? meta : p->cap_meta;
+    pipe_free_buffers(p);
+    for (HostSlot &s : p->slot) {
+      if (hipHostMalloc(&s.pin_in, ci, hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc(&s.pin_out, co, hipHostMallocDefault) != hipSuccess ||
+          hipHostMalloc((void **)&s.pin_meta, cm * 8, hipHostMallocDefault) != hipSuccess ||
+          hipMalloc(&s.d_in, ci) != hipSuccess || hipMalloc(&s.d_out, co) != hipSuccess ||
+          hipMalloc((void **)&s.d_meta, cm * 8) != hipSuccess) {
+        pipe_free_buffers(p);
+        return CPK_ENOMEM;
+      }
+    }
+    p->cap_in = ci;
+    p->cap_out = co;
+    p->cap_meta = cm;
+  }
+  *out = p;
+  return CPK_OK;
+}
+
+struct HostChunk {
+  uint32_t i0, i1;       // pieces [i0, i1)
+  uint64_t in0, in_len;  // input bytes (encode: words * 8; decode: packed range)
+  uint64_t out_cap;      // output bytes the chunk may produce
+  uint64_t maxw;         // largest piece, words
+};
+
+// chunks of whole pieces, each about `target` bytes of unpacked words (a
+// piece larger than that is a chunk of its own); decode also bounds the
+// packed bytes of a chunk
+std::vector<HostChunk> host_chunks(const uint64_t *swo, const uint64_t *in_off, uint32_t n,
+                                   uint64_t target) {
+  std::vector<HostChunk> cs;
+  uint32_t i = 0;
+  while (i < n) {
+    HostChunk c{i, i, 0, 0, 0, 0};
+    uint64_t words = 0, pk = 0, cap = 0;
+    while (c.i1 < n) {
+      const uint64_t w = swo[c.i1 + 1] - swo[c.i1];
+      const uint64_t p = in_off ? in_off[c.i1 + 1] - in_off[c.i1] : 0;
+      if (c.i1 > c.i0 && ((words + w) * 8 > target || pk + p > target)) break;
+      words += w;
+      pk += p;
+      cap += cpk_packed_bound(w);
+      c.maxw = w > c.maxw ? w : c.maxw;
+      ++c.i1;
+    }
+    if (in_off) {
+      c.in0 = in_off[c.i0];
+      c.in_len = pk;
+      c.out_cap = words * 8;
+    } else {
+      c.in0 = swo[c.i0] * 8;
+      c.in_len = words * 8;
+      c.out_cap = cap + 16;
+    }
+    cs.push_back(c);
+    i = c.i1;
+  }
+  return cs;
+}
+
+// wait for everything the pipe has in flight (error paths)
+void pipe_drain(HostPipe *p) {
+  hipStreamSynchronize(p->sh);
+  hipStreamSynchronize(p->sk);
+  hipStreamSynchronize(p->sd);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32_t n,
+                    void *h_out, uint64_t h_out_cap, uint64_t *h_out_off) {
+  if (!ctx || !h_swo || !h_out_off || (n && ((!h_in && h_swo[n] > h_swo[0]) || !h_out)))
+    return CPK_EINVAL;
+  if (n == 0) {
+    h_out_off[0] = 0;
+    return CPK_OK;
+  }
+  for (uint32_t i = 0; i < n; ++i)
+    if (h_swo[i + 1] < h_swo[i]) return CPK_EINVAL;
+  DeviceGuard g(ctx->device);
+  const std::vector<HostChunk> cs = host_chunks(h_swo, nullptr, n, host_chunk_bytes());
+  uint64_t mi = 0, mo = 0, mm = 0;
+  for (const HostChunk &c : cs) {
+    mi = c.in_len > mi ? c.in_len : mi;
+    mo = c.out_cap > mo ? c.out_cap : mo;
+    mm = c.i1 - c.i0 > mm ? c.i1 - c.i0 : mm;
+  }
+  HostPipe *p = nullptr;
+  int rc = pipe_get(ctx, mi, mo, 2 * (mm + 1), &p);
+  if (rc) return rc;
+  const uint8_t *src = (const uint8_t *)h_in;
+  uint8_t *dst = (uint8_t *)h_out;
+  uint64_t base = 0;          // output bytes so far
+  const size_t K = cs.size();
+  for (size_t k = 0; k <= K + 1 && rc == CPK_OK; ++k) {
+    if (k < K) {  // copy-in, H2D, kernels of chunk k
+      const HostChunk &c = cs[k];
+      HostSlot &s = p->slot[k & 1];
+      const uint32_t nk = c.i1 - c.i0;
+      par_copy(s.pin_in, src + c.in0, c.in_len);
+      for (uint32_t j = 0; j <= nk; ++j) s.pin_meta[j] = h_swo[c.i0 + j] - h_swo[c.i0];
+      if ((c.in_len && hipMemcpyAsync(s.d_in, s.pin_in, c.in_len, hipMemcpyHostToDevice, p->sh)) ||
+          hipMemcpyAsync(s.d_meta, s.pin_meta, (nk + 1) * 8ull, hipMemcpyHostToDevice, p->sh) ||
+          hipEventRecord(s.eh, p->sh) || hipStreamWaitEvent(p->sk, s.eh, 0) ||
+          (k >= 2 && hipStreamWaitEvent(p->sk, s.ed, 0))) {  // (d_out free: chunk k-2's D2H)
+        rc = CPK_EDEVICE;
+        break;
+      }
+      rc = cpk_encode_batch(ctx, s.d_in, s.d_meta, nk, c.maxw ? c.maxw : 1, s.d_out,
+                            s.d_meta + nk + 1, p->sk);
+      if (rc) break;
+      if (hipMemcpyAsync(s.pin_meta + nk + 1, s.d_meta + nk + 1, (nk + 1) * 8ull,
+                         hipMemcpyDeviceToHost, p->sk) ||
+          hipEventRecord(s.ek, p->sk)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+    }
+    if (k >= 1 && k - 1 < K) {  // chunk k-1: offsets, then its D2H
+      const HostChunk &c = cs[k - 1];
+      HostSlot &s = p->slot[(k - 1) & 1];
+      const uint32_t nk = c.i1 - c.i0;
+      if (hipEventSynchronize(s.ek)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      const uint64_t *off = s.pin_meta + nk + 1;
+      const uint64_t P = off[nk];
+      if (P > c.out_cap) {  // (cannot happen: a piece over its hint)
+        rc = CPK_EDEVICE;
+        break;
+      }
+      if (base + P > h_out_cap) {
+        rc = CPK_ENOMEM;
+        break;
+      }
+      for (uint32_t j = 0; j <= nk; ++j) h_out_off[c.i0 + j] = base + off[j];
+      if ((P && hipMemcpyAsync(s.pin_out, s.d_out, P, hipMemcpyDeviceToHost, p->sd)) ||
+          hipEventRecord(s.ed, p->sd)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      base += P;
+    }
+    if (k >= 2) {  // chunk k-2: copy-out
+      const HostChunk &c = cs[k - 2];
+      HostSlot &s = p->slot[k & 1];
+      if (hipEventSynchronize(s.ed)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      const uint64_t o0 = h_out_off[c.i0], o1 = h_out_off[c.i1];
+      par_copy(dst + o0, s.pin_out, o1 - o0);
+    }
+  }
+  if (rc) {
+    pipe_drain(p);
+    return rc;
+  }
+  // (a piece over its hint cannot occur: each chunk's hint is its largest piece)
+  return cpk_ctx_take_error(ctx, p->sk);
+}
+
+int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
+                    const uint64_t *h_swo, uint32_t n, void *h_out, int32_t *h_status) {
+  if (!ctx || !h_in_off || !h_swo || !h_status) return CPK_EINVAL;
+  if (n == 0) return CPK_OK;
+  for (uint32_t i = 0; i < n; ++i)
+    if (h_swo[i + 1] < h_swo[i] || h_in_off[i + 1] < h_in_off[i]) return CPK_EINVAL;
+  if ((!h_packed && h_in_off[n] > h_in_off[0]) || (!h_out && h_swo[n] > h_swo[0])) return CPK_EINVAL;
+  DeviceGuard g(ctx->device);
+  const std::vector<HostChunk> cs = host_chunks(h_swo, h_in_off, n, host_chunk_bytes());
+  uint64_t mi = 0, mo = 0, mm = 0;
+  for (const HostChunk &c : cs) {
+    mi = c.in_len > mi ? c.in_len : mi;
+    mo = c.out_cap > mo ? c.out_cap : mo;
+    mm = c.i1 - c.i0 > mm ? c.i1 - c.i0 : mm;
+  }
+  HostPipe *p = nullptr;
+  // meta: swo | in_off | status (int32, n/2 + 1 entries)
+  int rc = pipe_get(ctx, mi, mo, 2 * (mm + 1) + mm / 2 + 1, &p);
+  if (rc) return rc;
+  const uint8_t *src = (const uint8_t *)h_packed;
+  uint8_t *dst = (uint8_t *)h_out;
+  const size_t K = cs.size();
+  for (size_t k = 0; k <= K + 1 && rc == CPK_OK; ++k) {
+    if (k < K) {  // copy-in, H2D, decode of chunk k
+      const HostChunk &c = cs[k];
+      HostSlot &s = p->slot[k & 1];
+      const uint32_t nk = c.i1 - c.i0;
+      par_copy(s.pin_in, src + c.in0, c.in_len);
+      memset((uint8_t *)s.pin_in + c.in_len, 0, 32);  // (the decoder reads whole 16-byte lines)
+      for (uint32_t j = 0; j <= nk; ++j) {
+        s.pin_meta[j] = h_swo[c.i0 + j] - h_swo[c.i0];
+        s.pin_meta[nk + 1 + j] = h_in_off[c.i0 + j] - h_in_off[c.i0];
+      }
+      int32_t *st = (int32_t *)(s.d_meta + 2 * (nk + 1));
+      if (hipMemcpyAsync(s.d_in, s.pin_in, c.in_len + 32, hipMemcpyHostToDevice, p->sh) ||
+          hipMemcpyAsync(s.d_meta, s.pin_meta, 2 * (nk + 1) * 8ull, hipMemcpyHostToDevice, p->sh) ||
+          hipEventRecord(s.eh, p->sh) || hipStreamWaitEvent(p->sk, s.eh, 0) ||
+          (k >= 2 && hipStreamWaitEvent(p->sk, s.ed, 0))) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      rc = cpk_decode_batch(ctx, s.d_in, s.d_meta + nk + 1, s.d_meta, nk, s.d_out, st, p->sk);
+      if (rc) break;
+      if (hipMemcpyAsync(s.pin_meta + 2 * (nk + 1), st, nk * 4ull, hipMemcpyDeviceToHost, p->sk) ||
+          hipEventRecord(s.ek, p->sk)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+    }
+    if (k >= 1 && k - 1 < K) {  // chunk k-1: statuses, then its D2H
+      const HostChunk &c = cs[k - 1];
+      HostSlot &s = p->slot[(k - 1) & 1];
+      const uint32_t nk = c.i1 - c.i0;
+      if (hipEventSynchronize(s.ek)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      memcpy(h_status + c.i0, s.pin_meta + 2 * (nk + 1), nk * 4ull);
+      if ((c.out_cap && hipMemcpyAsync(s.pin_out, s.d_out, c.out_cap, hipMemcpyDeviceToHost, p->sd)) ||
+          hipEventRecord(s.ed, p->sd)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+    }
+    if (k >= 2) {  // chunk k-2: copy-out
+      const HostChunk &c = cs[k - 2];
+      HostSlot &s = p->slot[k & 1];
+      if (hipEventSynchronize(s.ed)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      par_copy(dst + 8 * h_swo[c.i0], s.pin_out, c.out_cap);
+    }
+  }
+  if (rc) {
+    pipe_drain(p);
+    return rc;
+  }
+  for (uint32_t i = 0; i < n; ++i)
+    if (h_status[i] != CPK_OK) return h_status[i];
+  return CPK_OK;
+}
+
+}  // extern "C"

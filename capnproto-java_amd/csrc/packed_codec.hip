@@ -25,6 +25,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <thread>
 #include <vector>
 
 #include "../../include/capnp_packed.h"
@@ -1813,6 +1814,8 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 }  // namespace cpk
 
 // ================================================================ C ABI
+struct HostPipe;  // host_pipe.hip: staging of the host-memory forms
+
 struct cpk_ctx_s {
   int device;
   int cus;
@@ -1821,7 +1824,7 @@ struct cpk_ctx_s {
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
   void *plan;             // tiled encode: toff | tmap | pstatus | tstate
   uint64_t plan_cap;      // bytes
-  int encoder;            // 3: workgroup-per-tile encoder (default); 1, 2: earlier encoders
+  int encoder;            // 4: size + emit passes (default); 1-3: earlier encoders
   uint32_t *e3_tfirst;    // encoder v3: tile -> first piece starting in it
   uint64_t *e3_status;    //   look-back word per tile
   uint64_t *e3_tstate;    //   exit run state per tile
@@ -1830,6 +1833,7 @@ struct cpk_ctx_s {
   int e3_grid;            //   workgroups of encode3_kernel resident at once
   uint64_t *e4_bv;        // encoder v4: run boundaries per 64-word step
   uint64_t e4_bv_cap;     //   entries
+  HostPipe *pipe;         // cpk_encode_host / cpk_decode_host staging (lazy)
 };
 
 namespace {
@@ -1934,6 +1938,8 @@ int e3_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
 }
 }  // namespace
 
+#include "host_pipe.hip"
+
 extern "C" {
 
 int cpk_abi_version(void) { return CPK_ABI_VERSION; }
@@ -2035,6 +2041,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->e3_status) hipFree(ctx->e3_status);
   if (ctx->e3_tstate) hipFree(ctx->e3_tstate);
   if (ctx->e4_bv) hipFree(ctx->e4_bv);
+  pipe_destroy(ctx->pipe);
   free(ctx);
 }
 
@@ -2219,112 +2226,6 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
                      (hipStream_t)stream, (const uint8_t *)d_packed, d_in_off, d_swo, n,
                      (uint64_t *)d_out, d_status, ctx->tickets + cpk::kTkDec, avail);
   return hip_ok(hipGetLastError());
-}
-
-int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32_t n,
-                    void *h_out, uint64_t h_out_cap, uint64_t *h_out_off) {
-  if (!ctx || !h_swo || !h_out_off) return CPK_EINVAL;
-  DeviceGuard g(ctx->device);
-  uint64_t words = h_swo[n] - h_swo[0];
-  uint64_t maxw = 0;
-  for (uint32_t i = 0; i < n; ++i) maxw = h_swo[i + 1] - h_swo[i] > maxw ? h_swo[i + 1] - h_swo[i] : maxw;
-  uint64_t cap = cpk_batch_packed_capacity(h_swo, n);
-  if (n == 0) {
-    h_out_off[0] = 0;
-    return CPK_OK;
-  }
-  if (maxw == 0) {  // only empty pieces: they pack to nothing (SerializePackedTest.java:21)
-    for (uint32_t i = 0; i <= n; ++i) h_out_off[i] = 0;
-    return CPK_OK;
-  }
-  void *d_in = nullptr, *d_out = nullptr;
-  uint64_t *d_swo = nullptr, *d_off = nullptr;
-  int rc = CPK_OK;
-  std::vector<uint64_t> rel;
-  if (hipMalloc(&d_in, words * 8 + 8) != hipSuccess || hipMalloc(&d_out, cap) != hipSuccess ||
-      hipMalloc(&d_swo, (n + 1) * 8ull) != hipSuccess ||
-      hipMalloc(&d_off, (n + 1) * 8ull) != hipSuccess) {
-    rc = CPK_ENOMEM;
-    goto done;
-  }
-  rel.resize(n + 1);
-  for (uint32_t i = 0; i <= n; ++i) rel[i] = h_swo[i] - h_swo[0];
-  if (hipMemcpy(d_in, (const uint8_t *)h_in + 8 * h_swo[0], words * 8, hipMemcpyHostToDevice) ||
-      hipMemcpy(d_swo, rel.data(), (n + 1) * 8ull, hipMemcpyHostToDevice)) {
-    rc = CPK_EDEVICE;
-    goto done;
-  }
-  rc = cpk_encode_batch(ctx, d_in, d_swo, n, maxw, d_out, d_off, nullptr);
-  if (rc) goto done;
-  rc = cpk_ctx_take_error(ctx, nullptr);
-  if (rc) goto done;
-  if (hipMemcpy(h_out_off, d_off, (n + 1) * 8ull, hipMemcpyDeviceToHost)) {
-    rc = CPK_EDEVICE;
-    goto done;
-  }
-  if (h_out_off[n] > h_out_cap) {
-    rc = CPK_ENOMEM;
-    goto done;
-  }
-  if (hipMemcpy(h_out, d_out, h_out_off[n], hipMemcpyDeviceToHost)) rc = CPK_EDEVICE;
-done:
-  if (d_in) hipFree(d_in);
-  if (d_out) hipFree(d_out);
-  if (d_swo) hipFree(d_swo);
-  if (d_off) hipFree(d_off);
-  return rc;
-}
-
-int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
-                    const uint64_t *h_swo, uint32_t n, void *h_out, int32_t *h_status) {
-  if (!ctx || !h_in_off || !h_swo || !h_status) return CPK_EINVAL;
-  if (n == 0) return CPK_OK;
-  DeviceGuard g(ctx->device);
-  uint64_t words = h_swo[n] - h_swo[0];
-  uint64_t pbytes = h_in_off[n] - h_in_off[0];
-  void *d_pk = nullptr, *d_out = nullptr;
-  uint64_t *d_swo = nullptr, *d_io = nullptr;
-  int32_t *d_st = nullptr;
-  int rc = CPK_OK;
-  std::vector<uint64_t> rs, ri;
-  if (hipMalloc(&d_pk, pbytes + 32) != hipSuccess || hipMalloc(&d_out, words * 8 + 8) != hipSuccess ||
-      hipMalloc(&d_swo, (n + 1) * 8ull) != hipSuccess ||
-      hipMalloc(&d_io, (n + 1) * 8ull) != hipSuccess || hipMalloc(&d_st, n * 4ull) != hipSuccess) {
-    rc = CPK_ENOMEM;
-    goto done;
-  }
-  rs.resize(n + 1);
-  ri.resize(n + 1);
-  for (uint32_t i = 0; i <= n; ++i) {
-    rs[i] = h_swo[i] - h_swo[0];
-    ri[i] = h_in_off[i] - h_in_off[0];
-  }
-  if (hipMemset(d_pk, 0, pbytes + 32) ||
-      (pbytes && hipMemcpy(d_pk, (const uint8_t *)h_packed + h_in_off[0], pbytes, hipMemcpyHostToDevice)) ||
-      hipMemcpy(d_swo, rs.data(), (n + 1) * 8ull, hipMemcpyHostToDevice) ||
-      hipMemcpy(d_io, ri.data(), (n + 1) * 8ull, hipMemcpyHostToDevice)) {
-    rc = CPK_EDEVICE;
-    goto done;
-  }
-  rc = cpk_decode_batch(ctx, d_pk, d_io, d_swo, n, d_out, d_st, nullptr);
-  if (rc) goto done;
-  if (hipMemcpy(h_status, d_st, n * 4ull, hipMemcpyDeviceToHost) ||
-      (words && hipMemcpy((uint8_t *)h_out + 8 * h_swo[0], d_out, words * 8, hipMemcpyDeviceToHost))) {
-    rc = CPK_EDEVICE;
-    goto done;
-  }
-  for (uint32_t i = 0; i < n; ++i)
-    if (h_status[i] != CPK_OK) {
-      rc = h_status[i];
-      break;
-    }
-done:
-  if (d_pk) hipFree(d_pk);
-  if (d_out) hipFree(d_out);
-  if (d_swo) hipFree(d_swo);
-  if (d_io) hipFree(d_io);
-  if (d_st) hipFree(d_st);
-  return rc;
 }
 
 int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,

@@ -130,8 +130,11 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
                       uint64_t *d_in_off, int32_t *d_status, void *stream);
 
 /* Host-memory convenience forms (the socket/file ByteBuffer path,
- * SerializePacked.java:75-96, :119-134): stage through device memory,
- * run the batch kernels, copy back.  Synchronous.
+ * SerializePacked.java:75-96, :119-134).  Synchronous.  encode_host and
+ * decode_host pipeline the batch in chunks of whole pieces through pinned
+ * staging kept in the context (CPK_HOST_CHUNK_MB, default 256;
+ * CPK_HOST_THREADS copy threads, default 8); decode_stream_host stages the
+ * whole stream.
  *   cpk_encode_host: h_out capacity >= cpk_batch_packed_capacity();
  *                    h_out_off[n+1] written.
  *   cpk_decode_host: h_status[n] written; returns CPK_OK iff all pieces OK. */

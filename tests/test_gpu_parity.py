@@ -384,3 +384,25 @@ def test_large_single_pieces(ctx, oracle):
         probs = [[.5, .2, .2, .1], [.05, .6, .3, .05], [.9, .04, .03, .03]][i % 3]
         parts.append(_random_words(rng, n, probs))
     _check_batch(ctx, oracle, np.concatenate(parts), _swo(sizes))
+
+
+@pytest.mark.parametrize("chunk_kb", ["1", "64"])
+def test_host_forms_pipelined_chunks(ctx, oracle, chunk_kb, monkeypatch):
+    """cpk_encode_host / cpk_decode_host cut a batch into chunks of whole
+    pieces that flow through two pinned staging slots (host_pipe.hip): many
+    chunks, a piece larger than a chunk, empty pieces, a malformed tail."""
+    monkeypatch.setenv("CPK_HOST_CHUNK_KB", chunk_kb)
+    rng = np.random.default_rng(int(chunk_kb))
+    sizes = [0, 3, 9000, 0, 1] + list(rng.integers(0, 2500, size=60)) + [20000, 7, 0]
+    parts = [_random_words(rng, int(s), [.4, .3, .2, .1]) for s in sizes]
+    _check_batch(ctx, oracle, np.concatenate(parts), _swo(sizes))
+    # per-piece statuses survive the chunking
+    cases = _corrupt_cases(oracle, rng)
+    packed = b"".join(p for p, _ in cases)
+    dec, st = ctx.decode_host(np.frombuffer(packed, np.uint8), _swo([len(p) for p, _ in cases]),
+                              _swo([n for _, n in cases]))
+    for i, (p, n) in enumerate(cases):
+        ost, _, used = oracle.unpack(p, 8 * n)
+        if ost == oracle.OK and used != len(p):
+            ost = oracle.ETRAILING
+        assert st[i] == ost, (i, st[i], ost)
