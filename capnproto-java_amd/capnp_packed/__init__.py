@@ -23,6 +23,7 @@ _PKG = Path(__file__).resolve().parents[1]
 LIB_PATH = _PKG / "lib" / "libcapnp_packed_hip.so"
 
 OK, EINVAL, ETRUNC, EOVERRUN, ETRAILING, ENOMEM, EDEVICE, EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6, -8
+EFRAME = -7  # segment table invalid (Serialize.java:45-53, :125-163)
 TILE_WORDS = 8192  # encoder tile: larger pieces are cut into tiles
 
 EXPORTS = [
@@ -30,6 +31,7 @@ EXPORTS = [
     "cpk_ctx_create", "cpk_ctx_destroy", "cpk_ctx_device", "cpk_encode_batch",
     "cpk_decode_batch", "cpk_decode_stream", "cpk_encode_host", "cpk_decode_host",
     "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch", "cpk_ctx_take_error",
+    "cpk_decode_messages",
 ]
 
 
@@ -82,6 +84,7 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_generate": ([vp, ctypes.POINTER(GenParams), vp, u32, vp, vp], i32),
         "cpk_count_mismatch": ([vp, vp, vp, u64, vp, vp], i32),
         "cpk_ctx_take_error": ([vp, vp], i32),
+        "cpk_decode_messages": ([vp, vp, vp, u32, u64, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         if not strict and not hasattr(L, name):
@@ -161,6 +164,29 @@ class Context:
                                         d_seg_word_off.data_ptr(), n, d_out.data_ptr(),
                                         d_status.data_ptr(), self._stream(stream))
         _check(rc, "cpk_decode_batch")
+
+    def decode_messages(self, d_packed, d_msg_off, d_out, d_seg_word_off, d_seg_in_off,
+                        d_seg_status, d_msg_seg_off, d_msg_status,
+                        traversal_limit_words: int = 8 * 1024 * 1024, stream=None):
+        """Serialize.read per message over a batch of packed messages with
+        known byte ranges (cpk_decode_messages).  Capacities come from the
+        tensors' sizes.  -> (status, total words, total segments); status
+        CPK_ENOMEM (nothing decoded) if the capacities are too small."""
+        nm = d_msg_off.numel() - 1
+        tot = (ctypes.c_uint64 * 2)()
+        seg_cap = min(d_seg_status.numel() if d_seg_status is not None else 0,
+                      d_seg_word_off.numel() - 1 if d_seg_word_off is not None else 0)
+
+        def ptr(t):
+            return t.data_ptr() if t is not None else None
+        rc = self._lib.cpk_decode_messages(
+            self.handle, d_packed.data_ptr(), d_msg_off.data_ptr(), nm, int(traversal_limit_words),
+            ptr(d_out), d_out.numel() * d_out.element_size() // 8 if d_out is not None else 0,
+            ptr(d_seg_word_off), ptr(d_seg_in_off), ptr(d_seg_status), seg_cap,
+            d_msg_seg_off.data_ptr(), d_msg_status.data_ptr(), tot, self._stream(stream))
+        if rc not in (OK, ENOMEM):
+            _check(rc, "cpk_decode_messages")
+        return rc, int(tot[0]), int(tot[1])
 
     def generate(self, params: GenParams, d_seg_word_off, d_out, stream=None):
         n = d_seg_word_off.numel() - 1

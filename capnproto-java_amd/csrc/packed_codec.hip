@@ -73,6 +73,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 // waves were placed (the XCD id only picks the first counter).  Work whose
 // items depend on their predecessors (the encoders' look-back) keeps one
 // ordered counter.
+constexpr int32_t kMaxSegmentWords = (1 << 28) - 1;  // Serialize.java:45
 constexpr int kTkStride = 32;          // u32 words between counters (128 B)
 constexpr int kTkEnc = 0;              // encoder counters [8]
 constexpr int kTkDec = 8 * kTkStride;  // decoder counters [8]
@@ -1442,16 +1443,23 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
 
 // kStream = false: piece i's packed bytes are [in_off[i], in_off[i+1]) and a
 //   piece that fills before its range ends is CPK_ETRAILING.
-// kStream = true: one wave decodes pieces 0..n-1 back to back from one
-//   packed stream of `avail` bytes; each read() fills its piece and leaves
-//   the rest of the stream to the next (PackedInputStream.java:35-140 as
-//   Serialize.read calls it, Serialize.java:165-175); in_off[0..n] is
-//   written with the piece boundaries found.
+// kStream = true: packed streams, each a wave's: the pieces of stream j,
+//   [spc[j], spc[j+1]), are decoded back to back from its bytes
+//   [sbeg[j], send[j]); each read() fills its piece and leaves the rest of
+//   the stream to the next (PackedInputStream.java:35-140 as Serialize.read
+//   calls it, Serialize.java:165-175).  in_off[piece] is written with the
+//   piece's start and send_out[j] with the stream's end.  sbeg == nullptr:
+//   one stream, pieces 0..n-1, bytes [0, avail).
+struct DecStreams {
+  const uint64_t *sbeg, *send, *spc;
+  uint32_t ns;
+  uint64_t *send_out;
+};
 template <bool kStream>
 __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
     const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
-    int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail) {
+    int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail, DecStreams sd) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem);
   const int lane = lane_id(), w = wave_id();
@@ -1461,11 +1469,12 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
   VisMask *visa = reinterpret_cast<VisMask *>(blk);  // [64], over the block map
   fill_luts(lut, true);
   __syncthreads();  // the only block-wide barrier: LUT ready
-  if (kStream && (blockIdx.x != 0 || w != 0)) return;
   int xq = xcc_id(), dry = 0;
   WPH_INIT
   uint64_t scur = 0;      // stream mode: start of the next piece
-  int sfail = CPK_OK;     // stream mode: a failed piece stops the stream
+  uint64_t slim = avail;  //   end of the stream's bytes
+  int sfail = CPK_OK;     //   a failed piece stops the stream
+  uint32_t snext = 0, sende = 0, sj = 0;  // next piece, end of the stream's pieces, stream
 
   for (uint32_t sidx = 0;; ++sidx) {
     // every branch below is on wave-uniform (SGPR) values: the compiler
@@ -1480,15 +1489,40 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
         if (seg < n || ++dry >= 8) break;
         xq = (xq + 1) & 7;  // this counter ran dry: help the next one
       }
+    } else {
+      // the next stream with pieces (empty streams end where they begin)
+      bool more = true;
+      while (snext >= sende) {
+        uint32_t j;
+        for (;;) {
+          j = take_ticket(ticket, xq);
+          if (j < sd.ns || ++dry >= 8) break;
+          xq = (xq + 1) & 7;
+        }
+        if (j >= sd.ns) {
+          more = false;
+          break;
+        }
+        sj = j;
+        snext = sd.sbeg ? (uint32_t)sd.spc[j] : 0u;
+        sende = sd.sbeg ? (uint32_t)sd.spc[j + 1] : n;
+        scur = sd.sbeg ? sd.sbeg[j] : 0;
+        slim = sd.sbeg ? sd.send[j] : avail;
+        sfail = CPK_OK;
+        if (snext >= sende) sd.send_out[j] = scur;
+      }
+      if (!more) break;
+      seg = snext++;
     }
     if (seg >= n) break;
     const uint64_t w0 = swo[seg];
     const int W = (int)(swo[seg + 1] - w0);
     const uint64_t a = kStream ? scur : in_off[seg];
-    const uint32_t P = kStream ? (uint32_t)min(avail - scur, (uint64_t)0xffffffffu)
+    const uint32_t P = kStream ? (uint32_t)min(slim - scur, (uint64_t)0xffffffffu)
                                : (uint32_t)(in_off[seg + 1] - a);
     if (kStream && sfail != CPK_OK) {
       status[seg] = sfail;
+      if (seg + 1 == sende) sd.send_out[sj] = scur;
       continue;
     }
     const uint8_t *gp = packed + a;
@@ -1741,10 +1775,143 @@ __global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
       in_off[seg] = a;
       scur = a + e;
       sfail = st;
-      if (seg == n - 1) in_off[n] = scur;
+      if (seg + 1 == sende) sd.send_out[sj] = scur;
     }
   }
   WPH_FLUSH(16)
+}
+
+// ------------------------------------------------------------ messages
+// Serialize.read over PackedInputStream for a batch of packed messages whose
+// byte ranges are known (Serialize.java:119-178): a thread per message reads
+// the segment table (two read() calls: the first word, then 4 * (count & ~1)
+// bytes), validates it, and the segments are then decoded as one packed
+// stream per message by decode_kernel<true>.
+
+// one read() of `words` words, byte-serial (tables are at most 257 words):
+// PackedInputStream.java:35-140 as the oracle restates it
+// (oracle/packed_oracle.c:cpko_unpack); f(word index, word) per word
+template <class F>
+__device__ int serial_read(const uint8_t *p, uint64_t n, uint64_t &ip, uint32_t words, F f) {
+  if (words == 0) return CPK_OK;
+  uint32_t wi = 0;
+  for (;;) {
+    if (ip >= n) return CPK_ETRUNC;
+    const uint32_t tag = p[ip++];
+    uint64_t w = 0;
+    for (int i = 0; i < 8; ++i)
+      if ((tag >> i) & 1) {
+        if (ip >= n) return CPK_ETRUNC;
+        w |= (uint64_t)p[ip++] << (8 * i);
+      }
+    f(wi++, w);
+    if (tag == 0 || tag == 0xffu) {
+      if (ip >= n) return CPK_ETRUNC;
+      const uint32_t run = p[ip++];
+      if (run > words - wi) return CPK_EOVERRUN;
+      if (tag == 0) {
+        for (uint32_t k = 0; k < run; ++k) f(wi++, 0ull);
+      } else {
+        if (n - ip < 8ull * run) return CPK_ETRUNC;
+        for (uint32_t k = 0; k < run; ++k) {
+          uint64_t v = 0;
+          for (int i = 0; i < 8; ++i) v |= (uint64_t)p[ip + i] << (8 * i);
+          ip += 8;
+          f(wi++, v);
+        }
+      }
+    }
+    if (wi == words) return CPK_OK;
+  }
+}
+
+// the table of message m: status, segment count, total words; on OK the
+// packed position after the table.  emit(i, size) per segment.
+template <class F>
+__device__ int read_table(const uint8_t *p, uint64_t n, uint64_t limit, uint64_t &ip,
+                          uint32_t &count, uint64_t &total, F emit) {
+  uint64_t first = 0;
+  int st = serial_read(p, n, ip, 1, [&](uint32_t, uint64_t w) { first = w; });
+  if (st) return st;
+  const int32_t raw = (int32_t)(uint32_t)first;
+  if (raw < 0 || raw > 511) return CPK_EFRAME;  // Serialize.java:128-131
+  count = (uint32_t)raw + 1;
+  const int32_t s0 = (int32_t)(uint32_t)(first >> 32);
+  if (s0 < 0) return CPK_EFRAME;  // :135-137
+  total = (uint64_t)s0;
+  bool neg = false, big = s0 > kMaxSegmentWords;
+  emit(0u, (uint32_t)s0);
+  if (count > 1) {  // :144-157
+    const uint32_t c = count;
+    st = serial_read(p, n, ip, (count & ~1u) / 2, [&](uint32_t i, uint64_t w) {
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t k = 2 * i + h;  // moreSizes[k] = segment k + 1
+        if (k + 1 < c) {
+          const int32_t v = (int32_t)(uint32_t)(w >> (32 * h));
+          neg |= v < 0;
+          big |= v > kMaxSegmentWords;
+          total += (uint64_t)(uint32_t)v;
+          emit(k + 1, (uint32_t)v);
+        }
+      }
+    });
+    if (st) return st;
+    if (neg) return CPK_EFRAME;  // :150-153 (the first negative size throws)
+  }
+  if (total > limit) return CPK_EFRAME;  // :160-162
+  // makeByteBufferForWords (:45-53) throws for a segment over 2^28 - 1 words
+  // when that segment is allocated: the message fails either way
+  if (big) return CPK_EFRAME;
+  return CPK_OK;
+}
+
+// pass 1: per message its table's status, segment count, words and the
+// packed position of segment 0
+__global__ void msg_table_kernel(const uint8_t *__restrict__ packed, const uint64_t *__restrict__ moff,
+                                 uint32_t nm, uint64_t limit, uint64_t *__restrict__ mwords,
+                                 uint64_t *__restrict__ mcount, uint64_t *__restrict__ mbeg,
+                                 int32_t *__restrict__ mstatus) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nm) return;
+  const uint64_t a = moff[m];
+  uint64_t ip = 0, total = 0;
+  uint32_t count = 0;
+  const int st = read_table(packed + a, moff[m + 1] - a, limit, ip, count, total,
+                            [](uint32_t, uint32_t) {});
+  mstatus[m] = st;
+  mwords[m] = st ? 0 : total;
+  mcount[m] = st ? 0 : count;
+  mbeg[m] = a + ip;
+}
+
+// pass 2: the segments' word offsets (segment table read again)
+__global__ void msg_swo_kernel(const uint8_t *__restrict__ packed, const uint64_t *__restrict__ moff,
+                               uint32_t nm, uint64_t limit, const uint64_t *__restrict__ mwoff,
+                               const uint64_t *__restrict__ mseg, const int32_t *__restrict__ mstatus,
+                               uint64_t *__restrict__ swo) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nm) return;
+  if (m == nm - 1) swo[mseg[nm]] = mwoff[nm];
+  if (mstatus[m] != CPK_OK) return;
+  const uint64_t a = moff[m], s0 = mseg[m];
+  uint64_t ip = 0, total = 0, acc = mwoff[m];
+  uint32_t count = 0;
+  read_table(packed + a, moff[m + 1] - a, limit, ip, count, total, [&](uint32_t i, uint32_t sz) {
+    swo[s0 + i] = acc;
+    acc += sz;
+  });
+}
+
+// pass 4: a message's status: its table's, else its first failed segment's
+// (a failure stops the stream: the last segment carries it), else
+// CPK_ETRAILING when the segments end before the message's bytes do
+__global__ void msg_final_kernel(const uint64_t *__restrict__ moff, uint32_t nm,
+                                 const uint64_t *__restrict__ mseg, const uint64_t *__restrict__ mend,
+                                 const int32_t *__restrict__ seg_status, int32_t *__restrict__ mstatus) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nm || mstatus[m] != CPK_OK) return;
+  const int32_t st = seg_status[mseg[m + 1] - 1];
+  mstatus[m] = st != CPK_OK ? st : (mend[m] != moff[m + 1] ? CPK_ETRAILING : CPK_OK);
 }
 
 // ------------------------------------------------------------ bench support
@@ -2211,7 +2378,8 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   if (grid > (n + 3) / 4) grid = (n + 3) / 4;
   hipLaunchKernelGGL(cpk::decode_kernel<false>, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
                      (const uint8_t *)d_packed, const_cast<uint64_t *>(d_in_off), d_swo, n,
-                     (uint64_t *)d_out, d_status, ctx->tickets + cpk::kTkDec, (uint64_t)0);
+                     (uint64_t *)d_out, d_status, ctx->tickets + cpk::kTkDec, (uint64_t)0,
+                     cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr});
   return hip_ok(hipGetLastError());
 }
 
@@ -2222,9 +2390,76 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
   if (((uintptr_t)d_packed & 15) || ((uintptr_t)d_out & 7)) return CPK_EINVAL;
   if (n == 0) return CPK_OK;
   DeviceGuard g(ctx->device);
-  hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds,
-                     (hipStream_t)stream, (const uint8_t *)d_packed, d_in_off, d_swo, n,
-                     (uint64_t *)d_out, d_status, ctx->tickets + cpk::kTkDec, avail);
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
+    return CPK_EDEVICE;
+  // one stream: one wave works, the others find no ticket
+  hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds, s,
+                     (const uint8_t *)d_packed, d_in_off, d_swo, n, (uint64_t *)d_out, d_status,
+                     ctx->tickets + cpk::kTkDec, avail,
+                     cpk::DecStreams{nullptr, nullptr, nullptr, 1, d_in_off + n});
+  return hip_ok(hipGetLastError());
+}
+
+int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg_off, uint32_t nm,
+                        uint64_t traversal_limit_words, void *d_out, uint64_t out_cap_words,
+                        uint64_t *d_seg_word_off, uint64_t *d_seg_in_off, int32_t *d_seg_status,
+                        uint32_t seg_cap, uint64_t *d_msg_seg_off, int32_t *d_msg_status,
+                        uint64_t *h_totals, void *stream) {
+  if (!ctx || !h_totals || (nm && (!d_msg_off || !d_msg_seg_off || !d_msg_status))) return CPK_EINVAL;
+  if (((uintptr_t)d_packed & 15) || ((uintptr_t)d_out & 7)) return CPK_EINVAL;
+  h_totals[0] = h_totals[1] = 0;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (nm == 0) return hip_ok(hipMemsetAsync(d_msg_seg_off, 0, 8, s));
+  // scratch: words | begin | words offsets [nm+1] | block sums x2
+  const uint32_t nb = (uint32_t)((nm + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
+  int rc = ensure_status(ctx, 3ull * nm + 1 + 2ull * nb);
+  if (rc) return rc;
+  uint64_t *mwords = ctx->status, *mbeg = mwords + nm, *mwoff = mbeg + nm;
+  uint64_t *bs0 = mwoff + nm + 1, *bs1 = bs0 + nb;
+  const unsigned tb = 256, tg = (nm + tb - 1) / tb;
+  // the segment counts go to d_msg_seg_off[0..nm) and are scanned into it
+  // (e4_scan_down: each thread reads its entries before it writes them)
+  hipLaunchKernelGGL(cpk::msg_table_kernel, dim3(tg), dim3(tb), 0, s, (const uint8_t *)d_packed,
+                     d_msg_off, nm, traversal_limit_words, mwords, d_msg_seg_off, mbeg, d_msg_status);
+  hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
+                     (const uint64_t *)mwords, nm, bs0);
+  hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
+                     (const uint64_t *)d_msg_seg_off, nm, bs1);
+  hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bs0, nb);
+  hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bs1, nb);
+  hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
+                     (const uint64_t *)mwords, nm, (const uint64_t *)bs0, mwoff);
+  hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
+                     (const uint64_t *)d_msg_seg_off, nm, (const uint64_t *)bs1, d_msg_seg_off);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(&h_totals[0], mwoff + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(&h_totals[1], d_msg_seg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CPK_EDEVICE;
+  if (h_totals[0] > out_cap_words || h_totals[1] > seg_cap) return CPK_ENOMEM;
+  if (h_totals[1] && (!d_seg_word_off || !d_seg_in_off || !d_seg_status)) return CPK_EINVAL;
+  if (!d_seg_word_off) return CPK_OK;  // (no segments: every table failed)
+  hipLaunchKernelGGL(cpk::msg_swo_kernel, dim3(tg), dim3(tb), 0, s, (const uint8_t *)d_packed,
+                     d_msg_off, nm, traversal_limit_words, (const uint64_t *)mwoff,
+                     (const uint64_t *)d_msg_seg_off, (const int32_t *)d_msg_status, d_seg_word_off);
+  if (h_totals[1]) {
+    if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
+      return CPK_EDEVICE;
+    const unsigned per_cu = (unsigned)min(8u, 160u * 1024u / cpk::kDecLds);
+    unsigned grid = per_cu * (unsigned)ctx->cus;
+    if (grid > (nm + 3) / 4) grid = (nm + 3) / 4;
+    // the stream ends overwrite the words array (no longer needed)
+    hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
+                       (const uint8_t *)d_packed, d_seg_in_off, (const uint64_t *)d_seg_word_off,
+                       (uint32_t)h_totals[1], (uint64_t *)d_out, d_seg_status,
+                       ctx->tickets + cpk::kTkDec, (uint64_t)0,
+                       cpk::DecStreams{mbeg, d_msg_off + 1, d_msg_seg_off, nm, mwords});
+    hipLaunchKernelGGL(cpk::msg_final_kernel, dim3(tg), dim3(tb), 0, s, d_msg_off, nm,
+                       (const uint64_t *)d_msg_seg_off, (const uint64_t *)mwords,
+                       (const int32_t *)d_seg_status, d_msg_status);
+  }
   return hip_ok(hipGetLastError());
 }
 

@@ -48,6 +48,9 @@ extern "C" {
  *   CPK_ETRAILING batch form only: the piece was filled before the end of
  *                 its packed byte range (the reference would leave the
  *                 bytes to the next read()).
+ *   CPK_EFRAME    segment table invalid: count over 512, a negative size, a
+ *                 message over the traversal limit or a segment over 2^28-1
+ *                 words -> DecodeException (Serialize.java:45-53, :125-163).
  *   CPK_ENOMEM, CPK_EDEVICE  allocation / HIP runtime failure (-> IOException).
  *   CPK_EUNSUPPORTED  a piece outside what this build handles.
  */
@@ -58,6 +61,7 @@ extern "C" {
 #define CPK_ETRAILING (-4)
 #define CPK_ENOMEM (-5)
 #define CPK_EDEVICE (-6)
+#define CPK_EFRAME (-7)
 #define CPK_EUNSUPPORTED (-8)
 
 typedef struct cpk_ctx_s *cpk_ctx;
@@ -128,6 +132,35 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
 int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
                       const uint64_t *d_seg_word_off, uint32_t n, void *d_out,
                       uint64_t *d_in_off, int32_t *d_status, void *stream);
+
+/* Batch of packed messages (Serialize.read over PackedInputStream for each,
+ * SerializePacked.read, Serialize.java:119-178): message m is the packed
+ * bytes [d_msg_off[m], d_msg_off[m+1]) -- its segment table (two read()
+ * calls: the first word, then 4 * (count & ~1) bytes), validated, then its
+ * segments back to back.  Segments of all messages are written contiguously
+ * in message order:
+ *   d_msg_seg_off   : uint64[nm+1], written: message m's segments are
+ *                     [d_msg_seg_off[m], d_msg_seg_off[m+1]) (none when its
+ *                     table failed).
+ *   d_seg_word_off  : uint64[segments+1], written: segment words in d_out.
+ *   d_seg_in_off    : uint64[segments], written: segment packed starts.
+ *   d_seg_status    : int32[segments], written (a failed segment stops its
+ *                     message: later segments carry its status).
+ *   d_msg_status    : int32[nm], written: CPK_OK, the table's error
+ *                     (CPK_EFRAME, CPK_ETRUNC, ...), the first failed
+ *                     segment's, or CPK_ETRAILING if the message's bytes
+ *                     outlast its segments.
+ *   traversal_limit_words: ReaderOptions.traversalLimitInWords (reference
+ *                     default 8 Mi words).
+ *   h_totals[2]     : host, written: total words, total segments.
+ * The call synchronises `stream` once (to read the totals) and returns
+ * CPK_ENOMEM, without decoding, if they exceed out_cap_words / seg_cap.
+ * d_packed readable up to round_up(d_msg_off[nm], 16). */
+int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg_off, uint32_t nm,
+                        uint64_t traversal_limit_words, void *d_out, uint64_t out_cap_words,
+                        uint64_t *d_seg_word_off, uint64_t *d_seg_in_off, int32_t *d_seg_status,
+                        uint32_t seg_cap, uint64_t *d_msg_seg_off, int32_t *d_msg_status,
+                        uint64_t *h_totals, void *stream);
 
 /* Host-memory convenience forms (the socket/file ByteBuffer path,
  * SerializePacked.java:75-96, :119-134).  Synchronous.  encode_host and

@@ -324,6 +324,7 @@ int cpko_read_message(const uint8_t *in, size_t in_len, size_t *consumed,
   if (8 * total > out_cap) return CPKO_EINVAL;
   size_t op = 0;
   for (uint32_t i = 0; i < count; ++i) {                 /* :165-175 */
+    if (seg_words[i] > 0x0fffffffu) return CPKO_EFRAME;  /* makeByteBufferForWords, :45-53 */
     size_t bytes = 8 * (size_t)seg_words[i];
     st = cpko_unpack(in + ip, in_len - ip, &used, out + op, bytes);
     if (st) return st;

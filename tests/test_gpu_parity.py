@@ -406,3 +406,79 @@ def test_host_forms_pipelined_chunks(ctx, oracle, chunk_kb, monkeypatch):
         if ost == oracle.OK and used != len(p):
             ost = oracle.ETRAILING
         assert st[i] == ost, (i, st[i], ost)
+
+
+def _message_cases(oracle, rng, limit):
+    """Packed messages (SerializePacked.write) and broken ones: truncated,
+    trailing bytes, flipped table bytes, segment count over 512, negative
+    sizes, over the traversal limit."""
+    import struct
+    msgs = []
+    for i in range(400):
+        nseg = int(rng.choice([1, 1, 2, 3, 4, 7, 40])) if i != 5 else 512
+        sizes = [int(rng.choice([0, 1, 3, 50, 700, 3000])) for _ in range(nseg)]
+        segs = [_random_words(rng, s, [.4, .3, .2, .1]).tobytes() for s in sizes]
+        m = bytearray(oracle.write_message(segs))
+        r = int(rng.integers(0, 12))
+        if r == 0 and len(m) > 1:
+            m = m[: int(rng.integers(1, len(m)))]
+        elif r == 1:
+            m += bytes(rng.integers(0, 256, size=int(rng.integers(1, 9)), dtype=np.uint8))
+        elif r == 2:
+            j = int(rng.integers(0, min(len(m), 12)))
+            m[j] = int(rng.integers(0, 256))
+        elif r in (3, 4, 5):
+            # a hand-made table: count over 512 / a negative size / over the limit
+            cnt = {3: 600, 4: 2, 5: 2}[r]
+            vals = {3: [0], 4: [5, -3], 5: [limit, 1]}[r]
+            words = ((cnt + 2) & ~1) // 2 if r != 3 else 1
+            tb = struct.pack("<I", cnt - 1) + b"".join(struct.pack("<i", v) for v in vals)
+            tb = (tb + b"\0" * (8 * words))[: 8 * words]
+            m = bytearray(oracle.pack(tb)) + m[8:]
+        msgs.append(bytes(m))
+    return msgs
+
+
+def test_decode_messages_matches_serialize_read(ctx, oracle):
+    """cpk_decode_messages (segment tables read and validated on the device,
+    Serialize.java:119-178) against the oracle's Serialize.read, per message."""
+    import torch
+    import capnp_packed as cp
+    rng = np.random.default_rng(31)
+    limit = 1 << 16
+    msgs = _message_cases(oracle, rng, limit)
+    moff = _swo([len(m) for m in msgs])
+    blob = b"".join(msgs) + b"\0" * 48
+    d_pk = torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).cuda()
+    d_moff = torch.from_numpy(moff.astype(np.int64)).cuda()
+    nm = len(msgs)
+    d_mseg = torch.zeros(nm + 1, dtype=torch.int64, device="cuda")
+    d_mst = torch.zeros(nm, dtype=torch.int32, device="cuda")
+    # sizing call: capacities of 0 -> CPK_ENOMEM with the totals
+    rc, W, S = ctx.decode_messages(d_pk, d_moff, None, None, None, None, d_mseg, d_mst,
+                                   traversal_limit_words=limit)
+    assert rc == cp.ENOMEM and S > 0
+    d_out = torch.zeros(W + 1, dtype=torch.int64, device="cuda")
+    d_swo = torch.zeros(S + 1, dtype=torch.int64, device="cuda")
+    d_sin = torch.zeros(S + 1, dtype=torch.int64, device="cuda")
+    d_sst = torch.zeros(S, dtype=torch.int32, device="cuda")
+    rc, W2, S2 = ctx.decode_messages(d_pk, d_moff, d_out, d_swo, d_sin, d_sst, d_mseg, d_mst,
+                                     traversal_limit_words=limit)
+    torch.cuda.synchronize()
+    assert rc == cp.OK and (W2, S2) == (W, S)
+    out = d_out.cpu().numpy().view(np.uint8)
+    swo = d_swo.cpu().numpy()
+    mseg = d_mseg.cpu().numpy()
+    mst = d_mst.cpu().numpy()
+    kinds = set()
+    for i, m in enumerate(msgs):
+        ost, segs, used = oracle.read_message(m, traversal_limit_words=limit,
+                                              out_cap=8 * limit + 4096)
+        if ost == oracle.OK and used != len(m):
+            ost = oracle.ETRAILING
+        kinds.add(ost)
+        assert mst[i] == ost, (i, mst[i], ost, m[:16].hex())
+        if ost == oracle.OK:
+            got = [out[8 * swo[j]: 8 * swo[j + 1]].tobytes() for j in range(mseg[i], mseg[i + 1])]
+            assert got == segs, i
+    assert {oracle.OK, oracle.ETRAILING, oracle.ETRUNC, cp.EFRAME} <= kinds, kinds
