@@ -31,7 +31,7 @@ EXPORTS = [
     "cpk_ctx_create", "cpk_ctx_destroy", "cpk_ctx_device", "cpk_encode_batch",
     "cpk_decode_batch", "cpk_decode_stream", "cpk_encode_host", "cpk_decode_host",
     "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch", "cpk_ctx_take_error",
-    "cpk_decode_messages",
+    "cpk_decode_messages", "cpk_encode_messages",
 ]
 
 
@@ -85,6 +85,7 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_count_mismatch": ([vp, vp, vp, u64, vp, vp], i32),
         "cpk_ctx_take_error": ([vp, vp], i32),
         "cpk_decode_messages": ([vp, vp, vp, u32, u64, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp], i32),
+        "cpk_encode_messages": ([vp, vp, vp, u32, vp, u32, u64, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         if not strict and not hasattr(L, name):
@@ -164,6 +165,19 @@ class Context:
                                         d_seg_word_off.data_ptr(), n, d_out.data_ptr(),
                                         d_status.data_ptr(), self._stream(stream))
         _check(rc, "cpk_decode_batch")
+
+    def encode_messages(self, d_in, d_seg_word_off, d_msg_seg_off, max_seg_words: int, d_out,
+                        d_out_off, stream=None):
+        """SerializePacked.write per message (cpk_encode_messages): the
+        segment tables are built and packed on the device.  d_out_off gets
+        nm + nseg + 1 piece offsets in message order."""
+        nseg = d_seg_word_off.numel() - 1
+        nm = d_msg_seg_off.numel() - 1
+        rc = self._lib.cpk_encode_messages(self.handle, d_in.data_ptr(), d_seg_word_off.data_ptr(),
+                                           nseg, d_msg_seg_off.data_ptr(), nm, int(max_seg_words),
+                                           d_out.data_ptr(), d_out_off.data_ptr(),
+                                           self._stream(stream))
+        _check(rc, "cpk_encode_messages")
 
     def decode_messages(self, d_packed, d_msg_off, d_out, d_seg_word_off, d_seg_in_off,
                         d_seg_status, d_msg_seg_off, d_msg_status,

@@ -1914,6 +1914,102 @@ __global__ void msg_final_kernel(const uint64_t *__restrict__ moff, uint32_t nm,
   mstatus[m] = st != CPK_OK ? st : (mend[m] != moff[m + 1] ? CPK_ETRAILING : CPK_OK);
 }
 
+// ---- message write: Serialize.write = table piece + segment pieces --------
+// PackedOutputStream.write (:35-205) byte-serial over a word source, as the
+// oracle restates it (oracle/packed_oracle.c:cpko_pack); for the segment
+// tables (a thread per message).  word(i) -> word i; emit(byte).
+template <class Wf, class Ef>
+__device__ void serial_pack(uint32_t nwords, Wf word, Ef emit) {
+  uint32_t i = 0;
+  while (i < nwords) {
+    const uint64_t w = word(i++);
+    uint32_t tag = 0;
+    for (int b = 0; b < 8; ++b) tag |= ((w >> (8 * b)) & 0xffu) ? (1u << b) : 0u;
+    emit(tag);
+    for (int b = 0; b < 8; ++b)
+      if ((tag >> b) & 1) emit((uint32_t)(w >> (8 * b)) & 0xffu);
+    if (tag == 0) {  // :119-131
+      uint32_t run = 0;
+      while (i < nwords && run < 255 && word(i) == 0) {
+        ++run;
+        ++i;
+      }
+      emit(run);
+    } else if (tag == 0xffu) {  // :133-193: stop before a word with >= 2 zero bytes
+      uint32_t run = 0;
+      while (i < nwords && run < 255) {
+        const uint64_t x = word(i);
+        int z = 0;
+        for (int b = 0; b < 8; ++b) z += ((x >> (8 * b)) & 0xffu) == 0;
+        if (z >= 2) break;
+        ++run;
+        ++i;
+      }
+      emit(run);
+      for (uint32_t k = i - run; k < i; ++k) {
+        const uint64_t x = word(k);
+        for (int b = 0; b < 8; ++b) emit((uint32_t)(x >> (8 * b)) & 0xffu);
+      }
+    }
+  }
+}
+
+// word k of message m's segment table (Serialize.java:256-273): ints
+// [count - 1, size_0 .. size_{count-1}, 0 pad], (count + 2) & ~1 of them
+__device__ __forceinline__ uint64_t table_word(const uint64_t *swo, uint64_t s0, uint32_t count,
+                                               uint32_t k) {
+  uint32_t v[2];
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t j = 2 * k + h;
+    v[h] = j == 0 ? count - 1 : (j <= count ? (uint32_t)(swo[s0 + j] - swo[s0 + j - 1]) : 0u);
+  }
+  return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+}
+__device__ __forceinline__ uint32_t table_words(uint32_t count) { return ((count + 2) & ~1u) / 2; }
+
+// packed size of every message's table
+__global__ void msg_table_size_kernel(const uint64_t *__restrict__ swo,
+                                      const uint64_t *__restrict__ mseg, uint32_t nm,
+                                      uint64_t *__restrict__ tsize) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nm) return;
+  const uint64_t s0 = mseg[m];
+  const uint32_t count = (uint32_t)(mseg[m + 1] - s0);
+  uint64_t nb = 0;
+  serial_pack(table_words(count), [&](uint32_t k) { return table_word(swo, s0, count, k); },
+              [&](uint32_t) { ++nb; });
+  tsize[m] = nb;
+}
+
+// piece sizes in message order: table, then its segments
+__global__ void msg_interleave_kernel(const uint64_t *__restrict__ mseg, uint32_t nm,
+                                      const uint64_t *__restrict__ tsize,
+                                      const uint64_t *__restrict__ ssize, uint64_t *__restrict__ comb) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nm) return;
+  const uint64_t s0 = mseg[m], s1 = mseg[m + 1];
+  uint64_t *c = comb + s0 + m;
+  c[0] = tsize[m];
+  for (uint64_t s = s0; s < s1; ++s) c[1 + s - s0] = ssize[s];
+}
+
+// each segment's packed offset (from the message-order offsets), and the
+// tables' packed bytes
+__global__ void msg_table_emit_kernel(const uint64_t *__restrict__ swo,
+                                      const uint64_t *__restrict__ mseg, uint32_t nm,
+                                      const uint64_t *__restrict__ poff, uint64_t *__restrict__ soff,
+                                      uint8_t *__restrict__ out) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nm) return;
+  const uint64_t s0 = mseg[m], s1 = mseg[m + 1];
+  const uint64_t *c = poff + s0 + m;
+  for (uint64_t s = s0; s < s1; ++s) soff[s] = c[1 + s - s0];
+  uint8_t *o = out + c[0];
+  const uint32_t count = (uint32_t)(s1 - s0);
+  serial_pack(table_words(count), [&](uint32_t k) { return table_word(swo, s0, count, k); },
+              [&](uint32_t b) { *o++ = (uint8_t)b; });
+}
+
 // ------------------------------------------------------------ bench support
 struct FastRand {
   int32_t x, y, z, w;
@@ -2260,6 +2356,60 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
                      (const uint64_t *)d_in, d_swo, n, (const uint64_t *)d_out_off,
                      (uint8_t *)d_out, ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv,
                      stride);
+  return hip_ok(hipGetLastError());
+}
+
+int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t nseg,
+                        const uint64_t *d_msg_seg_off, uint32_t nm, uint64_t max_seg_words,
+                        void *d_out, uint64_t *d_out_off, void *stream) {
+  if (!ctx || !d_out_off || (nm && !d_msg_seg_off) || (nseg && !d_swo)) return CPK_EINVAL;
+  if (((uintptr_t)d_out & 15) || ((uintptr_t)d_in & 7)) return CPK_EINVAL;
+  if (max_seg_words == 0) return CPK_EINVAL;  // (a bound is needed for the step rows)
+  DeviceGuard g(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (nm == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
+  const uint64_t np = (uint64_t)nm + nseg;  // pieces: a table per message + the segments
+  if (np > 0xffffffffull) return CPK_EINVAL;
+  const uint32_t nb = (uint32_t)((np + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
+  // scratch: segment sizes | table sizes | message-order sizes | segment offsets | block sums
+  int rc = ensure_status(ctx, (uint64_t)nseg + nm + np + nseg + nb + 1);
+  if (rc) return rc;
+  uint64_t *ssize = ctx->status, *tsize = ssize + nseg, *comb = tsize + nm, *soff = comb + np;
+  uint64_t *bsum = soff + nseg;
+  uint64_t stride = (max_seg_words + 63) / 64;
+  if (nseg && stride > (1ull << 29) / nseg) return CPK_EUNSUPPORTED;  // (> 4 GiB of step rows)
+  const uint64_t rows = (uint64_t)(nseg ? nseg : 1) * stride;
+  if (rows > ctx->e4_bv_cap) {
+    if (ctx->e4_bv) hipFree(ctx->e4_bv);
+    ctx->e4_bv = nullptr;
+    ctx->e4_bv_cap = 0;
+    const uint64_t cap = rows + rows / 4;
+    if (hipMalloc(&ctx->e4_bv, cap * 8) != hipSuccess) return CPK_ENOMEM;
+    ctx->e4_bv_cap = cap;
+  }
+  if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
+  const unsigned tb = 256, tg = (nm + tb - 1) / tb;
+  unsigned grid = (unsigned)(8 * ctx->cus);
+  if (grid > (nseg + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (nseg + cpk::kE4Waves - 1) / cpk::kE4Waves;
+  if (nseg)
+    hipLaunchKernelGGL(cpk::e4_size_kernel, dim3(grid), dim3(cpk::kE4Threads), 0, s,
+                       (const uint64_t *)d_in, d_swo, nseg, ssize, ctx->tickets + cpk::kTkEnc,
+                       max_seg_words, ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride);
+  hipLaunchKernelGGL(cpk::msg_table_size_kernel, dim3(tg), dim3(tb), 0, s, d_swo, d_msg_seg_off, nm,
+                     tsize);
+  hipLaunchKernelGGL(cpk::msg_interleave_kernel, dim3(tg), dim3(tb), 0, s, d_msg_seg_off, nm,
+                     (const uint64_t *)tsize, (const uint64_t *)ssize, comb);
+  hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
+                     (const uint64_t *)comb, (uint32_t)np, bsum);
+  hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bsum, nb);
+  hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
+                     (const uint64_t *)comb, (uint32_t)np, (const uint64_t *)bsum, d_out_off);
+  hipLaunchKernelGGL(cpk::msg_table_emit_kernel, dim3(tg), dim3(tb), 0, s, d_swo, d_msg_seg_off, nm,
+                     (const uint64_t *)d_out_off, soff, (uint8_t *)d_out);
+  if (nseg)
+    hipLaunchKernelGGL(cpk::e4_emit_kernel, dim3(grid), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
+                       (const uint64_t *)d_in, d_swo, nseg, (const uint64_t *)soff, (uint8_t *)d_out,
+                       ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv, stride);
   return hip_ok(hipGetLastError());
 }
 

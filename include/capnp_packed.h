@@ -105,6 +105,27 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_seg_word_o
                      uint32_t n, uint64_t max_seg_words, void *d_out,
                      uint64_t *d_out_off, void *stream);
 
+/* Batch of messages (Serialize.write through PackedOutputStream for each,
+ * SerializePacked.write, Serialize.java:256-288): message m's segments are
+ * pieces [d_msg_seg_off[m], d_msg_seg_off[m+1]) of d_in / d_seg_word_off
+ * (nseg pieces in message order, d_msg_seg_off[0] = 0, [nm] = nseg); its segment table (count - 1, the sizes in
+ * words, zero pad; :256-273) is built and packed on the device, so the
+ * output holds, per message, packed(table) || packed(seg 0) || ... -- the
+ * bytes SerializePacked.write produces, messages back to back.
+ *   max_seg_words   : host bound on every segment's words (required, > 0;
+ *                     a segment over it is reported by cpk_ctx_take_error).
+ *   d_out           : 16-byte aligned, capacity cpk_batch_packed_capacity()
+ *                     of the segments + 10 * ((count + 2) / 2 + 1) bytes per
+ *                     message of `count` segments.
+ *   d_out_off       : uint64[nm + nseg + 1], written: piece offsets in
+ *                     message order (table, segments; next message); message
+ *                     m starts at d_out_off[d_msg_seg_off[m] + m] and the
+ *                     last entry is the total.
+ * Asynchronous on `stream`. */
+int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_seg_word_off,
+                        uint32_t nseg, const uint64_t *d_msg_seg_off, uint32_t nm,
+                        uint64_t max_seg_words, void *d_out, uint64_t *d_out_off, void *stream);
+
 /* Synchronises `stream` and returns CPK_EINVAL if an encode issued since the
  * last call met a piece larger than its max_seg_words bound, else CPK_OK
  * (clears the flag).  The host forms below check it themselves. */

@@ -482,3 +482,70 @@ def test_decode_messages_matches_serialize_read(ctx, oracle):
             got = [out[8 * swo[j]: 8 * swo[j + 1]].tobytes() for j in range(mseg[i], mseg[i + 1])]
             assert got == segs, i
     assert {oracle.OK, oracle.ETRAILING, oracle.ETRUNC, cp.EFRAME} <= kinds, kinds
+
+
+def test_encode_messages_matches_serialize_write(ctx, oracle):
+    """cpk_encode_messages (segment tables built and packed on the device)
+    == SerializePacked.write per message, back to back; then the device
+    message decode reads them back."""
+    import torch
+    import capnp_packed as cp
+    rng = np.random.default_rng(41)
+    msgs = []
+    for i in range(300):
+        nseg = int(rng.choice([1, 1, 2, 3, 4, 5, 40])) if i not in (7, 8) else (512 if i == 7 else 600)
+        sizes = [int(rng.choice([0, 1, 2, 17, 300, 2000, 9000])) for _ in range(nseg)]
+        if i % 50 == 3:
+            sizes = [0x1ff01, 70000][: nseg] if nseg <= 2 else sizes  # table bytes with runs
+        msgs.append([_random_words(rng, s, [.4, .3, .2, .1]).tobytes() for s in sizes])
+    segs = [s for m in msgs for s in m]
+    swo = _swo([len(s) // 8 for s in segs])
+    mseg = _swo([len(m) for m in msgs])
+    data = np.frombuffer(b"".join(segs) + b"\0" * 8, np.uint8)
+    d_in = torch.from_numpy(data.view(np.int64).copy()).cuda()
+    d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
+    d_mseg = torch.from_numpy(mseg.astype(np.int64)).cuda()
+    cap = cp.batch_capacity(swo) + sum(10 * ((len(m) + 2) // 2 + 1) for m in msgs)
+    d_pk = torch.zeros((cap + 63) // 16 * 16, dtype=torch.uint8, device="cuda")
+    d_off = torch.zeros(len(msgs) + len(segs) + 1, dtype=torch.int64, device="cuda")
+    maxw = int(max(np.diff(swo)))
+    ctx.encode_messages(d_in, d_swo, d_mseg, maxw, d_pk, d_off)
+    assert ctx.take_error() == cp.OK
+    off = d_off.cpu().numpy()
+    want = b"".join(oracle.write_message(m) for m in msgs)
+    assert int(off[-1]) == len(want)
+    assert d_pk[: len(want)].cpu().numpy().tobytes() == want
+    # piece offsets: table, then segments, per message
+    o, k = 0, 0
+    for m in msgs:
+        nseg = len(m)
+        tb = ((nseg - 1) & 0xffffffff).to_bytes(4, "little") + b"".join(
+            (len(s) // 8).to_bytes(4, "little") for s in m)
+        tb += b"\0" * (-len(tb) % 8)
+        for piece in [tb] + m:
+            assert int(off[k]) == o, k
+            o += len(oracle.pack(piece))
+            k += 1
+    # and back: the message ranges are the table pieces' offsets
+    starts = off[(mseg[:-1] + np.arange(len(msgs))).astype(np.int64)]
+    d_moff = torch.from_numpy(np.append(starts, off[-1]).astype(np.int64)).cuda()
+    nm = len(msgs)
+    d_mso = torch.zeros(nm + 1, dtype=torch.int64, device="cuda")
+    d_mst = torch.zeros(nm, dtype=torch.int32, device="cuda")
+    d_out = torch.zeros(int(swo[-1]) + 1, dtype=torch.int64, device="cuda")
+    S = len(segs)
+    d_sw = torch.zeros(S + 1, dtype=torch.int64, device="cuda")
+    d_si = torch.zeros(S + 1, dtype=torch.int64, device="cuda")
+    d_ss = torch.zeros(S, dtype=torch.int32, device="cuda")
+    rc, W, S2 = ctx.decode_messages(d_pk, d_moff, d_out, d_sw, d_si, d_ss, d_mso, d_mst,
+                                    traversal_limit_words=1 << 24)
+    torch.cuda.synchronize()
+    st = d_mst.cpu().numpy()
+    assert rc == cp.OK
+    for i, m in enumerate(msgs):
+        # over 512 segments: Serialize.read rejects what Serialize.write wrote
+        assert st[i] == (cp.EFRAME if len(m) > 512 else cp.OK), i
+    ok = [len(m) <= 512 for m in msgs]
+    assert S2 == sum(len(m) for m, g in zip(msgs, ok) if g)
+    got = d_out.cpu().numpy().view(np.uint8)[: 8 * W].tobytes()
+    assert got == b"".join(s for m, g in zip(msgs, ok) if g for s in m)
