@@ -1,8 +1,9 @@
-"""Message-batch decode (cpk_decode_messages: segment tables read and
-validated on the device) against the piece batch decode of the same bytes
-(cpk_decode_batch with every piece's packed offsets known), on config-3
-shaped messages: 4 segments of 4-256 KiB each, dense data, preceded by
-their packed segment table.  For DESIGN.md; not the bench metric.
+"""Message batches on config-3 shaped messages (4 segments of 4-256 KiB,
+dense data, each message preceded by its packed segment table):
+cpk_encode_messages (tables built and packed on the device) against
+cpk_encode_batch with the table pieces supplied, and cpk_decode_messages
+(tables read and validated on the device) against cpk_decode_batch with
+every piece's packed offsets known.  For DESIGN.md; not the bench metric.
 usage: python tools/msg_bench.py [messages]"""
 import sys
 from pathlib import Path
@@ -89,10 +90,32 @@ def timed(f, reps=5):
     return sorted(ts)[len(ts) // 2]
 
 
+# message encode: the segments alone (tables built on the device); bytes
+# must equal the piece encode with the table pieces supplied
+segmask = torch.ones(int(swo[-1]), dtype=torch.bool, device="cuda")
+segmask[idx] = False
+d_seg = torch.empty(U // 8 + 1, dtype=torch.int64, device="cuda")
+d_seg[: U // 8] = d_in[: int(swo[-1])][segmask]
+del segmask
+sswo = np.concatenate([[0], np.cumsum(seg.reshape(-1))]).astype(np.int64)
+d_sswo = torch.from_numpy(sswo).cuda()
+d_msegs = torch.arange(0, 4 * nm + 1, 4, dtype=torch.int64, device="cuda")
+d_pk2 = torch.zeros_like(d_pk)
+d_off2 = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+ctx.encode_messages(d_seg, d_sswo, d_msegs, 32768, d_pk2, d_off2)
+assert ctx.take_error() == 0
+assert torch.equal(d_off2, d_off) and torch.equal(d_pk2[:P], d_pk[:P])
+t_em = timed(lambda: ctx.encode_messages(d_seg, d_sswo, d_msegs, 32768, d_pk2, d_off2))
+t_eb = timed(lambda: ctx.encode_batch(d_in, d_swo, 32768, d_pk2, d_off2))
+
 t_m = timed(run_msgs)
 t_b = timed(lambda: ctx.decode_batch(d_pk, d_off, d_swo, d_bout, d_bst))
 G = float(1 << 30)
 print(f"{nm} messages x 4 segments, U = {U / G:.2f} GiB, P/U = {P / U:.4f}")
+print(f"  encode_messages (tables built on device):                   {U / G / t_em:8.1f} GiB/s"
+      f"  ({t_em * 1e3:.2f} ms)")
+print(f"  encode_batch (table pieces supplied):                       {U / G / t_eb:8.1f} GiB/s"
+      f"  ({t_eb * 1e3:.2f} ms)")
 print(f"  decode_messages (tables on device, one stream per message): {U / G / t_m:8.1f} GiB/s"
       f"  ({t_m * 1e3:.2f} ms, incl. one host sync)")
 print(f"  decode_batch (every piece's offsets known):                 {U / G / t_b:8.1f} GiB/s"
