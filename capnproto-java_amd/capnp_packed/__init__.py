@@ -31,7 +31,8 @@ EXPORTS = [
     "cpk_ctx_create", "cpk_ctx_destroy", "cpk_ctx_device", "cpk_encode_batch",
     "cpk_decode_batch", "cpk_decode_stream", "cpk_encode_host", "cpk_decode_host",
     "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch", "cpk_ctx_take_error",
-    "cpk_decode_messages", "cpk_encode_messages",
+    "cpk_decode_messages", "cpk_encode_messages", "cpk_encode_messages_host",
+    "cpk_decode_messages_host",
 ]
 
 
@@ -86,6 +87,8 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_ctx_take_error": ([vp, vp], i32),
         "cpk_decode_messages": ([vp, vp, vp, u32, u64, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp], i32),
         "cpk_encode_messages": ([vp, vp, vp, u32, vp, u32, u64, vp, vp, vp], i32),
+        "cpk_encode_messages_host": ([vp, vp, vp, u32, vp, u32, vp, u64, vp], i32),
+        "cpk_decode_messages_host": ([vp, vp, vp, u32, u64, vp, u64, vp, u32, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         if not strict and not hasattr(L, name):
@@ -249,6 +252,55 @@ class Context:
         if rc not in (OK, ETRUNC, EOVERRUN, ETRAILING, EUNSUPPORTED, EINVAL):
             _check(rc, "cpk_decode_host")
         return out[: int(8 * swo[-1])], st[:n]
+
+
+def _encode_messages_host(self, messages):
+    """SerializePacked.write for each message (a list of segments, bytes of
+    whole words) -> the packed bytes of all messages, back to back."""
+    segs = [bytes(s) for m in messages for s in m]
+    swo = np.concatenate([[0], np.cumsum([len(s) // 8 for s in segs], dtype=np.uint64)]).astype(np.uint64)
+    mso = np.concatenate([[0], np.cumsum([len(m) for m in messages], dtype=np.uint64)]).astype(np.uint64)
+    data = np.frombuffer(b"".join(segs) + b"\0" * 8, np.uint8)
+    cap = batch_capacity(swo) + sum(10 * ((len(m) + 2) // 2 + 1) for m in messages)
+    out = np.zeros(cap, np.uint8)
+    off = np.zeros(len(messages) + len(segs) + 1, np.uint64)
+    _check(self._lib.cpk_encode_messages_host(self.handle, data.ctypes.data, swo.ctypes.data,
+                                              len(segs), mso.ctypes.data, len(messages),
+                                              out.ctypes.data, cap, off.ctypes.data),
+           "cpk_encode_messages_host")
+    return out[: int(off[-1])].tobytes(), off
+
+
+def _decode_messages_host(self, packed, msg_off, traversal_limit_words: int = 8 * 1024 * 1024):
+    """Serialize.read per message -> (message statuses, [[segment bytes]])."""
+    pk = np.frombuffer(bytes(packed), np.uint8)
+    mo = np.ascontiguousarray(msg_off, dtype=np.uint64)
+    nm = len(mo) - 1
+    mso = np.zeros(nm + 1, np.uint64)
+    mst = np.zeros(max(nm, 1), np.int32)
+    tot = np.zeros(2, np.uint64)
+    pkp = pk.ctypes.data if pk.size else None
+    rc = self._lib.cpk_decode_messages_host(self.handle, pkp, mo.ctypes.data, nm,
+                                            traversal_limit_words, None, 0, None, 0,
+                                            mso.ctypes.data, mst.ctypes.data, tot.ctypes.data)
+    if rc == ENOMEM:
+        out = np.zeros(int(tot[0]) * 8 + 8, np.uint8)
+        sw = np.zeros(int(tot[1]) + 1, np.uint64)
+        rc = self._lib.cpk_decode_messages_host(self.handle, pkp, mo.ctypes.data, nm,
+                                                traversal_limit_words, out.ctypes.data, int(tot[0]),
+                                                sw.ctypes.data, int(tot[1]), mso.ctypes.data,
+                                                mst.ctypes.data, tot.ctypes.data)
+    else:
+        out, sw = np.zeros(8, np.uint8), np.zeros(1, np.uint64)
+    if rc in (ENOMEM, EDEVICE):
+        _check(rc, "cpk_decode_messages_host")
+    msgs = [[out[8 * int(sw[j]): 8 * int(sw[j + 1])].tobytes() for j in range(int(mso[m]), int(mso[m + 1]))]
+            for m in range(nm)]
+    return mst[:nm], msgs
+
+
+Context.encode_messages_host = _encode_messages_host
+Context.decode_messages_host = _decode_messages_host
 
 
 def _decode_stream_host(self, packed: np.ndarray, seg_word_off: np.ndarray):

@@ -367,3 +367,115 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
 }
 
 }  // extern "C"
+
+// ---- message batches from host memory (staged whole; SerializePacked.write /
+// read for many messages, the JNI facade's encodeMessages / decodeMessages) --
+namespace {
+struct DevBufs {  // hipFree on scope exit
+  std::vector<void *> p;
+  void *get(uint64_t bytes) {
+    void *q = nullptr;
+    if (hipMalloc(&q, bytes ? bytes : 16) != hipSuccess) return nullptr;
+    p.push_back(q);
+    return q;
+  }
+  ~DevBufs() {
+    for (void *q : p) hipFree(q);
+  }
+};
+}  // namespace
+
+extern "C" {
+
+int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32_t nseg,
+                             const uint64_t *h_msg_seg_off, uint32_t nm, void *h_out,
+                             uint64_t h_out_cap, uint64_t *h_out_off) {
+  if (!ctx || !h_swo || !h_msg_seg_off || !h_out_off) return CPK_EINVAL;
+  if (h_msg_seg_off[0] != 0 || h_msg_seg_off[nm] != nseg) return CPK_EINVAL;
+  for (uint32_t m = 0; m < nm; ++m)
+    if (h_msg_seg_off[m + 1] < h_msg_seg_off[m]) return CPK_EINVAL;
+  uint64_t maxw = 1, cap = 16;
+  for (uint32_t i = 0; i < nseg; ++i) {
+    if (h_swo[i + 1] < h_swo[i]) return CPK_EINVAL;
+    const uint64_t w = h_swo[i + 1] - h_swo[i];
+    maxw = w > maxw ? w : maxw;
+    cap += cpk_packed_bound(w);
+  }
+  for (uint32_t m = 0; m < nm; ++m) cap += 10 * ((h_msg_seg_off[m + 1] - h_msg_seg_off[m] + 2) / 2 + 1);
+  if (nm == 0) {
+    h_out_off[0] = 0;
+    return CPK_OK;
+  }
+  DeviceGuard g(ctx->device);
+  const uint64_t words = h_swo[nseg] - h_swo[0];
+  std::vector<uint64_t> rel(nseg + 1);
+  for (uint32_t i = 0; i <= nseg; ++i) rel[i] = h_swo[i] - h_swo[0];
+  DevBufs b;
+  void *d_in = b.get(words * 8 + 8), *d_out = b.get((cap + 15) & ~15ull);
+  uint64_t *d_swo = (uint64_t *)b.get((nseg + 1) * 8ull), *d_ms = (uint64_t *)b.get((nm + 1) * 8ull);
+  uint64_t *d_off = (uint64_t *)b.get(((uint64_t)nm + nseg + 1) * 8);
+  if (!d_in || !d_out || !d_swo || !d_ms || !d_off) return CPK_ENOMEM;
+  if ((words && hipMemcpy(d_in, (const uint8_t *)h_in + 8 * h_swo[0], words * 8, hipMemcpyHostToDevice)) ||
+      hipMemcpy(d_swo, rel.data(), (nseg + 1) * 8ull, hipMemcpyHostToDevice) ||
+      hipMemcpy(d_ms, h_msg_seg_off, (nm + 1) * 8ull, hipMemcpyHostToDevice))
+    return CPK_EDEVICE;
+  int rc = cpk_encode_messages(ctx, d_in, d_swo, nseg, d_ms, nm, maxw, d_out, d_off, nullptr);
+  if (rc) return rc;
+  if ((rc = cpk_ctx_take_error(ctx, nullptr))) return rc;
+  if (hipMemcpy(h_out_off, d_off, ((uint64_t)nm + nseg + 1) * 8, hipMemcpyDeviceToHost))
+    return CPK_EDEVICE;
+  const uint64_t P = h_out_off[(uint64_t)nm + nseg];
+  if (P > h_out_cap) return CPK_ENOMEM;
+  return hip_ok(hipMemcpy(h_out, d_out, P, hipMemcpyDeviceToHost));
+}
+
+int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_msg_off, uint32_t nm,
+                             uint64_t traversal_limit_words, void *h_out, uint64_t out_cap_words,
+                             uint64_t *h_seg_word_off, uint32_t seg_cap, uint64_t *h_msg_seg_off,
+                             int32_t *h_msg_status, uint64_t *h_totals) {
+  if (!ctx || !h_msg_off || !h_msg_seg_off || !h_msg_status || !h_totals) return CPK_EINVAL;
+  h_totals[0] = h_totals[1] = 0;
+  if (nm == 0) {
+    h_msg_seg_off[0] = 0;
+    return CPK_OK;
+  }
+  for (uint32_t m = 0; m < nm; ++m)
+    if (h_msg_off[m + 1] < h_msg_off[m]) return CPK_EINVAL;
+  DeviceGuard g(ctx->device);
+  const uint64_t P = h_msg_off[nm] - h_msg_off[0];
+  std::vector<uint64_t> rel(nm + 1);
+  for (uint32_t m = 0; m <= nm; ++m) rel[m] = h_msg_off[m] - h_msg_off[0];
+  DevBufs b;
+  void *d_pk = b.get(P + 64);
+  uint64_t *d_mo = (uint64_t *)b.get((nm + 1) * 8ull), *d_ms = (uint64_t *)b.get((nm + 1) * 8ull);
+  int32_t *d_mst = (int32_t *)b.get(nm * 4ull);
+  if (!d_pk || !d_mo || !d_ms || !d_mst) return CPK_ENOMEM;
+  if (hipMemset(d_pk, 0, P + 64) ||
+      (P && hipMemcpy(d_pk, (const uint8_t *)h_packed + h_msg_off[0], P, hipMemcpyHostToDevice)) ||
+      hipMemcpy(d_mo, rel.data(), (nm + 1) * 8ull, hipMemcpyHostToDevice))
+    return CPK_EDEVICE;
+  // the totals first (the table pass), then the decode into buffers of that size
+  int rc = cpk_decode_messages(ctx, d_pk, d_mo, nm, traversal_limit_words, nullptr, 0, nullptr,
+                               nullptr, nullptr, 0, d_ms, d_mst, h_totals, nullptr);
+  if (rc != CPK_OK && rc != CPK_ENOMEM) return rc;
+  if (h_totals[0] > out_cap_words || h_totals[1] > seg_cap) return CPK_ENOMEM;
+  if (h_totals[1] && (!h_out || !h_seg_word_off)) return CPK_EINVAL;
+  const uint64_t W = h_totals[0], S = h_totals[1];
+  void *d_out = b.get(W * 8 + 8);
+  uint64_t *d_sw = (uint64_t *)b.get((S + 1) * 8), *d_si = (uint64_t *)b.get((S + 1) * 8);
+  int32_t *d_ss = (int32_t *)b.get(S * 4 + 4);
+  if (!d_out || !d_sw || !d_si || !d_ss) return CPK_ENOMEM;
+  rc = cpk_decode_messages(ctx, d_pk, d_mo, nm, traversal_limit_words, d_out, W, d_sw, d_si, d_ss,
+                           (uint32_t)S, d_ms, d_mst, h_totals, nullptr);
+  if (rc) return rc;
+  if (hipDeviceSynchronize() || hipMemcpy(h_msg_seg_off, d_ms, (nm + 1) * 8ull, hipMemcpyDeviceToHost) ||
+      hipMemcpy(h_msg_status, d_mst, nm * 4ull, hipMemcpyDeviceToHost) ||
+      (h_seg_word_off && hipMemcpy(h_seg_word_off, d_sw, (S + 1) * 8, hipMemcpyDeviceToHost)) ||
+      (W && hipMemcpy(h_out, d_out, W * 8, hipMemcpyDeviceToHost)))
+    return CPK_EDEVICE;
+  for (uint32_t m = 0; m < nm; ++m)
+    if (h_msg_status[m] != CPK_OK) return h_msg_status[m];
+  return CPK_OK;
+}
+
+}  // extern "C"

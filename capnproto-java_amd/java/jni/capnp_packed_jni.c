@@ -23,7 +23,7 @@
 
 static void throw_status(JNIEnv *env, int st) {
   const char *cls = (st == CPK_ETRUNC || st == CPK_EOVERRUN || st == CPK_ETRAILING ||
-                     st == CPK_EINVAL)
+                     st == CPK_EINVAL || st == CPK_EFRAME)
                         ? "org/capnproto/DecodeException"
                         : "java/io/IOException";
   jclass c = (*env)->FindClass(env, cls);
@@ -108,4 +108,69 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDecode(
   (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
   (*env)->ReleaseLongArrayElements(env, inOff, io, JNI_ABORT);
   if (st != CPK_OK) throw_status(env, st);
+}
+
+/* Serialize.write for each message (Serialize.java:256-288): segment i of
+ * the batch is words [segWordOff[i], segWordOff[i+1]) of `in` (direct);
+ * message m owns segments [msgSegOff[m], msgSegOff[m+1]).  The tables are
+ * built on the device.  outOff[nm + nseg + 1]: piece offsets, message order. */
+JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeMessages(
+    JNIEnv *env, jclass k, jlong h, jobject in, jlongArray segWordOff, jlongArray msgSegOff,
+    jobject out, jlongArray outOff) {
+  (void)k;
+  void *pin = (*env)->GetDirectBufferAddress(env, in);
+  void *pout = (*env)->GetDirectBufferAddress(env, out);
+  jlong cap = (*env)->GetDirectBufferCapacity(env, out);
+  if (!pin || !pout) {
+    throw_status(env, CPK_EINVAL);
+    return;
+  }
+  jsize ns1 = (*env)->GetArrayLength(env, segWordOff);
+  jsize nm1 = (*env)->GetArrayLength(env, msgSegOff);
+  jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
+  jlong *mso = (*env)->GetLongArrayElements(env, msgSegOff, NULL);
+  jlong *off = (*env)->GetLongArrayElements(env, outOff, NULL);
+  int st = cpk_encode_messages_host((cpk_ctx)(intptr_t)h, pin, (const uint64_t *)swo,
+                                    (uint32_t)(ns1 - 1), (const uint64_t *)mso, (uint32_t)(nm1 - 1),
+                                    pout, (uint64_t)cap, (uint64_t *)off);
+  (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, msgSegOff, mso, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, outOff, off, 0);
+  if (st != CPK_OK) throw_status(env, st);
+}
+
+/* Serialize.read for each message (Serialize.java:119-178): message m is
+ * packed[msgOff[m]..msgOff[m+1]).  totals[2] = {words, segments}.  With
+ * out == null it only sizes the batch (totals written, no exception); else
+ * it fills out, segWordOff[segments+1], msgSegOff[nm+1] and throws the first
+ * failed message's error (DecodeException). */
+JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDecodeMessages(
+    JNIEnv *env, jclass k, jlong h, jobject packed, jlongArray msgOff, jlong traversalLimit,
+    jobject out, jlongArray segWordOff, jlongArray msgSegOff, jlongArray totals) {
+  (void)k;
+  void *ppk = (*env)->GetDirectBufferAddress(env, packed);
+  void *pout = out ? (*env)->GetDirectBufferAddress(env, out) : NULL;
+  jlong ocap = out ? (*env)->GetDirectBufferCapacity(env, out) : 0;
+  if (!ppk || (out && !pout)) {
+    throw_status(env, CPK_EINVAL);
+    return;
+  }
+  jsize nm1 = (*env)->GetArrayLength(env, msgOff);
+  jsize sw1 = segWordOff ? (*env)->GetArrayLength(env, segWordOff) : 0;
+  jlong *mo = (*env)->GetLongArrayElements(env, msgOff, NULL);
+  jlong *ms = (*env)->GetLongArrayElements(env, msgSegOff, NULL);
+  jlong *sw = segWordOff ? (*env)->GetLongArrayElements(env, segWordOff, NULL) : NULL;
+  jlong *tot = (*env)->GetLongArrayElements(env, totals, NULL);
+  int32_t *mst = (int32_t *)calloc((size_t)(nm1 > 1 ? nm1 - 1 : 1), sizeof(int32_t));
+  int st = cpk_decode_messages_host((cpk_ctx)(intptr_t)h, ppk, (const uint64_t *)mo,
+                                    (uint32_t)(nm1 - 1), (uint64_t)traversalLimit, pout,
+                                    (uint64_t)ocap / 8, (uint64_t *)sw,
+                                    (uint32_t)(sw1 > 0 ? sw1 - 1 : 0), (uint64_t *)ms, mst,
+                                    (uint64_t *)tot);
+  free(mst);
+  if (sw) (*env)->ReleaseLongArrayElements(env, segWordOff, sw, 0);
+  (*env)->ReleaseLongArrayElements(env, msgOff, mo, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, msgSegOff, ms, 0);
+  (*env)->ReleaseLongArrayElements(env, totals, tot, 0);
+  if (st != CPK_OK && !(out == NULL && st == CPK_ENOMEM)) throw_status(env, st);
 }

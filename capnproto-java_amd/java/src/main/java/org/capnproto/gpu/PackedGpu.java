@@ -25,6 +25,13 @@ public final class PackedGpu implements AutoCloseable {
     private static native void nativeDecode(long handle, ByteBuffer packed, long[] inOff,
                                             long[] segWordOff, ByteBuffer out);
 
+    private static native void nativeEncodeMessages(long handle, ByteBuffer in, long[] segWordOff,
+                                                    long[] msgSegOff, ByteBuffer out, long[] outOff);
+    private static native void nativeDecodeMessages(long handle, ByteBuffer packed, long[] msgOff,
+                                                    long traversalLimit, ByteBuffer out,
+                                                    long[] segWordOff, long[] msgSegOff,
+                                                    long[] totals);
+
     private long handle;
 
     public PackedGpu(int device) {
@@ -68,6 +75,66 @@ public final class PackedGpu implements AutoCloseable {
         for (ByteBuffer p : pieces) p.position(p.limit());   // as write() leaves inBuf (:203)
         out.limit((int) off[n]);
         return new Packed(out, off);
+    }
+
+    /** SerializePacked.write for each message (its segments, as
+     *  MessageBuilder.getSegmentsForOutput returns them,
+     *  BuilderArena.java:143-154): the segment tables are built and packed on
+     *  the device; the bytes equal one SerializePacked.write per message,
+     *  back to back.  offsets: nm + nseg + 1 piece offsets, message order. */
+    public Packed encodeMessages(ByteBuffer[][] messages) throws IOException {
+        int nm = messages.length, nseg = 0;
+        for (ByteBuffer[] m : messages) nseg += m.length;
+        long[] swo = new long[nseg + 1];
+        long[] mso = new long[nm + 1];
+        long words = 0, tableCap = 0;
+        int s = 0;
+        for (int i = 0; i < nm; ++i) {
+            mso[i] = s;
+            tableCap += 10L * ((messages[i].length + 2) / 2 + 1);
+            for (ByteBuffer b : messages[i]) {
+                if (b.remaining() % 8 != 0) throw new IllegalArgumentException("segment not word-aligned");
+                swo[s++] = words;
+                words += b.remaining() / 8;
+            }
+        }
+        mso[nm] = s;
+        swo[nseg] = words;
+        ByteBuffer in = ByteBuffer.allocateDirect((int) (words * 8 + 8)).order(ByteOrder.LITTLE_ENDIAN);
+        for (ByteBuffer[] m : messages)
+            for (ByteBuffer b : m) in.put(b.duplicate());
+        ByteBuffer out = ByteBuffer.allocateDirect((int) (nativeCapacity(swo) + tableCap));
+        long[] off = new long[nm + nseg + 1];
+        nativeEncodeMessages(handle, in, swo, mso, out, off);
+        out.limit((int) off[nm + nseg]);
+        return new Packed(out, off);
+    }
+
+    /** SerializePacked.read for each message: message m is packed bytes
+     *  [msgOff[m], msgOff[m+1]) (direct buffer).  Returns each message's
+     *  segments (ByteBuffer[] per message, little-endian, as Serialize.read
+     *  hands them to MessageReader, Serialize.java:165-177).
+     *  @throws org.capnproto.DecodeException for the first bad message */
+    public ByteBuffer[][] decodeMessages(ByteBuffer packed, long[] msgOff, long traversalLimitInWords)
+            throws IOException {
+        int nm = msgOff.length - 1;
+        long[] mso = new long[nm + 1];
+        long[] tot = new long[2];
+        nativeDecodeMessages(handle, packed, msgOff, traversalLimitInWords, null, null, mso, tot);
+        ByteBuffer out = ByteBuffer.allocateDirect((int) (tot[0] * 8 + 8)).order(ByteOrder.LITTLE_ENDIAN);
+        long[] swo = new long[(int) tot[1] + 1];
+        nativeDecodeMessages(handle, packed, msgOff, traversalLimitInWords, out, swo, mso, tot);
+        ByteBuffer[][] res = new ByteBuffer[nm][];
+        for (int m = 0; m < nm; ++m) {
+            int a = (int) mso[m], b = (int) mso[m + 1];
+            res[m] = new ByteBuffer[b - a];
+            for (int j = a; j < b; ++j) {
+                ByteBuffer seg = out.duplicate();
+                seg.position((int) (swo[j] * 8)).limit((int) (swo[j + 1] * 8));
+                res[m][j - a] = seg.slice().order(ByteOrder.LITTLE_ENDIAN);
+            }
+        }
+        return res;
     }
 
     /** Unpacks piece i into outs[i] (filled to its limit, like

@@ -201,6 +201,23 @@ int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
                            const uint64_t *h_seg_word_off, uint32_t n, void *h_out,
                            uint64_t *h_in_off, int32_t *h_status);
 
+/* Host-memory forms of the message batches (staged whole through device
+ * memory; synchronous).
+ *   cpk_encode_messages_host: h_msg_seg_off[0] = 0, [nm] = nseg; h_out
+ *     capacity as cpk_encode_messages; h_out_off[nm + nseg + 1] written.
+ *   cpk_decode_messages_host: h_msg_seg_off[nm+1], h_msg_status[nm],
+ *     h_seg_word_off[segments+1] (segment words in h_out) and h_totals[2]
+ *     written; CPK_ENOMEM (with the totals) if out_cap_words / seg_cap are
+ *     too small -- call with 0 / NULL first to size them; otherwise returns
+ *     the first failed message's status or CPK_OK. */
+int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_seg_word_off,
+                             uint32_t nseg, const uint64_t *h_msg_seg_off, uint32_t nm,
+                             void *h_out, uint64_t h_out_cap, uint64_t *h_out_off);
+int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_msg_off,
+                             uint32_t nm, uint64_t traversal_limit_words, void *h_out,
+                             uint64_t out_cap_words, uint64_t *h_seg_word_off, uint32_t seg_cap,
+                             uint64_t *h_msg_seg_off, int32_t *h_msg_status, uint64_t *h_totals);
+
 /* ---- benchmark support (synthetic device-resident workloads) ---- */
 
 /* Device generator of the synthetic segments described in SURVEY.md 8d:

@@ -549,3 +549,29 @@ def test_encode_messages_matches_serialize_write(ctx, oracle):
     assert S2 == sum(len(m) for m, g in zip(msgs, ok) if g)
     got = d_out.cpu().numpy().view(np.uint8)[: 8 * W].tobytes()
     assert got == b"".join(s for m, g in zip(msgs, ok) if g for s in m)
+
+
+def test_message_host_forms(ctx, oracle):
+    """cpk_encode_messages_host / cpk_decode_messages_host: the JNI facade's
+    SerializePacked batch path, against the oracle's Serialize.write/read."""
+    import capnp_packed as cp
+    rng = np.random.default_rng(43)
+    msgs = [[_random_words(rng, int(rng.choice([0, 1, 9, 500, 4000])), [.4, .3, .2, .1]).tobytes()
+             for _ in range(int(rng.integers(1, 6)))] for _ in range(60)]
+    pk, off = ctx.encode_messages_host(msgs)
+    assert pk == b"".join(oracle.write_message(m) for m in msgs)
+    mso = np.concatenate([[0], np.cumsum([len(m) for m in msgs])])
+    moff = off[(mso[:-1] + np.arange(len(msgs))).astype(np.int64)]
+    moff = np.append(moff, off[-1])
+    st, got = ctx.decode_messages_host(pk, moff)
+    assert (st == 0).all() and got == msgs
+    # a broken message in the middle: its status, the others intact
+    bad = bytearray(pk)
+    j = int(moff[7])
+    bad[j: j + 1] = b"\x0f"  # first tag of message 7's table: 4 bytes follow
+    st, got = ctx.decode_messages_host(bytes(bad), moff)
+    ost, _, used = oracle.read_message(bytes(bad[j: int(moff[8])]))
+    if ost == oracle.OK and used != int(moff[8]) - j:
+        ost = oracle.ETRAILING
+    assert st[7] == ost and ost != oracle.OK
+    assert all(st[i] == 0 and got[i] == msgs[i] for i in range(len(msgs)) if i != 7)
