@@ -57,6 +57,24 @@ def test_negative_segment_size(oracle, ov):
     assert st == oracle.EFRAME
 
 
+def test_segment_over_max_words(oracle):
+    """A size over MAX_SEGMENT_WORDS (2^28 - 1) passes the traversal check
+    when the limit is raised, then makeByteBufferForWords throws when that
+    segment is allocated (Serialize.java:45-53, :165-175); an earlier
+    segment is still read first."""
+    import struct
+    table = struct.pack("<Iii", 1, 1, 1 << 28) + b"\0" * 4
+    stream = oracle.pack(table) + oracle.pack(b"\1" * 8)
+    st, _, _ = oracle.read_message(stream, traversal_limit_words=1 << 30, out_cap=1 << 12)
+    assert st == oracle.EINVAL  # (the oracle's own output bound is checked first)
+    st, _, _ = oracle.read_message(stream, traversal_limit_words=1 << 30, out_cap=(1 << 31) + 64)
+    assert st == oracle.EFRAME
+    table = struct.pack("<Iii", 1, 1, (1 << 28) - 1) + b"\0" * 4
+    st, _, _ = oracle.read_message(oracle.pack(table) + oracle.pack(b"\1" * 8),
+                                   traversal_limit_words=1 << 30, out_cap=(1 << 31) + 64)
+    assert st == oracle.ETRUNC  # allowed size, data missing
+
+
 def test_misaligned_read(oracle):
     st, _, _ = oracle.unpack(b"\x00\x00", 7)
     assert st == oracle.EINVAL
