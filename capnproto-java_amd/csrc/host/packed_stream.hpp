@@ -31,7 +31,8 @@ struct IOException : std::runtime_error {
 inline void check(int st, const char *what) {
   if (st == CPK_OK) return;
   std::string m = std::string(what) + ": " + cpk_status_string(st);
-  if (st == CPK_ETRUNC || st == CPK_EOVERRUN || st == CPK_ETRAILING || st == CPK_EINVAL)
+  if (st == CPK_ETRUNC || st == CPK_EOVERRUN || st == CPK_ETRAILING || st == CPK_EINVAL ||
+      st == CPK_EFRAME)
     throw DecodeException(m);
   throw IOException(m);
 }
@@ -182,6 +183,8 @@ struct SerializePacked {
       }
     }
     if (total > traversal_limit_words) throw DecodeException("Message size exceeds traversal limit.");
+    for (auto s : sizes)  // makeByteBufferForWords (Serialize.java:45-53)
+      if (s > (1u << 28) - 1) throw DecodeException("segment has too many words");
     // all segments in one stream-decode call (pieces back to back)
     std::vector<uint64_t> swo = {0};
     for (auto s : sizes) swo.push_back(swo.back() + s);
@@ -199,6 +202,68 @@ struct SerializePacked {
     for (uint32_t i = 0; i < count; ++i)
       segs.emplace_back(out.begin() + 8 * swo[i], out.begin() + 8 * swo[i + 1]);
     return segs;
+  }
+
+  using Message = std::vector<std::vector<uint8_t>>;  // its segments
+
+  // write() for each message, ONE GPU call: the segment tables are built and
+  // packed on the device (cpk_encode_messages_host).  Returns the packed
+  // bytes, messages back to back; msg_off[m] = message m's first byte.
+  static std::vector<uint8_t> writeMessages(Gpu &gpu, const std::vector<Message> &msgs,
+                                            std::vector<uint64_t> *msg_off = nullptr) {
+    std::vector<uint8_t> words;
+    std::vector<uint64_t> swo = {0}, mso = {0};
+    uint64_t cap = 16;
+    for (auto &m : msgs) {
+      for (auto &sg : m) {
+        if (sg.size() % 8) throw std::invalid_argument("segment not word-aligned");
+        words.insert(words.end(), sg.begin(), sg.end());
+        swo.push_back(words.size() / 8);
+        cap += cpk_packed_bound(sg.size() / 8);
+      }
+      mso.push_back(swo.size() - 1);
+      cap += 10 * ((m.size() + 2) / 2 + 1);
+    }
+    const uint32_t nseg = (uint32_t)swo.size() - 1, nm = (uint32_t)msgs.size();
+    words.resize(words.size() + 8);
+    std::vector<uint8_t> out(cap);
+    std::vector<uint64_t> off(nm + nseg + 1);
+    check(cpk_encode_messages_host(gpu.get(), words.data(), swo.data(), nseg, mso.data(), nm,
+                                   out.data(), out.size(), off.data()),
+          "SerializePacked.writeMessages");
+    out.resize(off[nm + nseg]);
+    if (msg_off) {
+      msg_off->clear();
+      for (uint32_t m = 0; m < nm; ++m) msg_off->push_back(off[mso[m] + m]);
+      msg_off->push_back(off[nm + nseg]);
+    }
+    return out;
+  }
+
+  // read() for each message, ONE GPU pass: message m is
+  // packed[msg_off[m], msg_off[m+1]); tables read and validated on the
+  // device (cpk_decode_messages_host).  Throws the first bad message's error.
+  static std::vector<Message> readMessages(Gpu &gpu, const std::vector<uint8_t> &packed,
+                                           const std::vector<uint64_t> &msg_off,
+                                           uint64_t traversal_limit_words = 8ull << 20) {
+    const uint32_t nm = (uint32_t)msg_off.size() - 1;
+    std::vector<uint64_t> mso(nm + 1), tot(2);
+    std::vector<int32_t> mst(nm ? nm : 1);
+    int rc = cpk_decode_messages_host(gpu.get(), packed.data(), msg_off.data(), nm,
+                                      traversal_limit_words, nullptr, 0, nullptr, 0, mso.data(),
+                                      mst.data(), tot.data());
+    std::vector<uint8_t> out(8 * tot[0] + 8);
+    std::vector<uint64_t> swo(tot[1] + 1);
+    if (rc == CPK_ENOMEM)
+      rc = cpk_decode_messages_host(gpu.get(), packed.data(), msg_off.data(), nm,
+                                    traversal_limit_words, out.data(), tot[0], swo.data(),
+                                    (uint32_t)tot[1], mso.data(), mst.data(), tot.data());
+    check(rc, "SerializePacked.readMessages");
+    std::vector<Message> res(nm);
+    for (uint32_t m = 0; m < nm; ++m)
+      for (uint64_t j = mso[m]; j < mso[m + 1]; ++j)
+        res[m].emplace_back(out.begin() + 8 * swo[j], out.begin() + 8 * swo[j + 1]);
+    return res;
   }
 };
 

@@ -2223,6 +2223,7 @@ const char *cpk_status_string(int s) {
     case CPK_ETRUNC: return "premature end of packed input";
     case CPK_EOVERRUN: return "packed run past the end of the piece";
     case CPK_ETRAILING: return "piece filled before the end of its packed bytes";
+    case CPK_EFRAME: return "invalid segment table";
     case CPK_ENOMEM: return "out of device memory";
     case CPK_EDEVICE: return "HIP runtime error";
     case CPK_EUNSUPPORTED: return "piece not supported by this build";

@@ -117,6 +117,43 @@ int main() {
     EXPECT(got == segs, "segments round trip");
     EXPECT(in.remaining() == 0, "stream consumed");
   }
+  // many messages in one GPU pass each way (cpk_encode_messages_host /
+  // cpk_decode_messages_host) == one write()/read() per message
+  {
+    std::vector<SerializePacked::Message> msgs;
+    for (int m = 0; m < 40; ++m) {
+      SerializePacked::Message msg;
+      for (int i = 0; i <= m % 5; ++i) {
+        Bytes sg;
+        for (int w = 0; w < (m * 7 + i * 13) % 90; ++w) {
+          Bytes word = {(uint8_t)(w * m), 0, (uint8_t)i, 0, 0, 0, (uint8_t)(w & 3 ? 0 : 9), 0};
+          sg.insert(sg.end(), word.begin(), word.end());
+        }
+        msg.push_back(sg);
+      }
+      msgs.push_back(msg);
+    }
+    std::vector<uint64_t> moff;
+    Bytes all = SerializePacked::writeMessages(gpu, msgs, &moff);
+    Bytes one;
+    for (auto &m : msgs) {
+      Bytes b = SerializePacked::write(gpu, m);
+      one.insert(one.end(), b.begin(), b.end());
+    }
+    EXPECT(all == one, "writeMessages == write per message");
+    EXPECT(SerializePacked::readMessages(gpu, all, moff) == msgs, "readMessages round trip");
+    bool threw = false;
+    try {
+      Bytes bad = all;
+      bad.resize(moff[3] + 5);  // message 3 truncated
+      std::vector<uint64_t> mo(moff.begin(), moff.begin() + 4);
+      mo.push_back(bad.size());
+      SerializePacked::readMessages(gpu, bad, mo);
+    } catch (const DecodeException &) {
+      threw = true;
+    }
+    EXPECT(threw, "truncated message must throw DecodeException");
+  }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
     return 1;
