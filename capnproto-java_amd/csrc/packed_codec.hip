@@ -1356,6 +1356,9 @@ __global__ __launch_bounds__(kPlanThreads) void tile_plan_kernel(
 //      gather-expand the blocks (PackedInputStream.java:82-134 per word).
 // No barriers: up to 32 pieces in flight per CU.
 constexpr int kDecThreads = 256;               // 4 independent waves
+#ifndef CPK_DEC_WPE
+#define CPK_DEC_WPE 8  // workgroups per CU the register budget is sized for
+#endif
 #ifndef CPK_DEC_CHUNK
 #define CPK_DEC_CHUNK 48
 #endif
@@ -1456,7 +1459,7 @@ struct DecStreams {
   uint64_t *send_out;
 };
 template <bool kStream>
-__global__ __launch_bounds__(kDecThreads, 8) void decode_kernel(
+__global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
     const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
     int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail, DecStreams sd) {
