@@ -174,3 +174,38 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDecodeMessages(
   (*env)->ReleaseLongArrayElements(env, totals, tot, 0);
   if (st != CPK_OK && !(out == NULL && st == CPK_ENOMEM)) throw_status(env, st);
 }
+
+/* long PackedGpu.nativeDecodeStream(long h, ByteBuffer packed, long[] segWordOff,
+ *                                   ByteBuffer out)
+ * read() calls back to back on one packed stream (PackedInputStream.java:
+ * 35-140, as fillBuffer issues them, Serialize.java:74-83): piece i fills
+ * words [segWordOff[i], segWordOff[i+1]) of `out`, each consuming only the
+ * bytes it needs.  The stream is packed[position, limit) (direct).  Returns
+ * the bytes consumed; throws the first failed piece's error. */
+JNIEXPORT jlong JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDecodeStream(
+    JNIEnv *env, jclass k, jlong h, jobject packed, jint position, jint limit,
+    jlongArray segWordOff, jobject out) {
+  (void)k;
+  uint8_t *ppk = (uint8_t *)(*env)->GetDirectBufferAddress(env, packed);
+  void *pout = (*env)->GetDirectBufferAddress(env, out);
+  if (!ppk || !pout || position < 0 || limit < position) {
+    throw_status(env, CPK_EINVAL);
+    return 0;
+  }
+  jsize n1 = (*env)->GetArrayLength(env, segWordOff);
+  uint32_t n = (uint32_t)(n1 > 1 ? n1 - 1 : 0);
+  jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
+  uint64_t *in_off = (uint64_t *)calloc((size_t)n + 1, sizeof(uint64_t));
+  int32_t *status = (int32_t *)calloc((size_t)(n ? n : 1), sizeof(int32_t));
+  int st = (in_off && status)
+               ? cpk_decode_stream_host((cpk_ctx)(intptr_t)h, ppk + position,
+                                        (uint64_t)(limit - position), (const uint64_t *)swo, n,
+                                        pout, in_off, status)
+               : CPK_ENOMEM;
+  jlong used = (st == CPK_OK) ? (jlong)in_off[n] : 0;
+  free(in_off);
+  free(status);
+  (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
+  if (st != CPK_OK) throw_status(env, st);
+  return used;
+}

@@ -31,6 +31,8 @@ public final class PackedGpu implements AutoCloseable {
                                                     long traversalLimit, ByteBuffer out,
                                                     long[] segWordOff, long[] msgSegOff,
                                                     long[] totals);
+    private static native long nativeDecodeStream(long handle, ByteBuffer packed, int position,
+                                                  int limit, long[] segWordOff, ByteBuffer out);
 
     private long handle;
 
@@ -162,4 +164,78 @@ public final class PackedGpu implements AutoCloseable {
             outs[i].put(slice);
         }
     }
+    /** read() calls back to back on one packed stream, as fillBuffer issues
+     *  them (Serialize.java:74-83 over PackedInputStream.read,
+     *  PackedInputStream.java:35-140): outs[i] is filled to its limit from
+     *  packed[position, limit), each read consuming only the bytes it needs.
+     *  packed.position advances by the bytes consumed (as the reference's
+     *  BufferedInputStream does).
+     *  @throws org.capnproto.DecodeException on malformed input */
+    public void decodeStream(ByteBuffer packed, ByteBuffer[] outs) throws IOException {
+        int n = outs.length;
+        long[] swo = new long[n + 1];
+        long words = 0;
+        for (int i = 0; i < n; ++i) {
+            int len = outs[i].remaining();
+            if (len % 8 != 0)
+                throw new org.capnproto.DecodeException("PackedInputStream reads must be word-aligned");
+            swo[i] = words;
+            words += len / 8;
+        }
+        swo[n] = words;
+        ByteBuffer pk = packed.isDirect() ? packed
+                : (ByteBuffer) ByteBuffer.allocateDirect(packed.remaining()).put(packed.duplicate()).flip();
+        ByteBuffer out = ByteBuffer.allocateDirect((int) (words * 8 + 8));
+        long used = nativeDecodeStream(handle, pk, pk.position(), pk.limit(), swo, out);
+        packed.position(packed.position() + (int) used);
+        for (int i = 0; i < n; ++i) {
+            ByteBuffer slice = out.duplicate();
+            slice.position((int) (swo[i] * 8)).limit((int) (swo[i + 1] * 8));
+            outs[i].put(slice);
+        }
+    }
+
+    /** SerializePacked.read of one message from the front of `packed`
+     *  (Serialize.java:119-178 over PackedInputStream): the first word, then
+     *  4 * (count & ~1) bytes of sizes, then every segment in one stream
+     *  decode; the same checks and messages as doRead.  packed.position
+     *  advances past the message.  Returns the segments (little-endian). */
+    public ByteBuffer[] readMessage(ByteBuffer packed, long traversalLimitInWords) throws IOException {
+        ByteBuffer first = ByteBuffer.allocate(8).order(ByteOrder.LITTLE_ENDIAN);
+        decodeStream(packed, new ByteBuffer[] {first});
+        int rawCount = first.getInt(0);
+        if (rawCount < 0 || rawCount > 511)
+            throw new org.capnproto.DecodeException("segment count must be between 0 and 512");
+        int count = 1 + rawCount;
+        int[] sizes = new int[count];
+        sizes[0] = first.getInt(4);
+        if (sizes[0] < 0)
+            throw new org.capnproto.DecodeException("segment 0 has more than 2^31 words, which is unsupported");
+        long total = sizes[0];
+        if (count > 1) {
+            ByteBuffer more = ByteBuffer.allocate(4 * (count & ~1)).order(ByteOrder.LITTLE_ENDIAN);
+            decodeStream(packed, new ByteBuffer[] {more});
+            for (int i = 0; i < count - 1; ++i) {
+                sizes[i + 1] = more.getInt(i * 4);
+                if (sizes[i + 1] < 0)
+                    throw new org.capnproto.DecodeException("segment " + (i + 1) +
+                                                            " has more than 2^31 words, which is unsupported");
+                total += sizes[i + 1];
+            }
+        }
+        if (total > traversalLimitInWords)
+            throw new org.capnproto.DecodeException("Message size exceeds traversal limit.");
+        ByteBuffer[] segs = new ByteBuffer[count];
+        for (int i = 0; i < count; ++i) {
+            if (sizes[i] > MAX_SEGMENT_WORDS)   // Serialize.makeByteBufferForWords, Serialize.java:45-53
+                throw new org.capnproto.DecodeException("segment has too many words (" + sizes[i] + ")");
+            segs[i] = ByteBuffer.allocate(8 * sizes[i]).order(ByteOrder.LITTLE_ENDIAN);
+        }
+        decodeStream(packed, segs);
+        for (ByteBuffer s : segs) s.rewind();
+        return segs;
+    }
+
+    /** Serialize.java:45 (largest segment makeByteBufferForWords accepts). */
+    public static final int MAX_SEGMENT_WORDS = (1 << 28) - 1;
 }
