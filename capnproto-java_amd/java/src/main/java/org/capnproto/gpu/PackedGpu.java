@@ -225,14 +225,25 @@ public final class PackedGpu implements AutoCloseable {
         }
         if (total > traversalLimitInWords)
             throw new org.capnproto.DecodeException("Message size exceeds traversal limit.");
-        ByteBuffer[] segs = new ByteBuffer[count];
+        // All segments land in ONE direct buffer (zero-copy for JNI, SURVEY.md
+        // §8f row 4) that the returned slices share; one stream decode.
+        long[] swo = new long[count + 1];
         for (int i = 0; i < count; ++i) {
             if (sizes[i] > MAX_SEGMENT_WORDS)   // Serialize.makeByteBufferForWords, Serialize.java:45-53
                 throw new org.capnproto.DecodeException("segment has too many words (" + sizes[i] + ")");
-            segs[i] = ByteBuffer.allocate(8 * sizes[i]).order(ByteOrder.LITTLE_ENDIAN);
+            swo[i + 1] = swo[i] + sizes[i];
         }
-        decodeStream(packed, segs);
-        for (ByteBuffer s : segs) s.rewind();
+        ByteBuffer out = ByteBuffer.allocateDirect((int) (swo[count] * 8 + 8)).order(ByteOrder.LITTLE_ENDIAN);
+        ByteBuffer pk = packed.isDirect() ? packed
+                : (ByteBuffer) ByteBuffer.allocateDirect(packed.remaining()).put(packed.duplicate()).flip();
+        long used = nativeDecodeStream(handle, pk, pk.position(), pk.limit(), swo, out);
+        packed.position(packed.position() + (int) used);
+        ByteBuffer[] segs = new ByteBuffer[count];
+        for (int i = 0; i < count; ++i) {
+            ByteBuffer seg = out.duplicate();
+            seg.position((int) (swo[i] * 8)).limit((int) (swo[i + 1] * 8));
+            segs[i] = seg.slice().order(ByteOrder.LITTLE_ENDIAN);
+        }
         return segs;
     }
 
