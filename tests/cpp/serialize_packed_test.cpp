@@ -154,6 +154,34 @@ int main() {
     }
     EXPECT(threw, "truncated message must throw DecodeException");
   }
+  // The benchmark harness's "bytes" mode with GPU_PACKED (TestCase.java:
+  // 78-120, GpuPacked.java): messages read one at a time from a reused scratch
+  // buffer that still holds stale bytes past the current message; each read
+  // consumes exactly its message's packed bytes.
+  {
+    std::vector<std::vector<Bytes>> msgs;
+    Bytes scratch;
+    for (int m = 0; m < 6; ++m) {
+      std::vector<Bytes> segs;
+      for (int i = 0; i <= m % 3; ++i) {
+        Bytes sg;
+        for (int w = 0; w < 3 + 17 * m + 5 * i; ++w) {
+          Bytes word = {(uint8_t)(w + m), (uint8_t)(w & 1 ? 0 : 7), 0, (uint8_t)i, 1, 2, 3, (uint8_t)m};
+          if (w % 5 == 0) word = Bytes(8, 0);
+          sg.insert(sg.end(), word.begin(), word.end());
+        }
+        segs.push_back(sg);
+      }
+      Bytes b = SerializePacked::write(gpu, segs);
+      scratch.insert(scratch.end(), b.begin(), b.end());
+      msgs.push_back(segs);
+    }
+    const size_t used = scratch.size();
+    for (int g = 0; g < 300; ++g) scratch.push_back((uint8_t)(g * 37 + 11));  // stale bytes
+    ArrayInputStream in(scratch.data(), scratch.size());
+    for (auto &segs : msgs) EXPECT(SerializePacked::read(gpu, in) == segs, "message from scratch");
+    EXPECT(in.remaining() == scratch.size() - used, "stale bytes left unread");
+  }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
     return 1;
