@@ -27,6 +27,9 @@ static_assert(kE4RingBytes == kE3RingBytes, "the v3 ring helpers are reused");
 #ifndef CPK_E4_WPE
 #define CPK_E4_WPE 8
 #endif
+#ifndef CPK_E4_PF
+#define CPK_E4_PF 4  // steps of loads in flight ahead of the size pass's classification
+#endif
 
 // Run state entering a step (wave-uniform): g 0 zero run, 1 D/L stretch,
 // 2 none (piece start or after an M word); len: words of the run before the
@@ -186,36 +189,34 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     // (32-bit step / word indices: a piece is at most 2^31 words, Serialize
     // limits segments to 2^29 - 1, Serialize.java:45-53)
     const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;
-    // software pipeline: the next four steps' loads are in flight while
-    // these four are classified
-    uint64_t v[4], vn[4];
+    // software pipeline: the next CPK_E4_PF steps' loads are in flight while
+    // these are classified
+    constexpr int PF = CPK_E4_PF;
+    uint64_t v[PF], vn[PF];
     // loads clamped to the piece's last word, not predicated (no exec-mask
     // branches around them); words past the end are masked by `valid`
     const uint32_t kl = W32 - 1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = src[min(((uint32_t)j << 6) + lane, kl)];
-    for (uint32_t s0 = 0; s0 < nsteps; s0 += 4) {
+    for (int j = 0; j < PF; ++j) v[j] = src[min(((uint32_t)j << 6) + lane, kl)];
+    for (uint32_t s0 = 0; s0 < nsteps; s0 += PF) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) vn[j] = src[min(((s0 + 4 + j) << 6) + lane, kl)];
-      uint64_t bvg[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+      for (int j = 0; j < PF; ++j) vn[j] = src[min(((s0 + PF + j) << 6) + lane, kl)];
+      uint64_t x = ~0ull;  // lane j keeps step s0 + j's boundary row
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < PF; ++j) {
         const uint32_t k = ((s0 + j) << 6) + lane;
         const bool valid = k < W32;
         if (s0 + j < nsteps) {
           const E4Cls c = e4_classify(v[j], valid, gl);
           const E4Role r = e4_roles(e3_tag(v[j]), valid, c, st, lane, lem);
           acc += r.nb;
-          bvg[j] = c.BV;
+          x = lane == j ? c.BV : x;
         }
       }
-      // the group's boundary rows for the emit pass: lanes 0-3, one store
-      {
-        const uint64_t x = lane == 0 ? bvg[0] : lane == 1 ? bvg[1] : lane == 2 ? bvg[2] : bvg[3];
-        if (lane < 4 && s0 + lane < nsteps && s0 + lane < rows) bvp[s0 + lane] = x;
-      }
+      // the group's boundary rows for the emit pass: lanes 0..PF-1, one store
+      if (lane < PF && s0 + lane < nsteps && s0 + lane < rows) bvp[s0 + lane] = x;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = vn[j];
+      for (int j = 0; j < PF; ++j) v[j] = vn[j];
     }
     // wave sum in two 16-bit halves (a piece's packed size may pass 2^31)
     const uint32_t thi = (uint32_t)wave_incl_add((int)(acc >> 16));
