@@ -32,7 +32,7 @@ EXPORTS = [
     "cpk_decode_batch", "cpk_decode_stream", "cpk_encode_host", "cpk_decode_host",
     "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch", "cpk_ctx_take_error",
     "cpk_decode_messages", "cpk_encode_messages", "cpk_encode_messages_host",
-    "cpk_decode_messages_host",
+    "cpk_decode_messages_host", "cpk_encode_host_gather",
 ]
 
 
@@ -79,6 +79,7 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_encode_batch": ([vp, vp, vp, u32, u64, vp, vp, vp], i32),
         "cpk_decode_batch": ([vp, vp, vp, vp, u32, vp, vp, vp], i32),
         "cpk_encode_host": ([vp, vp, vp, u32, vp, u64, vp], i32),
+        "cpk_encode_host_gather": ([vp, vp, vp, u32, vp, u64, vp], i32),
         "cpk_decode_host": ([vp, vp, vp, vp, u32, vp, vp], i32),
         "cpk_decode_stream": ([vp, vp, u64, vp, u32, vp, vp, vp, vp], i32),
         "cpk_decode_stream_host": ([vp, vp, u64, vp, u32, vp, vp, vp], i32),
@@ -231,6 +232,22 @@ class Context:
         rc = self._lib.cpk_encode_host(self.handle, data.ctypes.data if data.size else None,
                                        swo.ctypes.data, n, out.ctypes.data, cap, off.ctypes.data)
         _check(rc, "cpk_encode_host")
+        return out[: int(off[-1])], off
+
+    def encode_host_gather(self, pieces):
+        """Gather form: `pieces` = list of uint64 word arrays, one per piece,
+        each left where it lies (no concatenation).  -> (packed uint8, out_off)."""
+        pieces = [np.ascontiguousarray(x, dtype=np.uint64) for x in pieces]
+        n = len(pieces)
+        swo = np.zeros(n + 1, dtype=np.uint64)
+        swo[1:] = np.cumsum([x.size for x in pieces])
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[x.ctypes.data if x.size else None for x in pieces])
+        cap = batch_capacity(swo)
+        out = np.zeros(cap, dtype=np.uint8)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        rc = self._lib.cpk_encode_host_gather(self.handle, ptrs, swo.ctypes.data, n,
+                                              out.ctypes.data, cap, off.ctypes.data)
+        _check(rc, "cpk_encode_host_gather")
         return out[: int(off[-1])], off
 
     def decode_host(self, packed: np.ndarray, in_off: np.ndarray, seg_word_off: np.ndarray,

@@ -189,10 +189,43 @@ void pipe_drain(HostPipe *p) {
 
 extern "C" {
 
-int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32_t n,
-                    void *h_out, uint64_t h_out_cap, uint64_t *h_out_off) {
-  if (!ctx || !h_swo || !h_out_off || (n && ((!h_in && h_swo[n] > h_swo[0]) || !h_out)))
-    return CPK_EINVAL;
+}  // extern "C"
+
+namespace {
+
+// piece j of the chunk is 8 * (swo[j+1] - swo[j]) bytes at pieces[j]; they go
+// back to back into `dst` (pinned staging), split over host threads by bytes
+void gather_copy(uint8_t *dst, const void *const *pieces, const uint64_t *swo, uint32_t i0,
+                 uint32_t i1) {
+  const uint64_t bytes = 8 * (swo[i1] - swo[i0]);
+  const int T = host_threads();
+  auto run = [=](uint32_t a, uint32_t b) {
+    for (uint32_t j = a; j < b; ++j)
+      if (swo[j + 1] > swo[j])
+        memcpy(dst + 8 * (swo[j] - swo[i0]), pieces[j], 8 * (swo[j + 1] - swo[j]));
+  };
+  if (T <= 1 || bytes < (4u << 20)) {
+    run(i0, i1);
+    return;
+  }
+  std::vector<std::thread> ts;
+  uint32_t a = i0;
+  for (int t = 1; t <= T && a < i1; ++t) {
+    const uint64_t goal = swo[i0] + (swo[i1] - swo[i0]) * t / T;
+    uint32_t b = a;
+    while (b < i1 && (swo[b] < goal || b == a)) ++b;
+    if (t == T) b = i1;
+    ts.emplace_back(run, a, b);
+    a = b;
+  }
+  for (auto &t : ts) t.join();
+}
+
+// cpk_encode_host / cpk_encode_host_gather: `copy_in` fills a chunk's pinned
+// input slot
+template <class CopyIn>
+int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_t n, void *h_out,
+                     uint64_t h_out_cap, uint64_t *h_out_off) {
   if (n == 0) {
     h_out_off[0] = 0;
     return CPK_OK;
@@ -210,7 +243,6 @@ int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32
   HostPipe *p = nullptr;
   int rc = pipe_get(ctx, mi, mo, 2 * (mm + 1), &p);
   if (rc) return rc;
-  const uint8_t *src = (const uint8_t *)h_in;
   uint8_t *dst = (uint8_t *)h_out;
   uint64_t base = 0;          // output bytes so far
   const size_t K = cs.size();
@@ -219,7 +251,7 @@ int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32
       const HostChunk &c = cs[k];
       HostSlot &s = p->slot[k & 1];
       const uint32_t nk = c.i1 - c.i0;
-      par_copy(s.pin_in, src + c.in0, c.in_len);
+      copy_in((uint8_t *)s.pin_in, c);
       for (uint32_t j = 0; j <= nk; ++j) s.pin_meta[j] = h_swo[c.i0 + j] - h_swo[c.i0];
       if ((c.in_len && hipMemcpyAsync(s.d_in, s.pin_in, c.in_len, hipMemcpyHostToDevice, p->sh)) ||
           hipMemcpyAsync(s.d_meta, s.pin_meta, (nk + 1) * 8ull, hipMemcpyHostToDevice, p->sh) ||
@@ -281,6 +313,31 @@ int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32
   }
   // (a piece over its hint cannot occur: each chunk's hint is its largest piece)
   return cpk_ctx_take_error(ctx, p->sk);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32_t n,
+                    void *h_out, uint64_t h_out_cap, uint64_t *h_out_off) {
+  if (!ctx || !h_swo || !h_out_off || (n && ((!h_in && h_swo[n] > h_swo[0]) || !h_out)))
+    return CPK_EINVAL;
+  const uint8_t *src = (const uint8_t *)h_in;
+  return encode_host_impl(
+      ctx, [&](uint8_t *pin, const HostChunk &c) { par_copy(pin, src + c.in0, c.in_len); }, h_swo,
+      n, h_out, h_out_cap, h_out_off);
+}
+
+int cpk_encode_host_gather(cpk_ctx ctx, const void *const *h_pieces, const uint64_t *h_swo,
+                           uint32_t n, void *h_out, uint64_t h_out_cap, uint64_t *h_out_off) {
+  if (!ctx || !h_swo || !h_out_off || (n && (!h_pieces || !h_out))) return CPK_EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (h_swo[i + 1] > h_swo[i] && !h_pieces[i]) return CPK_EINVAL;
+  return encode_host_impl(
+      ctx,
+      [&](uint8_t *pin, const HostChunk &c) { gather_copy(pin, h_pieces, h_swo, c.i0, c.i1); },
+      h_swo, n, h_out, h_out_cap, h_out_off);
 }
 
 int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,

@@ -194,6 +194,13 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
  *   cpk_decode_host: h_status[n] written; returns CPK_OK iff all pieces OK. */
 int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_seg_word_off,
                     uint32_t n, void *h_out, uint64_t h_out_cap, uint64_t *h_out_off);
+/* Gather form of cpk_encode_host (builder segments in
+ * their own direct ByteBuffers, DefaultAllocator.java:56-62, packed without a
+ * host-side concatenation): piece i is the h_swo[i+1] - h_swo[i] words at
+ * h_pieces[i] (any 8-byte-aligned host pointer; NULL only for an empty
+ * piece); h_swo is read only for the sizes.  Output as cpk_encode_host. */
+int cpk_encode_host_gather(cpk_ctx ctx, const void *const *h_pieces, const uint64_t *h_swo,
+                           uint32_t n, void *h_out, uint64_t h_out_cap, uint64_t *h_out_off);
 int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
                     const uint64_t *h_seg_word_off, uint32_t n, void *h_out,
                     int32_t *h_status);

@@ -408,6 +408,23 @@ def test_host_forms_pipelined_chunks(ctx, oracle, chunk_kb, monkeypatch):
         assert st[i] == ost, (i, st[i], ost)
 
 
+@pytest.mark.parametrize("chunk_kb", ["1", "64"])
+def test_encode_host_gather_matches_contiguous(ctx, oracle, chunk_kb, monkeypatch):
+    """cpk_encode_host_gather (pieces left in their own host buffers, SURVEY.md
+    §8f row 4) writes the bytes and offsets of cpk_encode_host over the
+    concatenation, and those are the oracle's."""
+    monkeypatch.setenv("CPK_HOST_CHUNK_KB", chunk_kb)
+    rng = np.random.default_rng(77 + int(chunk_kb))
+    sizes = [0, 5, 3000, 0, 1] + list(rng.integers(0, 4000, size=80)) + [30000, 0]
+    parts = [_random_words(rng, int(s), [.4, .3, .2, .1]) for s in sizes]
+    got, goff = ctx.encode_host_gather([p.view(np.uint64) for p in parts])
+    ref, roff = ctx.encode_host(np.concatenate(parts), _swo(sizes))
+    assert np.array_equal(goff, roff)
+    assert got.tobytes() == ref.tobytes()
+    for i in (0, 1, 2, 7, len(parts) - 2):
+        assert got[int(goff[i]):int(goff[i + 1])].tobytes() == oracle.pack(parts[i].tobytes())
+
+
 def _message_cases(oracle, rng, limit):
     """Packed messages (SerializePacked.write) and broken ones: truncated,
     trailing bytes, flipped table bytes, segment count over 512, negative
