@@ -209,3 +209,46 @@ JNIEXPORT jlong JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDecodeStream(
   if (st != CPK_OK) throw_status(env, st);
   return used;
 }
+
+/* void PackedGpu.nativeEncodeGather(long h, ByteBuffer[] pieces, int[] positions,
+ *                                   long[] segWordOff, ByteBuffer out, long[] outOff)
+ * Zero-copy encode of direct buffers where they lie (SURVEY.md §8f row 4;
+ * builder segments allocated DIRECT, DefaultAllocator.java:56-62): piece i is
+ * pieces[i][positions[i], +8*(segWordOff[i+1]-segWordOff[i])) ->
+ * cpk_encode_host_gather.  Same bytes as nativeEncode over the concatenation. */
+JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeGather(
+    JNIEnv *env, jclass k, jlong h, jobjectArray pieces, jintArray positions,
+    jlongArray segWordOff, jobject out, jlongArray outOff) {
+  (void)k;
+  void *pout = (*env)->GetDirectBufferAddress(env, out);
+  jlong cap = (*env)->GetDirectBufferCapacity(env, out);
+  jsize n = (*env)->GetArrayLength(env, pieces);
+  if (!pout || (*env)->GetArrayLength(env, segWordOff) != n + 1) {
+    throw_status(env, CPK_EINVAL);
+    return;
+  }
+  const void **ptrs = (const void **)calloc((size_t)(n ? n : 1), sizeof(void *));
+  if (!ptrs) {
+    throw_status(env, CPK_ENOMEM);
+    return;
+  }
+  jint *pos = (*env)->GetIntArrayElements(env, positions, NULL);
+  int st = CPK_OK;
+  for (jsize i = 0; i < n && st == CPK_OK; ++i) {
+    jobject b = (*env)->GetObjectArrayElement(env, pieces, i);
+    uint8_t *a = (uint8_t *)(*env)->GetDirectBufferAddress(env, b);
+    if (!a) st = CPK_EINVAL;
+    else ptrs[i] = a + pos[i];
+    (*env)->DeleteLocalRef(env, b);
+  }
+  (*env)->ReleaseIntArrayElements(env, positions, pos, JNI_ABORT);
+  jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
+  jlong *off = (*env)->GetLongArrayElements(env, outOff, NULL);
+  if (st == CPK_OK)
+    st = cpk_encode_host_gather((cpk_ctx)(intptr_t)h, ptrs, (const uint64_t *)swo, (uint32_t)n,
+                                pout, (uint64_t)cap, (uint64_t *)off);
+  free(ptrs);
+  (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, outOff, off, st == CPK_OK ? 0 : JNI_ABORT);
+  if (st != CPK_OK) throw_status(env, st);
+}

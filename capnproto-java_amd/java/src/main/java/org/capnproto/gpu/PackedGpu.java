@@ -31,6 +31,8 @@ public final class PackedGpu implements AutoCloseable {
                                                     long traversalLimit, ByteBuffer out,
                                                     long[] segWordOff, long[] msgSegOff,
                                                     long[] totals);
+    private static native void nativeEncodeGather(long handle, ByteBuffer[] pieces, int[] positions,
+                                                  long[] segWordOff, ByteBuffer out, long[] outOff);
     private static native long nativeDecodeStream(long handle, ByteBuffer packed, int position,
                                                   int limit, long[] segWordOff, ByteBuffer out);
 
@@ -69,11 +71,19 @@ public final class PackedGpu implements AutoCloseable {
             words += len / 8;
         }
         swo[n] = words;
-        ByteBuffer in = ByteBuffer.allocateDirect((int) (words * 8)).order(ByteOrder.LITTLE_ENDIAN);
-        for (ByteBuffer p : pieces) in.put(p.duplicate());
         ByteBuffer out = ByteBuffer.allocateDirect((int) nativeCapacity(swo));
         long[] off = new long[n + 1];
-        nativeEncode(handle, in, swo, out, off);
+        boolean direct = true;
+        for (ByteBuffer p : pieces) direct &= p.isDirect();
+        if (direct) {  // builder segments allocated DIRECT: packed where they lie
+            int[] pos = new int[n];
+            for (int i = 0; i < n; ++i) pos[i] = pieces[i].position();
+            nativeEncodeGather(handle, pieces, pos, swo, out, off);
+        } else {
+            ByteBuffer in = ByteBuffer.allocateDirect((int) (words * 8)).order(ByteOrder.LITTLE_ENDIAN);
+            for (ByteBuffer p : pieces) in.put(p.duplicate());
+            nativeEncode(handle, in, swo, out, off);
+        }
         for (ByteBuffer p : pieces) p.position(p.limit());   // as write() leaves inBuf (:203)
         out.limit((int) off[n]);
         return new Packed(out, off);
