@@ -234,7 +234,7 @@ class Context:
         _check(rc, "cpk_encode_host")
         return out[: int(off[-1])], off
 
-    def encode_host_gather(self, pieces):
+    def encode_host_gather(self, pieces, out: np.ndarray = None):
         """Gather form: `pieces` = list of uint64 word arrays, one per piece,
         each left where it lies (no concatenation).  -> (packed uint8, out_off)."""
         pieces = [np.ascontiguousarray(x, dtype=np.uint64) for x in pieces]
@@ -243,7 +243,10 @@ class Context:
         swo[1:] = np.cumsum([x.size for x in pieces])
         ptrs = (ctypes.c_void_p * max(n, 1))(*[x.ctypes.data if x.size else None for x in pieces])
         cap = batch_capacity(swo)
-        out = np.zeros(cap, dtype=np.uint8)
+        if out is None:
+            out = np.zeros(cap, dtype=np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < cap:
+            raise ValueError("out: contiguous uint8, at least batch_capacity() bytes")
         off = np.zeros(n + 1, dtype=np.uint64)
         rc = self._lib.cpk_encode_host_gather(self.handle, ptrs, swo.ctypes.data, n,
                                               out.ctypes.data, cap, off.ctypes.data)

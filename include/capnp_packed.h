@@ -197,7 +197,7 @@ int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_seg_word_of
 /* Gather form of cpk_encode_host (builder segments in
  * their own direct ByteBuffers, DefaultAllocator.java:56-62, packed without a
  * host-side concatenation): piece i is the h_swo[i+1] - h_swo[i] words at
- * h_pieces[i] (any 8-byte-aligned host pointer; NULL only for an empty
+ * h_pieces[i] (any host pointer, no alignment needed; NULL only for an empty
  * piece); h_swo is read only for the sizes.  Output as cpk_encode_host. */
 int cpk_encode_host_gather(cpk_ctx ctx, const void *const *h_pieces, const uint64_t *h_swo,
                            uint32_t n, void *h_out, uint64_t h_out_cap, uint64_t *h_out_off);

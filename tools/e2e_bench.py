@@ -50,6 +50,20 @@ t_dec, (dec, st) = best(lambda: ctx.decode_host(pk, off, swo, out=db))
 assert np.array_equal(pk2, pk) and (st == 0).all() and np.array_equal(dec, host)
 print(f"  host forms, reused outputs: encode {U / GIB / t_enc:7.2f} GiB/s  decode {U / GIB / t_dec:7.2f} GiB/s"
       f"  round trip {U / GIB / (t_enc + t_dec):7.2f} GiB/s")
+# gather form: every piece in its own host allocation (builder segments)
+parts = [host[i * sw * 8:(i + 1) * sw * 8].view(np.uint64).copy() for i in range(n)]
+pk3, off3 = ctx.encode_host_gather(parts, out=ob)
+assert np.array_equal(pk3, pk) and np.array_equal(off3, off)
+# the C call alone (the Python wrapper's per-piece pointer list is not the
+# JNI path's cost)
+import ctypes  # noqa: E402
+ptrs = (ctypes.c_void_p * n)(*[x.ctypes.data for x in parts])
+off3 = np.zeros(n + 1, dtype=np.uint64)
+t_g, rc = best(lambda: ctx._lib.cpk_encode_host_gather(ctx.handle, ptrs, swo.ctypes.data, n,
+                                                        ob.ctypes.data, ob.size, off3.ctypes.data))
+assert rc == 0 and np.array_equal(off3, off)
+print(f"  gather encode (separate piece buffers), reused output: {U / GIB / t_g:7.2f} GiB/s")
+del parts
 # pinned copy rates (the PCIe bound of any pipelined host path)
 pin = torch.empty(U, dtype=torch.uint8).pin_memory()
 dev = torch.empty(U, dtype=torch.uint8, device="cuda")
