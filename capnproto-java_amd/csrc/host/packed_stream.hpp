@@ -130,28 +130,27 @@ class PackedInputStream {
 // ---- SerializePacked: a message = [segment table, seg0, ...] pieces -------
 struct SerializePacked {
   // Serialize.writeSegmentTable (Serialize.java:256-273) + one write per
-  // segment (:283-287), all pieces in ONE batched GPU call.
+  // segment (:283-287), all pieces in ONE batched GPU call; the segments are
+  // packed where they lie (cpk_encode_host_gather, no concatenation).
   static std::vector<uint8_t> write(Gpu &gpu, const std::vector<std::vector<uint8_t>> &segs) {
     const size_t n = segs.size();
-    std::vector<uint8_t> words;
     const size_t table_ints = (n + 2) & ~size_t(1);
-    words.resize(4 * table_ints, 0);
+    std::vector<uint8_t> table(4 * table_ints, 0);
     uint32_t v = (uint32_t)n - 1;
-    std::memcpy(words.data(), &v, 4);
+    std::memcpy(table.data(), &v, 4);
+    std::vector<const void *> pieces = {table.data()};
+    std::vector<uint64_t> swo = {0, table.size() / 8};
     for (size_t i = 0; i < n; ++i) {
       if (segs[i].size() % 8) throw std::invalid_argument("segment not word-aligned");
       uint32_t w = (uint32_t)(segs[i].size() / 8);
-      std::memcpy(words.data() + 4 * (i + 1), &w, 4);
-    }
-    std::vector<uint64_t> swo = {0, words.size() / 8};
-    for (auto &s : segs) {
-      words.insert(words.end(), s.begin(), s.end());
-      swo.push_back(words.size() / 8);
+      std::memcpy(table.data() + 4 * (i + 1), &w, 4);
+      pieces.push_back(segs[i].empty() ? nullptr : segs[i].data());
+      swo.push_back(swo.back() + w);
     }
     std::vector<uint8_t> out(cpk_batch_packed_capacity(swo.data(), (uint32_t)n + 1));
     std::vector<uint64_t> off(n + 2);
-    check(cpk_encode_host(gpu.get(), words.data(), swo.data(), (uint32_t)n + 1, out.data(),
-                          out.size(), off.data()),
+    check(cpk_encode_host_gather(gpu.get(), pieces.data(), swo.data(), (uint32_t)n + 1,
+                                 out.data(), out.size(), off.data()),
           "SerializePacked.write");
     out.resize(off[n + 1]);
     return out;
