@@ -32,7 +32,7 @@ EXPORTS = [
     "cpk_decode_batch", "cpk_decode_stream", "cpk_encode_host", "cpk_decode_host",
     "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch", "cpk_ctx_take_error",
     "cpk_decode_messages", "cpk_encode_messages", "cpk_encode_messages_host",
-    "cpk_decode_messages_host", "cpk_encode_host_gather",
+    "cpk_decode_messages_host", "cpk_encode_host_gather", "cpk_encode_messages_host_gather",
 ]
 
 
@@ -89,6 +89,7 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_decode_messages": ([vp, vp, vp, u32, u64, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp], i32),
         "cpk_encode_messages": ([vp, vp, vp, u32, vp, u32, u64, vp, vp, vp], i32),
         "cpk_encode_messages_host": ([vp, vp, vp, u32, vp, u32, vp, u64, vp], i32),
+        "cpk_encode_messages_host_gather": ([vp, vp, vp, u32, vp, u32, vp, u64, vp], i32),
         "cpk_decode_messages_host": ([vp, vp, vp, u32, u64, vp, u64, vp, u32, vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
@@ -291,6 +292,23 @@ def _encode_messages_host(self, messages):
     return out[: int(off[-1])].tobytes(), off
 
 
+def _encode_messages_host_gather(self, messages):
+    """As _encode_messages_host, each segment passed where it lies
+    (cpk_encode_messages_host_gather)."""
+    segs = [np.frombuffer(bytes(s), np.uint8) for m in messages for s in m]
+    swo = np.concatenate([[0], np.cumsum([s.size // 8 for s in segs], dtype=np.uint64)]).astype(np.uint64)
+    mso = np.concatenate([[0], np.cumsum([len(m) for m in messages], dtype=np.uint64)]).astype(np.uint64)
+    ptrs = (ctypes.c_void_p * max(len(segs), 1))(*[s.ctypes.data if s.size else None for s in segs])
+    cap = batch_capacity(swo) + sum(10 * ((len(m) + 2) // 2 + 1) for m in messages)
+    out = np.zeros(cap, np.uint8)
+    off = np.zeros(len(messages) + len(segs) + 1, np.uint64)
+    _check(self._lib.cpk_encode_messages_host_gather(self.handle, ptrs, swo.ctypes.data,
+                                                     len(segs), mso.ctypes.data, len(messages),
+                                                     out.ctypes.data, cap, off.ctypes.data),
+           "cpk_encode_messages_host_gather")
+    return out[: int(off[-1])].tobytes(), off
+
+
 def _decode_messages_host(self, packed, msg_off, traversal_limit_words: int = 8 * 1024 * 1024):
     """Serialize.read per message -> (message statuses, [[segment bytes]])."""
     pk = np.frombuffer(bytes(packed), np.uint8)
@@ -320,6 +338,7 @@ def _decode_messages_host(self, packed, msg_off, traversal_limit_words: int = 8 
 
 
 Context.encode_messages_host = _encode_messages_host
+Context.encode_messages_host_gather = _encode_messages_host_gather
 Context.decode_messages_host = _decode_messages_host
 
 

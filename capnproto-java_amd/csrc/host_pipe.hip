@@ -444,9 +444,16 @@ struct DevBufs {  // hipFree on scope exit
 
 extern "C" {
 
-int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32_t nseg,
-                             const uint64_t *h_msg_seg_off, uint32_t nm, void *h_out,
-                             uint64_t h_out_cap, uint64_t *h_out_off) {
+}  // extern "C"
+
+namespace {
+
+// cpk_encode_messages_host(_gather): `fill(d_in, words)` puts the segments'
+// words, back to back, into device memory
+template <class Fill>
+int encode_messages_host_impl(cpk_ctx ctx, Fill fill, const uint64_t *h_swo, uint32_t nseg,
+                              const uint64_t *h_msg_seg_off, uint32_t nm, void *h_out,
+                              uint64_t h_out_cap, uint64_t *h_out_off) {
   if (!ctx || !h_swo || !h_msg_seg_off || !h_out_off) return CPK_EINVAL;
   if (h_msg_seg_off[0] != 0 || h_msg_seg_off[nm] != nseg) return CPK_EINVAL;
   for (uint32_t m = 0; m < nm; ++m)
@@ -472,7 +479,7 @@ int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_sw
   uint64_t *d_swo = (uint64_t *)b.get((nseg + 1) * 8ull), *d_ms = (uint64_t *)b.get((nm + 1) * 8ull);
   uint64_t *d_off = (uint64_t *)b.get(((uint64_t)nm + nseg + 1) * 8);
   if (!d_in || !d_out || !d_swo || !d_ms || !d_off) return CPK_ENOMEM;
-  if ((words && hipMemcpy(d_in, (const uint8_t *)h_in + 8 * h_swo[0], words * 8, hipMemcpyHostToDevice)) ||
+  if ((words && fill(d_in, words)) ||
       hipMemcpy(d_swo, rel.data(), (nseg + 1) * 8ull, hipMemcpyHostToDevice) ||
       hipMemcpy(d_ms, h_msg_seg_off, (nm + 1) * 8ull, hipMemcpyHostToDevice))
     return CPK_EDEVICE;
@@ -484,6 +491,43 @@ int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_sw
   const uint64_t P = h_out_off[(uint64_t)nm + nseg];
   if (P > h_out_cap) return CPK_ENOMEM;
   return hip_ok(hipMemcpy(h_out, d_out, P, hipMemcpyDeviceToHost));
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32_t nseg,
+                             const uint64_t *h_msg_seg_off, uint32_t nm, void *h_out,
+                             uint64_t h_out_cap, uint64_t *h_out_off) {
+  if (!h_swo) return CPK_EINVAL;
+  const uint8_t *src = (const uint8_t *)h_in + 8 * h_swo[0];
+  return encode_messages_host_impl(
+      ctx,
+      [&](void *d_in, uint64_t words) {
+        return hipMemcpy(d_in, src, words * 8, hipMemcpyHostToDevice) != hipSuccess;
+      },
+      h_swo, nseg, h_msg_seg_off, nm, h_out, h_out_cap, h_out_off);
+}
+
+int cpk_encode_messages_host_gather(cpk_ctx ctx, const void *const *h_segs, const uint64_t *h_swo,
+                                    uint32_t nseg, const uint64_t *h_msg_seg_off, uint32_t nm,
+                                    void *h_out, uint64_t h_out_cap, uint64_t *h_out_off) {
+  if (!h_swo || (nseg && !h_segs)) return CPK_EINVAL;
+  for (uint32_t i = 0; i < nseg; ++i)
+    if (h_swo[i + 1] > h_swo[i] && !h_segs[i]) return CPK_EINVAL;
+  return encode_messages_host_impl(
+      ctx,
+      [&](void *d_in, uint64_t words) {
+        // segments gathered by host threads into pinned memory, one DMA
+        void *pin = nullptr;
+        if (hipHostMalloc(&pin, words * 8, hipHostMallocDefault) != hipSuccess) return true;
+        gather_copy((uint8_t *)pin, h_segs, h_swo, 0, nseg);
+        const bool bad = hipMemcpy(d_in, pin, words * 8, hipMemcpyHostToDevice) != hipSuccess;
+        hipHostFree(pin);
+        return bad;
+      },
+      h_swo, nseg, h_msg_seg_off, nm, h_out, h_out_cap, h_out_off);
 }
 
 int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_msg_off, uint32_t nm,

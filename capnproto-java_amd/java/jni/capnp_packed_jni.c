@@ -252,3 +252,49 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeGather(
   (*env)->ReleaseLongArrayElements(env, outOff, off, st == CPK_OK ? 0 : JNI_ABORT);
   if (st != CPK_OK) throw_status(env, st);
 }
+
+/* void PackedGpu.nativeEncodeMessagesGather(long h, ByteBuffer[] segs, int[] positions,
+ *     long[] segWordOff, long[] msgSegOff, ByteBuffer out, long[] outOff)
+ * nativeEncodeMessages with every segment a direct buffer packed where it
+ * lies (cpk_encode_messages_host_gather; builder segments allocated DIRECT,
+ * DefaultAllocator.java:56-62). */
+JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeMessagesGather(
+    JNIEnv *env, jclass k, jlong h, jobjectArray segs, jintArray positions, jlongArray segWordOff,
+    jlongArray msgSegOff, jobject out, jlongArray outOff) {
+  (void)k;
+  void *pout = (*env)->GetDirectBufferAddress(env, out);
+  jlong cap = (*env)->GetDirectBufferCapacity(env, out);
+  jsize ns = (*env)->GetArrayLength(env, segs);
+  if (!pout || (*env)->GetArrayLength(env, segWordOff) != ns + 1) {
+    throw_status(env, CPK_EINVAL);
+    return;
+  }
+  const void **ptrs = (const void **)calloc((size_t)(ns ? ns : 1), sizeof(void *));
+  if (!ptrs) {
+    throw_status(env, CPK_ENOMEM);
+    return;
+  }
+  jint *pos = (*env)->GetIntArrayElements(env, positions, NULL);
+  int st = CPK_OK;
+  for (jsize i = 0; i < ns && st == CPK_OK; ++i) {
+    jobject b = (*env)->GetObjectArrayElement(env, segs, i);
+    uint8_t *a = (uint8_t *)(*env)->GetDirectBufferAddress(env, b);
+    if (!a) st = CPK_EINVAL;
+    else ptrs[i] = a + pos[i];
+    (*env)->DeleteLocalRef(env, b);
+  }
+  (*env)->ReleaseIntArrayElements(env, positions, pos, JNI_ABORT);
+  jsize nm1 = (*env)->GetArrayLength(env, msgSegOff);
+  jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
+  jlong *mso = (*env)->GetLongArrayElements(env, msgSegOff, NULL);
+  jlong *off = (*env)->GetLongArrayElements(env, outOff, NULL);
+  if (st == CPK_OK)
+    st = cpk_encode_messages_host_gather((cpk_ctx)(intptr_t)h, ptrs, (const uint64_t *)swo,
+                                         (uint32_t)ns, (const uint64_t *)mso, (uint32_t)(nm1 - 1),
+                                         pout, (uint64_t)cap, (uint64_t *)off);
+  free(ptrs);
+  (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, msgSegOff, mso, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, outOff, off, st == CPK_OK ? 0 : JNI_ABORT);
+  if (st != CPK_OK) throw_status(env, st);
+}

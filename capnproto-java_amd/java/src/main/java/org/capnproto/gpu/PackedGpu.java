@@ -33,6 +33,9 @@ public final class PackedGpu implements AutoCloseable {
                                                     long[] totals);
     private static native void nativeEncodeGather(long handle, ByteBuffer[] pieces, int[] positions,
                                                   long[] segWordOff, ByteBuffer out, long[] outOff);
+    private static native void nativeEncodeMessagesGather(long handle, ByteBuffer[] segs, int[] positions,
+                                                          long[] segWordOff, long[] msgSegOff,
+                                                          ByteBuffer out, long[] outOff);
     private static native long nativeDecodeStream(long handle, ByteBuffer packed, int position,
                                                   int limit, long[] segWordOff, ByteBuffer out);
 
@@ -112,12 +115,22 @@ public final class PackedGpu implements AutoCloseable {
         }
         mso[nm] = s;
         swo[nseg] = words;
-        ByteBuffer in = ByteBuffer.allocateDirect((int) (words * 8 + 8)).order(ByteOrder.LITTLE_ENDIAN);
-        for (ByteBuffer[] m : messages)
-            for (ByteBuffer b : m) in.put(b.duplicate());
         ByteBuffer out = ByteBuffer.allocateDirect((int) (nativeCapacity(swo) + tableCap));
         long[] off = new long[nm + nseg + 1];
-        nativeEncodeMessages(handle, in, swo, mso, out, off);
+        ByteBuffer[] flat = new ByteBuffer[nseg];
+        boolean direct = true;
+        s = 0;
+        for (ByteBuffer[] m : messages)
+            for (ByteBuffer b : m) { flat[s++] = b; direct &= b.isDirect(); }
+        if (direct) {  // DIRECT builder segments: packed where they lie
+            int[] pos = new int[nseg];
+            for (int i = 0; i < nseg; ++i) pos[i] = flat[i].position();
+            nativeEncodeMessagesGather(handle, flat, pos, swo, mso, out, off);
+        } else {
+            ByteBuffer in = ByteBuffer.allocateDirect((int) (words * 8 + 8)).order(ByteOrder.LITTLE_ENDIAN);
+            for (ByteBuffer b : flat) in.put(b.duplicate());
+            nativeEncodeMessages(handle, in, swo, mso, out, off);
+        }
         out.limit((int) off[nm + nseg]);
         return new Packed(out, off);
     }

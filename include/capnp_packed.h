@@ -220,6 +220,14 @@ int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
 int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_seg_word_off,
                              uint32_t nseg, const uint64_t *h_msg_seg_off, uint32_t nm,
                              void *h_out, uint64_t h_out_cap, uint64_t *h_out_off);
+/* Gather form of cpk_encode_messages_host: segment i is the
+ * h_swo[i+1] - h_swo[i] words at h_segs[i] (any host pointer; NULL only for
+ * an empty segment), e.g. each MessageBuilder's own segment buffers
+ * (BuilderArena.getSegmentsForOutput, BuilderArena.java:143-154).  Output as
+ * cpk_encode_messages_host. */
+int cpk_encode_messages_host_gather(cpk_ctx ctx, const void *const *h_segs, const uint64_t *h_swo,
+                                    uint32_t nseg, const uint64_t *h_msg_seg_off, uint32_t nm,
+                                    void *h_out, uint64_t h_out_cap, uint64_t *h_out_off);
 int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_msg_off,
                              uint32_t nm, uint64_t traversal_limit_words, void *h_out,
                              uint64_t out_cap_words, uint64_t *h_seg_word_off, uint32_t seg_cap,

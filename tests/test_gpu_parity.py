@@ -577,6 +577,8 @@ def test_message_host_forms(ctx, oracle):
              for _ in range(int(rng.integers(1, 6)))] for _ in range(60)]
     pk, off = ctx.encode_messages_host(msgs)
     assert pk == b"".join(oracle.write_message(m) for m in msgs)
+    pkg, offg = ctx.encode_messages_host_gather(msgs)  # segments where they lie
+    assert pkg == pk and np.array_equal(offg, off)
     mso = np.concatenate([[0], np.cumsum([len(m) for m in msgs])])
     moff = off[(mso[:-1] + np.arange(len(msgs))).astype(np.int64)]
     moff = np.append(moff, off[-1])
