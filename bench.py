@@ -5,21 +5,33 @@ Metric (BASELINE.json): "GiB/s packed encode+decode (device-resident
 segments) at 1/2/4/8 MI355X".  One step = one PackedOutputStream.write per
 piece (encode) + one PackedInputStream.read per piece (decode) over the whole
 batch, i.e. a round trip of every segment, inputs already resident in HBM.
-value = unpacked bytes of all ranks / (max over ranks of the timed wall time).
+value = unpacked bytes of all ranks / (max over ranks of the timed wall time
+per step); encode_ms / decode_ms are the medians of the HIP-event times.
 
-Workload (configs[1]): 1 Mi pieces x 64 KiB (8192 words), ~50 % zero words
-(z=0.5, Lz=4, q=0.25), synthetic, one shard per GPU (weak
-scaling, no collective: pieces are independent, Serialize.java:283-287).
+Workloads (synthetic Markov generator on the device):
+  --config 2 (default, configs[1]): 1 Mi pieces x 64 KiB per GPU, ~50 % zero
+             words, cpk_encode_batch / cpk_decode_batch;
+  --config 3: 256 Ki messages x 4 segments per GPU, segment sizes uniform over
+             {4..256} KiB, dense; SerializePacked.write / read per message
+             (cpk_encode_messages / cpk_decode_messages: tables included);
+  --config 4: 1 Mi pieces x 64 KiB per GPU, ~90 % zero words.
+Multi-GPU (config 5 = config 2 per GPU): one shard per rank, contiguous
+piece ranges of the global batch (capnp_packed.shard.plan_shards), no
+collective on the data path (pieces are independent, Serialize.java:283-287).
 
-Run:  python bench.py [--gpus N --steps K --warmup W --config 2 --segments S]
-Multi-GPU: torch.distributed.run, one rank per GPU (RCCL only for the
-barrier and the max-over-ranks reduction of the timings).
+Run:  python bench.py [--gpus N --steps K --warmup W --config C]
+  --gpus N without a torch.distributed launcher starts N rank processes
+  itself (before any GPU call); under torchrun WORLD_SIZE must equal N.
+  --stub: CPU-only rehearsal of the multi-rank path (gloo, the oracle as
+  the "kernel"), used by tests/test_shard.py.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -31,67 +43,166 @@ sys.path.insert(0, str(REPO / "capnproto-java_amd"))
 
 GIB = float(1 << 30)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SEED = 0x1D2ACD47
+CFG3_SEG_WORDS = np.array([512, 1024, 2048, 4096, 8192, 16384, 32768], dtype=np.uint64)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4])
-    ap.add_argument("--segments", type=int, default=1 << 20, help="pieces per GPU")
+    ap.add_argument("--segments", type=int, default=None,
+                    help="pieces per GPU (config 3: messages per GPU)")
     ap.add_argument("--seg-words", type=int, default=8192)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
-                    help="time budget of the CPU baseline sample")
+                    help="time budget of each CPU-baseline sample (1 thread, then all threads)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--sample-check", type=int, default=64,
                     help="pieces re-packed on the host oracle and compared")
-    return ap.parse_args()
+    ap.add_argument("--stub", action="store_true", help="CPU rehearsal (gloo, no GPU)")
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------- launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn(args) -> int:
+    """Start args.gpus rank processes (this process never touches the GPU)
+    and return the worst exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    for p in procs:
+        p.wait()
+        rc = rc or p.returncode
+    return rc
+
+
+# ---------------------------------------------------------------- workloads
+def global_layout(args, world):
+    """The whole job's batch (all ranks) and each rank's shard boundaries.
+    Config 3: message segment counts / sizes from a seeded RNG (identical on
+    every rank); configs 2/4: uniform pieces."""
+    from capnp_packed.shard import plan_shards
+    if args.config == 3:
+        nm = (args.segments or (1 << 18)) * world
+        rng = np.random.default_rng(SEED)
+        seg_words = CFG3_SEG_WORDS[rng.integers(0, len(CFG3_SEG_WORDS), size=4 * nm)]
+        msg_words = seg_words.reshape(nm, 4).sum(1)
+        mwo = np.concatenate([[0], np.cumsum(msg_words)]).astype(np.uint64)
+        bounds = plan_shards(mwo, world)  # messages per rank, balanced by bytes
+        return dict(seg_words=seg_words, bounds=bounds)
+    n = (args.segments or (1 << 20)) * world
+    swo = np.arange(0, (n + 1) * args.seg_words, args.seg_words, dtype=np.uint64)
+    return dict(swo=swo, bounds=plan_shards(swo, world))
+
+
+def rank_shard(args, lay, rank):
+    """This rank's pieces: (seg_word_off from 0, msg_seg_off or None)."""
+    b0, b1 = int(lay["bounds"][rank]), int(lay["bounds"][rank + 1])
+    if args.config == 3:
+        sw = lay["seg_words"][4 * b0: 4 * b1]
+        swo = np.concatenate([[0], np.cumsum(sw)]).astype(np.uint64)
+        mso = np.arange(0, 4 * (b1 - b0) + 1, 4, dtype=np.uint64)
+        return swo, mso
+    swo = lay["swo"][b0: b1 + 1] - lay["swo"][b0]
+    return swo.astype(np.uint64), None
+
+
+# ---------------------------------------------------------------- GPU rank
+def run_rank(args, rank, world, local):
     import torch
     import capnp_packed as cp
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
     ctx = cp.Context(local)
-    n = args.segments
-    sw = args.seg_words
-    swo = np.arange(0, (n + 1) * sw, sw, dtype=np.uint64)
-    d_swo = torch.from_numpy(swo.astype(np.int64)).to(dev)
-    words = n * sw
+
+    lay = global_layout(args, world)
+    swo, mso = rank_shard(args, lay, rank)
+    n = len(swo) - 1
+    words = int(swo[-1])
     U = 8 * words
+    maxw = int(np.diff(swo).max()) if n else 0
+    d_swo = torch.from_numpy(swo.astype(np.int64)).to(dev)
     d_in = torch.empty(words, dtype=torch.int64, device=dev)
     params = cp.preset(args.config)
     params.cfg = args.config | (rank << 8)          # distinct shard per rank
     ctx.generate(params, d_swo, d_in)
-    cap = cp.batch_capacity(swo)
-    d_pk = torch.empty((cap + 255) // 256 * 256, dtype=torch.uint8, device=dev)
-    d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    d_out = torch.empty(words, dtype=torch.int64, device=dev)
-    d_st = torch.empty(n, dtype=torch.int32, device=dev)
+    d_out = torch.empty(words + 1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
+
+    if mso is None:
+        cap = cp.batch_capacity(swo)
+        d_pk = torch.empty((cap + 255) // 256 * 256, dtype=torch.uint8, device=dev)
+        d_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_st = torch.empty(n, dtype=torch.int32, device=dev)
+
+        def encode():
+            ctx.encode_batch(d_in, d_swo, maxw, d_pk, d_off, stream)
+
+        def decode():
+            ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st, stream)
+
+        def piece_range(i):
+            return int(offs[i]), int(offs[i + 1])
+    else:
+        nm = len(mso) - 1
+        d_mso = torch.from_numpy(mso.astype(np.int64)).to(dev)
+        segs_per = np.diff(mso)
+        cap = cp.batch_capacity(swo) + int(sum(10 * ((c + 2) // 2 + 1) for c in segs_per))
+        d_pk = torch.empty((cap + 255) // 256 * 256, dtype=torch.uint8, device=dev)
+        d_off = torch.empty(nm + n + 1, dtype=torch.int64, device=dev)
+        # message m starts at piece mso[m] + m (its table), the last entry is the total
+        d_msg_idx = d_mso + torch.arange(nm + 1, device=dev, dtype=torch.int64)
+        d_moff = torch.empty(nm + 1, dtype=torch.int64, device=dev)
+        d_swo_o = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_sio = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_sst = torch.empty(n, dtype=torch.int32, device=dev)
+        d_mso_o = torch.empty(nm + 1, dtype=torch.int64, device=dev)
+        d_st = torch.empty(nm, dtype=torch.int32, device=dev)
+        msg_fail = [0]
+
+        def encode():
+            ctx.encode_messages(d_in, d_swo, d_mso, maxw, d_pk, d_off, stream)
+
+        def decode():
+            torch.index_select(d_off, 0, d_msg_idx, out=d_moff)
+            rc, tw, ts = ctx.decode_messages(d_pk, d_moff, d_out, d_swo_o, d_sio, d_sst,
+                                             d_mso_o, d_st, stream=stream)
+            if rc != cp.OK or tw != words or ts != n:
+                msg_fail[0] += 1
+
+        def piece_range(i):
+            # segment i of message i // 4 is piece mso[m] + m + 1 + (i - mso[m])
+            p = i + i // 4 + 1
+            return int(offs[p]), int(offs[p + 1])
     torch.cuda.synchronize(dev)
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        ctx.encode_batch(d_in, d_swo, sw, d_pk, d_off, stream)
+        encode()
         if ev is not None:
             ev[1].record(stream)
-        ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st, stream)
+        decode()
         if ev is not None:
             ev[2].record(stream)
 
@@ -111,42 +222,55 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    enc_t = [e[0].elapsed_time(e[1]) for e in evs]
+    dec_t = [e[1].elapsed_time(e[2]) for e in evs]
+    enc_ms, dec_ms = float(np.median(enc_t)), float(np.median(dec_t))
 
     # ---- parity: decoded == input, statuses, sample vs the host oracle ----
     cnt = torch.zeros(1, dtype=torch.int64, device=dev)
     ctx.count_mismatch(d_in, d_out, words, cnt, stream)
     bad_status = int((d_st != 0).sum().item())
+    if mso is not None:
+        bad_status += int((d_sst != 0).sum().item()) + msg_fail[0]
     mism = int(cnt.item())
-    P = int(d_off[-1].item())
+    offs = d_off.cpu().numpy().astype(np.uint64)
+    P = int(offs[-1])
     sample_ok = None
     if rank == 0 and args.sample_check > 0:
         sys.path.insert(0, str(REPO / "oracle"))
-        import oracle  # checker only
+        import oracle  # checker only, after the timed region
         rng = np.random.default_rng(0)
         idx = np.unique(np.concatenate([[0, n - 1], rng.integers(0, n, size=args.sample_check)]))
-        off = d_off.cpu().numpy().astype(np.uint64)
         op = oracle.preset(args.config)
         op.cfg = params.cfg
         sample_ok = True
         for i in idx:
             host = oracle.generate(op, swo, first=int(i), count=1)
-            ref = oracle.pack(host)
-            got = d_pk[int(off[i]): int(off[i + 1])].cpu().numpy().tobytes()
-            if ref != got:
+            a, b = piece_range(int(i))
+            if oracle.pack(host) != d_pk[a:b].cpu().numpy().tobytes():
                 sample_ok = False
                 break
+        if mso is not None and sample_ok:
+            # whole messages = SerializePacked.write bytes (Serialize.java:256-288)
+            for m in np.unique(rng.integers(0, len(mso) - 1, size=8)):
+                s0, s1 = int(mso[m]), int(mso[m + 1])
+                segs = [oracle.generate(op, swo, first=s, count=1).tobytes() for s in range(s0, s1)]
+                a, b = int(offs[s0 + m]), int(offs[s1 + m + 1])
+                if oracle.write_message(segs) != d_pk[a:b].cpu().numpy().tobytes():
+                    sample_ok = False
+                    break
 
     if dist:
         from capnp_packed.shard import reduce_max_sum
-        mx, sm = reduce_max_sum([wall, enc_ms, dec_ms, float(mism + bad_status), float(P)])
+        mx, sm = reduce_max_sum([wall, enc_ms, dec_ms, float(mism + bad_status), float(P), float(U)])
         wall, enc_ms, dec_ms = mx[0], mx[1], mx[2]
         errors = int(sm[3])
-        P_total = sm[4]
+        P_total, U_total = sm[4], sm[5]
+        per_rank = {"encode_ms_max": round(mx[1], 4), "decode_ms_max": round(mx[2], 4)}
     else:
         errors = mism + bad_status
-        P_total = float(P)
+        P_total, U_total = float(P), float(U)
+        per_rank = None
 
     if rank != 0:
         if dist:
@@ -154,29 +278,21 @@ def main():
         return
 
     ms_per_step = 1e3 * wall / args.steps
-    value = world * U / GIB / (wall / args.steps)
+    value = U_total / GIB / (wall / args.steps)
     r = P / U
-    # Roofline of the dominant kernel.  The encode stage is two kernels (the
-    # size pass e4_size_kernel and the emit pass e4_emit_kernel, plus a scan
-    # of a few microseconds) and the decode stage one (decode_kernel); each
-    # of the three reads or writes U+P algorithmic bytes (the size pass: U).
-    # decode_kernel is the longest single launch (rocprofv3 summaries under
-    # profiles/), so the roofline object is decode_kernel's: U+P per launch
-    # over its HIP-event time; the encode stage's figure is reported beside it.
-    dom = "decode"
+    # Roofline of the dominant kernel: the decode stage is one launch of
+    # decode_kernel (U+P algorithmic bytes); the encode stage's kernels are
+    # reported beside it.  HIP events on the launch stream, median of K.
     dom_ms = dec_ms
     achieved = (U + P) / (dom_ms * 1e-3) / 1e9
-    # HBM bytes per launch of the dominant kernel from the committed PMC
-    # passes (tools/profile.sh + tools/pmc_summary.py), when they were taken
-    # on this same workload
     traffic = None
     pmc = REPO / "profiles" / "pmc_traffic.json"
-    workload_key = f"config{args.config}:{n}x{sw}"
+    workload_key = f"config{args.config}:{n}x{args.seg_words if mso is None else 'mixed'}"
     if pmc.exists():
         try:
             t = json.loads(pmc.read_text())
-            if t.get("workload") == workload_key and dom in t:
-                traffic = int(t[dom]["hbm_bytes"])
+            if t.get("workload") == workload_key and "decode" in t:
+                traffic = int(t["decode"]["hbm_bytes"])
         except (ValueError, KeyError, TypeError):
             traffic = None
 
@@ -184,6 +300,12 @@ def main():
     if not args.no_cpu:
         cpu = cpu_baseline(args, params)
 
+    if mso is None:
+        workload = (f"config{args.config}: {n} pieces x {8 * args.seg_words // 1024} KiB per GPU, "
+                    + {2: "~50% zero words", 4: "~90% zero words"}[args.config])
+    else:
+        workload = (f"config3: {len(mso) - 1} messages x 4 segments (4-256 KiB) per GPU, dense "
+                    "(<10% zero words), SerializePacked.write/read incl. segment tables")
     line = {
         "metric": "GiB/s packed encode+decode (device-resident segments)",
         "value": round(value, 2),
@@ -198,18 +320,18 @@ def main():
         "dtype": "u8",
         "data": "synthetic (device Markov generator, SURVEY.md 8d)",
         "config": {
-            "workload": f"config{args.config}: {n} pieces x {8 * sw // 1024} KiB per GPU, "
-                        + {2: "~50% zero words", 3: "dense (<10% zero words)", 4: "~90% zero words"}[args.config],
-            "pieces_per_gpu": n, "piece_bytes": 8 * sw, "unpacked_bytes_per_gpu": U,
+            "workload": workload,
+            "pieces_per_gpu": n, "unpacked_bytes_per_gpu": U,
             "packed_bytes_per_gpu": P, "packed_ratio": round(r, 4),
             "parallelism": f"shard x{world} (no collective)",
         },
         "encode_ms": round(enc_ms, 4),
         "decode_ms": round(dec_ms, 4),
+        "timing": "encode_ms/decode_ms: median of the K steps' HIP events; value: wall time of K steps",
         "encode_GiBps": round(U / GIB / (enc_ms * 1e-3), 2),
         "decode_GiBps": round(U / GIB / (dec_ms * 1e-3), 2),
         "roofline": {
-            "kernel": f"{dom}_kernel",
+            "kernel": "decode_kernel",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": PEAK_HBM_GBS,
@@ -219,57 +341,150 @@ def main():
             "algorithmic_bytes_per_launch": U + P,
         },
         "encode_stage_roofline": {
-            "kernels": ["e4_size_kernel", "e4_scan_*", "e4_emit_kernel"],
             "achieved": round((U + P) / (enc_ms * 1e-3) / 1e9, 1),
             "frac": round((U + P) / (enc_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-            "note": "algorithmic U+P over the stage's event time; the stage reads U twice",
+            "note": "algorithmic U+P over the encode stage's event time",
         },
         "roundtrip_roofline_frac": round(2 * (U + P) / ((enc_ms + dec_ms) * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
         "parity": {"mismatched_words_plus_bad_status": errors, "oracle_sample_equal": sample_ok},
         "cpu_baseline": cpu,
     }
+    if per_rank:
+        line["per_rank"] = per_rank
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
+# ---------------------------------------------------------------- CPU baseline
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    """Threads for the multi-core leg: the CPUs this process may use, capped
+    at 16 (a one-GPU box's share of its host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(args, params):
-    """The oracle's scalar restatement of the Java loops ("port"), 1 thread,
-    on a bounded sample of the same workload (same generator + seeds)."""
+    """The oracle's scalar restatement of the Java loops ("port") on a bounded
+    sample of the same workload (same generator + seeds): 1 thread, then
+    cpu_threads() threads over independent pieces."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
-    sw = args.seg_words
+    sw = args.seg_words if args.config != 3 else 8192
     m = 512  # 32 MiB per pass
     swo = np.arange(0, (m + 1) * sw, sw, dtype=np.uint64)
     op = oracle.preset(args.config)
     op.cfg = params.cfg
     data = oracle.generate(op, swo)
-    t_enc = t_dec = 0.0
-    passes = 0
-    t_start = time.perf_counter()
-    while True:
-        t0 = time.perf_counter()
-        pk, off = oracle.pack_batch(data, swo, threads=1)
-        t1 = time.perf_counter()
-        dec, st = oracle.unpack_batch(pk, off, swo, threads=1)
-        t2 = time.perf_counter()
-        assert (st == 0).all() and np.array_equal(dec, data)
-        t_enc += t1 - t0
-        t_dec += t2 - t1
-        passes += 1
-        if time.perf_counter() - t_start >= args.cpu_seconds:
-            break
-    U = passes * 8 * int(swo[-1])
+    U1 = 8 * int(swo[-1])
+
+    def leg(threads, budget):
+        t_enc = t_dec = 0.0
+        passes = 0
+        t_start = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            pk, off = oracle.pack_batch(data, swo, threads=threads)
+            t1 = time.perf_counter()
+            dec, st = oracle.unpack_batch(pk, off, swo, threads=threads)
+            t2 = time.perf_counter()
+            assert (st == 0).all() and np.array_equal(dec, data)
+            t_enc += t1 - t0
+            t_dec += t2 - t1
+            passes += 1
+            if time.perf_counter() - t_start >= budget:
+                break
+        U = passes * U1
+        return passes, U / GIB / (t_enc + t_dec), U / GIB / t_enc, U / GIB / t_dec
+
+    p1, v1, e1, d1 = leg(1, args.cpu_seconds)
+    T = cpu_threads()
+    pT, vT, eT, dT = leg(T, args.cpu_seconds / 2) if T > 1 else (p1, v1, e1, d1)
     return {
-        "value": round(U / GIB / (t_enc + t_dec), 3),
+        "value": round(vT, 3),
         "unit": "GiB/s",
-        "cores": 1,
+        "cores": T,
         "kind": "port",
-        "sample": f"{passes} passes x {m} pieces x {8 * sw // 1024} KiB (config{args.config} generator), "
-                  f"scalar C restatement of PackedOutputStream/PackedInputStream, 1 thread",
-        "encode_GiBps": round(U / GIB / t_enc, 3),
-        "decode_GiBps": round(U / GIB / t_dec, 3),
+        "cpu_model": cpu_model(),
+        "sample": f"{pT} passes x {m} pieces x {8 * sw // 1024} KiB (config{args.config} generator), "
+                  f"scalar C restatement of PackedOutputStream/PackedInputStream, {T} threads over "
+                  f"independent pieces; single thread: {p1} passes",
+        "encode_GiBps": round(eT, 3),
+        "decode_GiBps": round(dT, 3),
+        "single_thread": {"value": round(v1, 3), "encode_GiBps": round(e1, 3),
+                          "decode_GiBps": round(d1, 3), "cores": 1},
     }
+
+
+# ---------------------------------------------------------------- CPU stub
+def run_stub(args, rank, world):
+    """The multi-rank path with the oracle as the kernel (gloo): shard
+    planning, per-rank generation, round trip, barrier-bracketed timing and
+    the max/sum reduction -- what the GPU ranks do, without a GPU."""
+    import torch.distributed as dist
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    from capnp_packed.shard import reduce_max_sum
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    lay = global_layout(args, world)
+    swo, mso = rank_shard(args, lay, rank)
+    op = oracle.preset(args.config)
+    op.cfg = args.config | (rank << 8)
+    data = oracle.generate(op, swo)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    errs = 0
+    for _ in range(args.steps):
+        pk, off = oracle.pack_batch(data, swo)
+        dec, st = oracle.unpack_batch(pk, off, swo)
+        errs += int((st != 0).sum()) + int(not np.array_equal(dec, data))
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    U = float(8 * int(swo[-1]))
+    vals = [wall, float(errs), U, float(len(swo) - 1)]
+    if world > 1:
+        mx, sm = reduce_max_sum(vals)
+        dist.destroy_process_group()
+    else:
+        mx, sm = vals, vals
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "n_gpus": world, "steps": args.steps,
+                          "value": sm[2] / GIB / (mx[0] / args.steps), "errors": int(sm[1]),
+                          "pieces_total": int(sm[3]), "unpacked_bytes_total": int(sm[2]),
+                          "shard_bounds": [int(b) for b in lay["bounds"]]}), flush=True)
+
+
+def main():
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn(args))
+    world = int(env_world or 1)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub:
+        run_stub(args, rank, world)
+    else:
+        run_rank(args, rank, world, local)
 
 
 if __name__ == "__main__":

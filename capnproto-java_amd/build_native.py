@@ -10,6 +10,9 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 SRC = PKG / "csrc" / "packed_codec.hip"
 HDR = PKG.parent / "include" / "capnp_packed.h"
+# every source the library is built from: packed_codec.hip #includes the
+# other csrc/*.hip files, so any of them (or the header) being newer rebuilds
+DEPS = sorted((PKG / "csrc").glob("*.hip")) + [HDR]
 LIB = PKG / "lib" / "libcapnp_packed_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("CPK_OFFLOAD_ARCH", "gfx950")
@@ -17,7 +20,7 @@ ARCH = os.environ.get("CPK_OFFLOAD_ARCH", "gfx950")
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     if (not force and LIB.exists()
-            and LIB.stat().st_mtime >= max(SRC.stat().st_mtime, HDR.stat().st_mtime)):
+            and LIB.stat().st_mtime >= max(d.stat().st_mtime for d in DEPS)):
         return LIB
     LIB.parent.mkdir(parents=True, exist_ok=True)
     cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",

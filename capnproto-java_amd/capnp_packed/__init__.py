@@ -5,9 +5,12 @@ Mirrors capnproto-java's packed API for the hot path:
     (each piece = one PackedOutputStream.write / PackedInputStream.read,
     runtime/src/main/java/org/capnproto/PackedOutputStream.java:35-205,
     PackedInputStream.java:35-140).
-  * PackedOutputStream / PackedInputStream / SerializePacked in
-    capnp_packed.stream -- the reference's stream classes, same names and
-    error behaviour, routed through the batch kernels.
+  * encode_messages / decode_messages -- SerializePacked.write / read per
+    message (Serialize.java:256-288, :119-178), segment tables on the device.
+  * host-memory forms (encode_host, decode_host, *_gather, decode_stream_host)
+    for ByteBuffers that start and end in host memory.
+The reference's stream classes themselves are mirrored in C++
+(csrc/host/packed_stream.hpp) and Java (java/, INTEGRATION.md).
 
 torch is used only for device memory and streams.  There is no CPU fallback:
 if the HIP library cannot be loaded every entry point raises.
@@ -24,7 +27,6 @@ LIB_PATH = _PKG / "lib" / "libcapnp_packed_hip.so"
 
 OK, EINVAL, ETRUNC, EOVERRUN, ETRAILING, ENOMEM, EDEVICE, EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6, -8
 EFRAME = -7  # segment table invalid (Serialize.java:45-53, :125-163)
-TILE_WORDS = 8192  # encoder tile: larger pieces are cut into tiles
 
 EXPORTS = [
     "cpk_abi_version", "cpk_status_string", "cpk_packed_bound", "cpk_batch_packed_capacity",

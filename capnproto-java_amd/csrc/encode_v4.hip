@@ -22,7 +22,53 @@ constexpr uint32_t kE4RingBytes = 2048;  // output ring per wave (<= 41 live lin
 constexpr uint32_t kE4oLut = 0;                                   // u64[256]
 constexpr uint32_t kE4oRing = 2048;                               // u32[waves][512]
 constexpr uint32_t kE4Lds = kE4oRing + kE4Waves * kE4RingBytes;   // 10 KiB
-static_assert(kE4RingBytes == kE3RingBytes, "the v3 ring helpers are reused");
+
+constexpr uint32_t kE4RingLines = kE4RingBytes / 16;
+constexpr uint32_t kE4RingDw = kE4RingBytes / 4;
+
+// nonzero-byte tag of a word (PackedOutputStream.java:64-117): bit i set iff
+// byte i != 0.  SWAR: bit 7 of every byte of t = byte != 0, gathered by shifts.
+__device__ __forceinline__ uint32_t e4_tag(uint64_t v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t tl = ((lo & 0x7f7f7f7fu) + 0x7f7f7f7fu) | lo;
+  const uint32_t th = ((hi & 0x7f7f7f7fu) + 0x7f7f7f7fu) | hi;
+  const uint32_t y = ((tl >> 7) & 0x01010101u) | ((th >> 3) & 0x10101010u);
+  return (y | (y >> 7) | (y >> 14) | (y >> 21)) & 0xffu;
+}
+
+// bytes [j0, j1) of global line L from the ring, then clears the ring line
+__device__ __forceinline__ void e4_store_bytes(uint8_t *out, uint32_t *ring, uint64_t L, int j0,
+                                               int j1, int lane) {
+  uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kE4RingLines - 1));
+  const uint4 val = *rl;
+  if (lane >= j0 && lane < j1) {
+    const uint32_t d = (lane & 8) ? ((lane & 4) ? val.w : val.z) : ((lane & 4) ? val.y : val.x);
+    out[L * 16 + lane] = (uint8_t)(d >> (8 * (lane & 3)));
+  }
+  wave_lds_order();
+  if (lane == 0) *rl = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// stores the complete lines [fl, upto) of the ring; bytes below `lo` belong
+// to the previous piece (only the piece's first line can hold them)
+__device__ __forceinline__ void e4_flush(uint8_t *out, uint32_t *ring, uint64_t &fl, uint64_t upto,
+                                         uint64_t lo, int lane) {
+  if (fl >= upto) return;
+  if (fl * 16 < lo) {
+    e4_store_bytes(out, ring, fl, (int)(lo - fl * 16), 16, lane);
+    ++fl;
+  }
+  for (uint64_t L0 = fl; L0 < upto; L0 += 64) {
+    const uint64_t L = L0 + lane;
+    if (L < upto) {
+      uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kE4RingLines - 1));
+      const uint4 val = *rl;
+      *rl = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4 *>(out + L * 16) = val;
+    }
+  }
+  fl = upto;
+}
 
 #ifndef CPK_E4_WPE
 #define CPK_E4_WPE 8
@@ -55,7 +101,7 @@ __device__ __forceinline__ int e4_group(uint32_t m, bool valid) {
 // gl: group of the word before the step (2 at the piece start); updated to
 // the group of the step's last word (2 for M or past the end)
 __device__ __forceinline__ E4Cls e4_classify(uint64_t word, bool valid, int &gl) {
-  const uint32_t m = e3_tag(word);
+  const uint32_t m = e4_tag(word);
   const int g = e4_group(m, valid);
   const int gp = wave_shr1(g, gl);
   E4Cls c;
@@ -208,7 +254,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
         const bool valid = k < W32;
         if (s0 + j < nsteps) {
           const E4Cls c = e4_classify(v[j], valid, gl);
-          const E4Role r = e4_roles(e3_tag(v[j]), valid, c, st, lane, lem);
+          const E4Role r = e4_roles(e4_tag(v[j]), valid, c, st, lane, lem);
           acc += r.nb;
           x = lane == j ? c.BV : x;
         }
@@ -321,7 +367,7 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
                                              uint64_t bv4, E4St &st, int lane, uint64_t lem,
                                              const uint64_t *lut, uint32_t *ring, uint8_t *out,
                                              uint64_t &rpos, uint64_t &fl, uint64_t obase) {
-  const uint32_t m = e3_tag(word);
+  const uint32_t m = e4_tag(word);
   // this step's classification: the boundaries came with the look-ahead
   // (only they are kept for 4 steps: SGPR pressure), D and the last group
   // are recomputed here
@@ -372,12 +418,12 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
     const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
     const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
     const uint32_t w3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
-    const uint32_t d0 = (p >> 2) & (kE3RingDw - 1);
+    const uint32_t d0 = (p >> 2) & (kE4RingDw - 1);
     if (nb) {
       atomicOr(&ring[d0], (uint32_t)a01);
-      atomicOr(&ring[(d0 + 1) & (kE3RingDw - 1)], (uint32_t)(a01 >> 32));
-      atomicOr(&ring[(d0 + 2) & (kE3RingDw - 1)], (uint32_t)(a12 >> 32));
-      atomicOr(&ring[(d0 + 3) & (kE3RingDw - 1)], w3);
+      atomicOr(&ring[(d0 + 1) & (kE4RingDw - 1)], (uint32_t)(a01 >> 32));
+      atomicOr(&ring[(d0 + 2) & (kE4RingDw - 1)], (uint32_t)(a12 >> 32));
+      atomicOr(&ring[(d0 + 3) & (kE4RingDw - 1)], w3);
     }
     rpos += stot;
     // complete lines go out 64 at a time (one full-wave store: flushing
@@ -385,7 +431,7 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
     // 63 + 41 lines
     if ((uint32_t)(rpos >> 4) - (uint32_t)fl >= 64u) {  // (32-bit: a 64-bit < is VALU work)
       wave_lds_order();
-      e3_flush(out, ring, fl, fl + 64, obase, lane);
+      e4_flush(out, ring, fl, fl + 64, obase, lane);
     }
   }
 }
@@ -400,7 +446,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kE4oRing + w * kE4RingBytes);
   fill_luts(reinterpret_cast<uint64_t *>(smem + kE4oLut), false);
-  for (uint32_t i = lane; i < kE3RingLines; i += 64)
+  for (uint32_t i = lane; i < kE4RingLines; i += 64)
     reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
@@ -441,11 +487,11 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
       for (int j = 0; j < 4; ++j) vc[j] = vl[j];
     }
     wave_lds_order();
-    e3_flush(out, ring, fl, rpos >> 4, obase, lane);
+    e4_flush(out, ring, fl, rpos >> 4, obase, lane);
     // the piece's last, partial line
     if (rpos > fl * 16) {
       const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
-      e3_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane);
+      e4_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane);
     }
   }
 }

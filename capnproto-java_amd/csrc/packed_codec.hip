@@ -7,18 +7,13 @@
 //   (PackedOutputStream.java:36-43 re-initialises all run state per call).
 //
 // Design (DESIGN.md has the full derivation and the rooflines):
-//   encode_kernel  one 512-thread workgroup per piece (<= 8192 words), 16
-//                  words per lane held in VGPRs, word classes from a SWAR
-//                  nonzero-byte mask, run roles from three workgroup scans
-//                  (run start, run end, byte offsets), the 0xFF literal-run
-//                  chain walked only for D/L stretches > 256 words, the
-//                  packed bytes compacted in LDS and stored as 16-byte lines.
-//                  Piece output offsets come from a decoupled look-back over
-//                  an ordered ticket, so the output is one contiguous stream.
-//   decode_kernel  one 512-thread workgroup per piece: packed bytes staged in
-//                  LDS, the tag chain found by speculative per-lane walks with
-//                  pointer-doubling validation, then a gather-expand of every
-//                  8-word output block from its covering record.
+//   encoder        encode_v4.hip: one wave per piece, a size pass, a scan of
+//                  the sizes, an emit pass (tag + v_perm-compacted bytes +
+//                  count per word into an LDS ring, 16-byte line stores).
+//   decode_kernel  one wave per piece: packed bytes staged in LDS window by
+//                  window, the tag chain found by speculative per-lane walks
+//                  with pointer-doubling validation, then a gather-expand of
+//                  every 4-word output block from its covering record.
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include <stdint.h>
@@ -31,36 +26,6 @@
 #include "../../include/capnp_packed.h"
 
 namespace cpk {
-
-constexpr int kThreads = 512;
-constexpr int kWaves = kThreads / 64;
-constexpr int kChunk = 4;                       // contiguous words per lane chunk
-constexpr int kJ = 4;                           // chunks per lane
-constexpr int kWaveWords = 64 * kChunk * kJ;    // 1024
-constexpr int kTileWords = kWaves * kWaveWords; // 8192
-constexpr int kBig = 0x3fffffff;
-// encoder geometry: 1024 threads, 8 words per lane (2 chunks of 4)
-#ifndef CPK_ENC_WPE
-#define CPK_ENC_WPE 8  // waves per SIMD the encoder's registers must allow (2 workgroups per CU)
-#endif
-constexpr int kEncThreads = 1024;
-constexpr int kEncWaves = kEncThreads / 64;                 // 16
-constexpr int kEncJ = kTileWords / (kEncThreads * kChunk);  // 2
-constexpr int kEncWaveWords = 64 * kChunk * kEncJ;          // 512
-
-// ---------------------------------------------------------------- LDS maps
-// Encoder: staging for the packed bytes of one piece (bound 9*8192 = 73,728)
-// plus 16 bytes of alignment pad and slack; then LUT, bitmaps, scratch.
-constexpr uint32_t kEncStage = 9 * kTileWords + 64;
-constexpr uint32_t kEncLut = kEncStage;                 // u64[256]
-constexpr uint32_t kEncDbits = kEncLut + 2048;          // u32[256]
-constexpr uint32_t kEncHbits = kEncDbits + 1024;        // u32[256]
-constexpr uint32_t kEncScr = kEncHbits + 1024;          // int[128]
-constexpr uint32_t kEncMasks = kEncScr + 512;           // u64[16 waves][8 steps][2]
-constexpr uint32_t kEncLds = kEncMasks + 2048;          // 80,448 B -> 2 WG / CU
-
-static_assert(kEncLut % 16 == 0, "lut must be aligned");
-static_assert(kEncLds <= 81920, "2 encoder workgroups per CU");
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
@@ -240,40 +205,6 @@ __device__ __forceinline__ uint64_t ld_status(uint64_t *p) {
 __device__ __forceinline__ void lb_publish(uint64_t *status, uint32_t tile, uint64_t agg) {
   st_status(&status[tile], (tile == 0 ? kFlagInc : kFlagAgg) | agg);
 }
-// Called by all 64 lanes of one wave after lb_publish.  Returns the
-// exclusive prefix and publishes the inclusive one.
-__device__ uint64_t lb_resolve(uint64_t *status, uint32_t tile, uint64_t agg) {
-  const int lane = lane_id();
-  if (tile == 0) return 0;
-  uint64_t excl = 0;
-  int64_t top = (int64_t)tile - 1;
-  uint32_t spins = 0;
-  for (;;) {
-    int64_t idx = top - lane;
-    uint64_t v = idx >= 0 ? ld_status(&status[idx]) : kFlagInc;
-    uint64_t flag = v >> 62;
-    uint64_t inc = __ballot(flag == 2);
-    int first = inc ? __builtin_ctzll(inc) : 64;
-    uint64_t rel = first >= 63 ? ~0ull : ((2ull << first) - 1);
-    uint64_t zero = __ballot(flag == 0);
-    if (zero & rel) {
-      // bounded spin: a predecessor that never publishes must not hang the
-      // GPU (it cannot happen with in-order tickets; belt and braces)
-      if (++spins > (1u << 24)) break;
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    uint64_t val = (lane <= first) ? (v & kValMask) : 0;
-    // wave sum of 64-bit values
-    for (int d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
-    excl += val;
-    if (first < 64) break;
-    top -= 64;
-  }
-  if (lane == 0) st_status(&status[tile], kFlagInc | (excl + agg));
-  return excl;
-}
-
 // Wide form: each poll reads the 256 nearest predecessors (4 per lane), so
 // the inclusive-prefix frontier advances 256 items per memory round trip
 // instead of 64 -- the bound on items per second when thousands of waves
@@ -320,1022 +251,6 @@ __device__ uint64_t lb_resolve_wide(uint64_t *status, uint32_t tile, uint64_t ag
   }
   if (lane == 0) st_status(&status[tile], kFlagInc | (excl + agg));
   return excl;
-}
-
-// ------------------------------------------------------------ encoder
-struct WordInfo {
-  uint32_t lo, hi;
-};
-
-// find first set bit in [from, to) of an LDS bitmap; returns `to` if none
-__device__ int bm_next(const uint32_t *bits, int from, int to) {
-  if (from >= to) return to;
-  int d = from >> 5;
-  uint32_t m = bits[d] & (~0u << (from & 31));
-  while (!m) {
-    ++d;
-    if (d * 32 >= to) return to;
-    m = bits[d];
-  }
-  int p = d * 32 + __builtin_ctz(m);
-  return p < to ? p : to;
-}
-// any set bit in [lo, hi] (inclusive)?
-__device__ bool bm_any(const uint32_t *bits, int lo, int hi) {
-  if (lo > hi) return false;
-  int d0 = lo >> 5, d1 = hi >> 5;
-  for (int d = d0; d <= d1; ++d) {
-    uint32_t m = bits[d];
-    if (d == d0) m &= ~0u << (lo & 31);
-    if (d == d1) m &= (hi & 31) == 31 ? ~0u : ((2u << (hi & 31)) - 1);
-    if (m) return true;
-  }
-  return false;
-}
-
-// Re-materialise a value so masks derived from it earlier cannot be kept
-// alive across a phase (hipcc otherwise CSEs ~60 per-word compare masks and
-// spills the SGPRs).
-#define CPK_OPAQUE(x) asm volatile("" : "+v"(x))
-
-__device__ __forceinline__ int grp_of(uint32_t m) {
-  // 0 = Z (all-zero word), 1 = D/L (<= 1 zero byte), 2 = M
-  return m == 0 ? 0 : __builtin_popcount(m) >= 7 ? 1 : 2;
-}
-__device__ __forceinline__ uint32_t word_mask(uint32_t lo, uint32_t hi) {
-  return nzmask4(lo) | (nzmask4(hi) << 4);
-}
-
-// Lane-per-word encoder.  A 1024-thread workgroup holds one piece of up to
-// 8192 words: wave w owns words [512w, 512w + 512) as 8 steps of 64
-// consecutive words (lane = word).  Runs, run ends, "last D" and byte
-// offsets are 64-bit ballot masks + mbcnt inside a step, wave-uniform carries
-// across steps, and one LDS exchange across waves.
-constexpr int kSteps = kTileWords / (kEncThreads);   // 8 steps of 64 words per wave
-
-__device__ __forceinline__ uint64_t lanemask_le() {
-  const int l = lane_id();
-  return l == 63 ? ~0ull : ((2ull << l) - 1);
-}
-// highest set bit of m as a lane index (m != 0)
-__device__ __forceinline__ int hi_bit(uint64_t m) { return 63 - __builtin_clzll(m); }
-__device__ __forceinline__ int lo_bit(uint64_t m) { return __builtin_ctzll(m); }
-// number of set bits of m below this lane
-__device__ __forceinline__ int mbcnt(uint64_t m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// ---- tiled pieces: run state carried across 8192-word tiles --------------
-// A piece longer than one tile is cut into tiles that are encoded by
-// different workgroups.  What a tile's roles need from before it is the state
-// of the run that crosses its first word (PackedOutputStream.java:119-161):
-// a zero run's phase (heads every 256 words from the run start) or a D/L
-// stretch's last 0xFF head.  Each tile publishes the state at its end in
-// tstate[tau] ([63:62] flag, [33:32] group, [31:0] value):
-//   LOCAL  value known: Z -> (tile end - run start) mod 256; D/L -> distance
-//          from the tile end back to the last head (0 = no D yet); M -> none;
-//   PASS   the whole tile continues one run and maps the state through
-//          unchanged (zero run: 8192 is a multiple of 256) or, all-D, to
-//          min(dist, 256) -- republished as LOCAL once resolved.
-// A continued tile resolves its entry state by a look-back to the nearest
-// LOCAL (tile 0 of every piece is LOCAL), the pattern of lb_resolve.
-constexpr uint64_t kStLocal = 1ull << 62, kStPass = 2ull << 62;
-constexpr int kNoHead = -(1 << 28);
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-// first D word at or after x (< W) from the D ballots of pass 1 (mks[2q+1]
-// is the D mask of 64-word step q); W if none
-__device__ int enc_first_d(const uint64_t *mks, int x, int W) {
-  if (x >= W) return W;
-  int q = x >> 6;
-  uint64_t m = mks[2 * q + 1] & (~0ull << (x & 63));
-  while (!m) {
-    ++q;
-    if (q * 64 >= W) return W;
-    m = mks[2 * q + 1];
-  }
-  return min(q * 64 + __builtin_ctzll(m), W);
-}
-// walk the head chain from the first D >= x; distance from W back to the
-// last head, 0 if there is none
-__device__ int enc_chain_dist(const uint64_t *mks, int x, int W) {
-  int last = -1;
-  int h = enc_first_d(mks, x, W);
-  while (h < W) {
-    last = h;
-    h = enc_first_d(mks, h + 256, W);
-  }
-  return last >= 0 ? W - last : 0;
-}
-// Exit state of a full tile from its final run (start sF, -1 if the run
-// covers the whole tile; group gF) or 0 when it needs the entry state (a
-// tile-long D/L stretch with L words).  mks: per 64-word step {S, D} masks.
-__device__ uint64_t tile_exit_state(const uint64_t *mks, int W, int gF, int sF, bool allD) {
-  if (gF == 2) return kStLocal | (2ull << 32);
-  if (sF >= 0)
-    return kStLocal | ((uint64_t)gF << 32) |
-           (gF == 0 ? (uint64_t)((-sF) & 255) : (uint64_t)enc_chain_dist(mks, sF, W));
-  if (gF == 0) return kStPass;
-  if (allD) return kStPass | (1ull << 32);
-  return 0;
-}
-// Entry state by look-back over tstate (all 64 lanes of one wave): the
-// nearest LOCAL state before tau, PASS tiles composed on the way.  Returns
-// the Z phase (g0 == 0) or the D/L head distance (0 = none yet).
-__device__ uint32_t tile_entry_state(uint64_t *tstate, uint32_t tau, int g0) {
-  const int lane = lane_id();
-  int64_t top = (int64_t)tau - 1;
-  bool sawD = false;
-  uint64_t val = 0;
-  uint32_t spins = 0;
-  for (;;) {
-    const int64_t idx = top - lane;
-    const uint64_t v = idx >= 0 ? ld_status(&tstate[idx]) : kStLocal;
-    const uint64_t loc = __ballot((v >> 62) == 1);
-    const int first = loc ? __builtin_ctzll(loc) : 64;
-    const uint64_t rel = first >= 63 ? ~0ull : ((2ull << first) - 1);
-    if (__ballot((v >> 62) == 0) & rel) {
-      if (++spins > (1u << 24)) break;  // cannot happen with in-order tickets
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    sawD = sawD || __ballot(lane < first && ((v >> 32) & 1)) != 0;
-    if (first < 64) {
-      val = readlane64(v, first);
-      break;
-    }
-    top -= 64;
-  }
-  uint32_t x = (uint32_t)val;
-  if (g0 == 0) return x & 255;
-  if (sawD) x = (x == 0 || x > 256) ? 256u : x;
-  return x;
-}
-
-// wave 0, all lanes: publish this tile's exit state, resolve its entry state
-// into scr[69..71]
-__device__ void enc_tile_state(const uint64_t *mks, int *scr, uint64_t *tstate, uint32_t tau,
-                               int j, int W, bool lastTile, int g0, int gm1) {
-  const int lane = lane_id();
-  int sF = -1;
-  bool allD = true;
-  for (int q = 0; q < kEncWaves; ++q) {
-    sF = max(sF, scr[q]);
-    allD = allD && scr[76 + q] != 0;
-  }
-  uint64_t outv = 0;
-  if (!lastTile) {
-    outv = tile_exit_state(mks, W, scr[72], sF, allD);
-    if (outv && lane == 0) st_status(&tstate[tau], outv);
-  }
-  int rsIn = -1, hlIn = kNoHead, cont = 0;
-  if (j > 0 && W > 0 && g0 == gm1) {
-    cont = g0 + 1;
-    if (g0 != 2) {
-      const uint32_t x = tile_entry_state(tstate, tau, g0);
-      if (g0 == 0) {
-        rsIn = -(int)x;
-        if (!lastTile && outv == kStPass && lane == 0) st_status(&tstate[tau], kStLocal | (uint64_t)x);
-      } else {
-        rsIn = -kTileWords;  // forces the chain walk for the continued stretch
-        hlIn = x ? -(int)x : kNoHead;
-        if (!lastTile && (outv >> 62) == 2 && lane == 0)
-          st_status(&tstate[tau], kStLocal | (1ull << 32) | (uint64_t)((x == 0 || x > 256) ? 256u : x));
-      }
-    }
-  }
-  if (!lastTile && !outv) {
-    // one D/L stretch over the whole tile, with L words: its chain goes on
-    // from the entry head
-    outv = kStLocal | (1ull << 32) | (uint64_t)enc_chain_dist(mks, max(hlIn + 256, 0), W);
-    if (lane == 0) st_status(&tstate[tau], outv);
-  }
-  if (lane == 0) {
-    scr[69] = rsIn;
-    scr[70] = hlIn;
-    scr[71] = cont;
-  }
-}
-
-// info word per (step, lane): [7:0] nonzero mask, [9:8] group,
-// [10] member, [11] zero-run head, [15:12] bytes, [23:16] run count,
-// [24] word of a D/L stretch longer than 256 words (chain walk decides)
-template <bool kTiled>
-__global__ __launch_bounds__(kEncThreads, CPK_ENC_WPE) void encode_kernel(
-    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
-    uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status,
-    uint32_t *ticket, const uint32_t *__restrict__ tmap, const uint64_t *__restrict__ toff,
-    uint64_t *tstate, uint32_t *err) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t *stage = smem;
-  uint32_t *stage32 = reinterpret_cast<uint32_t *>(smem);
-  uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kEncLut);
-  uint32_t *dbits = reinterpret_cast<uint32_t *>(smem + kEncDbits);
-  uint32_t *hbits = reinterpret_cast<uint32_t *>(smem + kEncHbits);
-  int *scr = reinterpret_cast<int *>(smem + kEncScr);
-  uint64_t *mks = reinterpret_cast<uint64_t *>(smem + kEncMasks);
-  // scr[0..15] last run start per wave, [16..31] first run start,
-  // [32..47] last D, [48..63] bytes per wave, [64..65] ticket, [66..67] base,
-  // tiled only: [68] run end after the tile, [69] run start entering it,
-  // [70] last 0xFF head entering it, [71] continued group + 1, [72] group of
-  // the tile's last word, [76..91] all-D flag per wave
-
-  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
-  fill_luts(lut, false);
-  PH_INIT(scr)
-
-  // tiled: work item = tile tau of T (pieces cut into 8192-word tiles, in
-  // stream order); otherwise work item = piece
-  const uint32_t T = kTiled ? (uint32_t)toff[n] : n;
-  for (uint32_t it = 0;; ++it) {
-    if (tid == 0) scr[64 + (it & 1)] = (int)atomicAdd(ticket, 1u);
-    __syncthreads();  // also orders the previous piece's LDS use
-    const uint32_t tau = (uint32_t)__builtin_amdgcn_readfirstlane(scr[64 + (it & 1)]);
-    if (tau >= T) break;
-    PH(0)
-    uint32_t seg = tau;
-    int j = 0;             // tile index within the piece
-    bool lastTile = true;  // no tile of this piece follows
-    uint64_t w0, rest = 0;  // rest: words of the piece after this tile
-    int W;
-    if (kTiled) {
-      seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)tmap[tau]);
-      j = (int)(tau - (uint32_t)toff[seg]);
-      const uint64_t p0 = swo[seg], pw = swo[seg + 1] - p0, tb = (uint64_t)j * kTileWords;
-      const uint64_t rem = pw - tb;
-      w0 = p0 + tb;
-      W = rem < (uint64_t)kTileWords ? (int)rem : kTileWords;
-      lastTile = rem <= (uint64_t)kTileWords;
-      rest = rem - (uint64_t)W;
-    } else {
-      w0 = swo[seg];
-      const uint64_t pw = swo[seg + 1] - w0;
-      if (pw > (uint64_t)kTileWords) {  // max_seg_words hint was wrong
-        if (tid == 0) atomicOr(err, 1u);
-      }
-      W = pw > (uint64_t)kTileWords ? kTileWords : (int)pw;
-    }
-    // per-piece opaque copies of this wave's / lane's first word: keep hipcc
-    // from hoisting ~100 per-lane addresses out of the persistent loop
-    int wb = __builtin_amdgcn_readfirstlane(w * (kSteps * 64));  // first word of this wave
-    asm volatile("" : "+s"(wb));
-    int k0 = wb + lane;
-    asm volatile("" : "+v"(k0));
-
-    // ---- pass 1: load, classify, run-start and D masks --------------------
-    uint32_t info[kSteps];
-    // run-start / D ballots of each step live in LDS (wave-private rows):
-    // kept in SGPRs they spilled.
-    uint64_t *mrow = mks + (wb >> 9) * (2 * kSteps);
-#define SMASK(s) mrow[2 * (s)]
-#define DMASK(s) mrow[2 * (s) + 1]
-    const uint64_t *src = in + w0;
-    // all 8 loads in flight at once (clamped, not predicated: no branches)
-    uint64_t wv[kSteps];
-    {
-      const int kl = max(W - 1, 0);
-#pragma unroll
-      for (int s = 0; s < kSteps; ++s) wv[s] = W ? src[min(k0 + s * 64, kl)] : 0ull;
-    }
-    int gprev = 3;  // group of word wb - 1 (3 = none: a run starts at word 0)
-    if (lane == 0 && (w > 0 ? wb - 1 < W : j > 0)) {
-      uint64_t v = src[wb - 1];
-      gprev = grp_of(word_mask((uint32_t)v, (uint32_t)(v >> 32)));
-    }
-    gprev = readlane(gprev, 0);
-    const int gm1 = gprev;  // wave 0: group of the word before the tile
-    bool allD = true;
-#pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-      const int k = k0 + s * 64;
-      const uint64_t v = k < W ? wv[s] : 0ull;
-      const uint32_t m = word_mask((uint32_t)v, (uint32_t)(v >> 32));
-      const int g = k < W ? grp_of(m) : 3;
-      const int gp = wave_shr1(g, gprev);
-      const uint64_t sb = __ballot(g != 3 && g != gp);
-      const uint64_t db = __ballot(k < W && m == 0xffu);
-      allD = allD && db == ~0ull;
-      if (lane == 0) {
-        SMASK(s) = sb;
-        DMASK(s) = db;
-      }
-      gprev = readlane(g, 63);
-      info[s] = m | ((uint32_t)g << 8);
-    }
-    {
-      int ls = -kBig, fs = kBig, ld = -1;  // -kBig: no start (below any carried start)
-#pragma unroll
-      for (int s = 0; s < kSteps; ++s) {
-        const uint64_t sb = SMASK(s), db = DMASK(s);
-        if (sb) {
-          ls = wb + s * 64 + hi_bit(sb);
-          if (fs == kBig) fs = wb + s * 64 + lo_bit(sb);
-        }
-        if (db) ld = wb + s * 64 + hi_bit(db);
-      }
-      if (lane == 0) {
-        scr[w] = ls;
-        scr[16 + w] = fs;
-        scr[32 + w] = ld;
-        if (kTiled) scr[76 + w] = allD;
-      }
-    }
-    if (kTiled && w == kEncWaves - 1) {
-      // run end after the tile (looked up to 256 words ahead: counts cap at
-      // 255, stretches longer than 256 words take the chain walk anyway)
-      int look = W;
-      if (!lastTile) {
-        uint64_t v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint64_t p = (uint64_t)(64 * r + lane);
-          v[r] = p < rest ? src[W + 64 * r + lane] : 0ull;
-        }
-        int gp = gprev;  // group of word W - 1
-        look = W + 256;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int g = (uint64_t)(64 * r + lane) < rest
-                            ? grp_of(word_mask((uint32_t)v[r], (uint32_t)(v[r] >> 32)))
-                            : 3;
-          const uint64_t b = __ballot(g != wave_shr1(g, gp));
-          if (b && look == W + 256) look = W + 64 * r + lo_bit(b);
-          gp = readlane(g, 63);
-        }
-      }
-      if (lane == 0) {
-        scr[68] = look;
-        scr[72] = gprev;
-      }
-    }
-    __syncthreads();
-    if (kTiled) {
-      if (w == 0) enc_tile_state(mks, scr, tstate, tau, j, W, lastTile, readlane((int)info[0], 0) >> 8 & 3, gm1);
-      __syncthreads();
-    }
-    PH(1)
-    // carries across waves: run start / last D entering this wave, first
-    // run start after it
-    int cS = kTiled ? scr[69] : -1, cD = -1, eOut = kTiled ? scr[68] : W;
-    for (int q = 0; q < w; ++q) {
-      cS = max(cS, scr[q]);
-      cD = max(cD, scr[32 + q]);
-    }
-    for (int q = kEncWaves - 1; q > w; --q) eOut = scr[16 + q] < kBig ? min(eOut, scr[16 + q]) : eOut;
-    // first run start in steps after s (within the wave), else eOut
-    int nextS[kSteps];
-    {
-      int r = eOut;
-#pragma unroll
-      for (int s = kSteps - 1; s >= 0; --s) {
-        nextS[s] = r;
-        const uint64_t sb = SMASK(s);
-        if (sb) r = wb + s * 64 + lo_bit(sb);
-      }
-    }
-
-    // ---- pass 2: roles (PackedOutputStream.java:119-193 restated per word) --
-    const uint64_t le = lanemask_le();
-    int anyLong = 0;
-#pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-      const int k = k0 + s * 64;
-      const int base = wb + s * 64;
-      const uint32_t m = info[s] & 0xffu;
-      const int g = (int)((info[s] >> 8) & 3);
-      const uint64_t smask_s = SMASK(s), dmask_s = DMASK(s);
-      const uint64_t sm = smask_s & le;
-      const int rs = sm ? base + hi_bit(sm) : cS;          // run start s(k)
-      const uint64_t sg = smask_s & ~le;
-      const int re = sg ? base + lo_bit(sg) : nextS[s];    // run end e(k)
-      const uint64_t dm = dmask_s & (le >> 1);             // D words before k
-      const int rd = dm ? base + hi_bit(dm) : cD;          // last D before k
-      uint32_t x = info[s];
-      int nb = 0;
-      if (g == 0) {
-        // every 256th word of a zero run is a 0x00 head (the 255 cap, :125-127)
-        if (((k - rs) & 255) == 0) {
-          x |= 1u << 11;
-          nb = 2;
-        }
-      } else if (g == 1) {
-        if (re - rs > 256) {
-          anyLong = 1;  // resolved by the chain walk below
-          x |= 1u << 24;  // long-stretch word
-          nb = 8;       // provisional: L words are 8 either way, D fixed below
-        } else if (rd >= rs) {
-          x |= 1u << 10;  // inside the 0xFF run of the stretch's first D
-          nb = 8;
-        } else {
-          nb = m == 0xffu ? 10 : 8;
-        }
-      } else if (g == 2) {
-        nb = 1 + __builtin_popcount(m);
-      }
-      const uint32_t cnt = (uint32_t)min(255, max(re - k - 1, 0));
-      info[s] = (x & 0x10007ffu) | ((uint32_t)nb << 12) | (cnt << 16);
-      if (smask_s) cS = base + hi_bit(smask_s);
-      if (dmask_s) cD = base + hi_bit(dmask_s);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    PH(2)
-    if (__syncthreads_or(anyLong)) {
-      // D/L stretch longer than 256 words: heads chain h1 = first D,
-      // h' = first D at or after h + 256 (PackedOutputStream.java:145-161).
-      if (tid < 256) dbits[tid] = 0;
-      else if (tid < 512) hbits[tid - 256] = 0;
-      __syncthreads();
-      // bitmaps are built from the ballots: lane 0 / 1 write 32-bit halves
-#pragma unroll
-      for (int s = 0; s < kSteps; ++s) {
-        const int dw = (wb + s * 64) >> 5;
-        if (lane == 0) {
-          dbits[dw] = (uint32_t)DMASK(s);
-          // a stretch continued from the previous tile: a start marker at 0
-          hbits[dw] = (uint32_t)SMASK(s) | (kTiled && dw == 0 && scr[71] == 2 ? 1u : 0u);
-        } else if (lane == 1) {
-          dbits[dw + 1] = (uint32_t)(DMASK(s) >> 32);
-          hbits[dw + 1] = (uint32_t)(SMASK(s) >> 32);
-        }
-      }
-      __syncthreads();
-      // run start of every long-stretch word, then clear hbits for heads
-      int sl[kSteps];
-#pragma unroll
-      for (int s = 0; s < kSteps; ++s) {
-        sl[s] = 0;
-        const int k = k0 + s * 64;
-        if ((info[s] >> 24) & 1) {
-          int d = k >> 5;
-          uint32_t mm = hbits[d] & ((k & 31) == 31 ? ~0u : ((2u << (k & 31)) - 1));
-          while (!mm) mm = hbits[--d];
-          sl[s] = d * 32 + 31 - __builtin_clz(mm);
-          if (kTiled && sl[s] == 0 && scr[71] == 2) sl[s] = -kTileWords;  // continued stretch
-        }
-      }
-      __syncthreads();
-      if (tid < 256) hbits[tid] = 0;
-      __syncthreads();
-      // walkers: the first word of each long stretch
-#pragma unroll
-      for (int s = 0; s < kSteps; ++s) {
-        const int k = k0 + s * 64;
-        const int base = wb + s * 64;
-        const uint64_t sg = SMASK(s) & ~lanemask_le();
-        const int re = sg ? base + lo_bit(sg) : nextS[s];
-        const bool st = (SMASK(s) >> lane) & 1;
-        if (st && ((info[s] >> 8) & 3) == 1 && re - k > 256) {
-          const int rw = min(re, W);
-          int h = bm_next(dbits, k, rw);
-          while (h < rw) {
-            atomicOr(&hbits[h >> 5], 1u << (h & 31));
-            const int p = h + 256;
-            if (p >= rw) break;
-            h = bm_next(dbits, p, rw);
-          }
-        }
-      }
-      if (kTiled && tid == 0 && scr[71] == 2) {
-        // the continued stretch: its chain goes on from the last head of the
-        // previous tile, h' = first D >= h + 256 (PackedOutputStream.java:145-161)
-        int rw = scr[68];
-        for (int q = 0; q < kEncWaves; ++q) rw = scr[16 + q] < kBig ? min(rw, scr[16 + q]) : rw;
-        rw = min(rw, W);
-        int h = bm_next(dbits, max(scr[70] + 256, 0), rw);
-        while (h < rw) {
-          atomicOr(&hbits[h >> 5], 1u << (h & 31));
-          const int p = h + 256;
-          if (p >= rw) break;
-          h = bm_next(dbits, p, rw);
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < kSteps; ++s) {
-        const int k = k0 + s * 64;
-        const uint32_t m = info[s] & 0xffu;
-        if ((info[s] >> 24) & 1) {
-          // member iff a head of its stretch lies in [k - 255, k - 1]
-          bool mem = bm_any(hbits, max(max(sl[s], k - 255), 0), k - 1);
-          if (kTiled && sl[s] < 0) mem = mem || k - 255 <= scr[70];
-          const int nb = mem ? 8 : (m == 0xffu ? 10 : 8);
-          info[s] = (info[s] & ~(0xfu << 12)) | ((uint32_t)nb << 12) | (mem ? (1u << 10) : 0u);
-        }
-      }
-    }
-    PH(3)
-
-    // ---- bytes per wave -> piece offsets -----------------------------------
-    {
-      int tot = 0;
-#pragma unroll
-      for (int s = 0; s < kSteps; ++s) {
-        const uint32_t nb = (info[s] >> 12) & 15u;
-        tot += __popcll(__ballot(nb & 1)) + 2 * __popcll(__ballot(nb & 2)) +
-               4 * __popcll(__ballot(nb & 4)) + 8 * __popcll(__ballot(nb & 8));
-      }
-      if (lane == 0) scr[48 + w] = tot;
-    }
-    __syncthreads();
-    int wbytes = 0, total = 0;
-    for (int q = 0; q < kEncWaves; ++q) {
-      const int t = scr[48 + q];
-      if (q < w) wbytes += t;
-      total += t;
-    }
-    // publish the aggregate now; the prefix is resolved after compaction
-    if (tid == 0) lb_publish(status, tau, (uint64_t)total);
-    // zero the staging lines this piece uses (the strings are OR-ed in)
-    {
-      const int nl = (total + 19) >> 4;
-      uint4 z = {0u, 0u, 0u, 0u};
-      for (int c = tid; c < nl; c += kEncThreads) reinterpret_cast<uint4 *>(stage)[c] = z;
-    }
-    __syncthreads();
-    PH(4)
-
-    // ---- pass 3: packed strings into LDS ------------------------------------
-#pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-      const uint32_t x = info[s];
-      const uint32_t nb = (x >> 12) & 15u;
-      const uint64_t b0 = __ballot(nb & 1), b1 = __ballot(nb & 2), b2 = __ballot(nb & 4),
-                     b3 = __ballot(nb & 8);
-      const int o = wbytes + mbcnt(b0) + 2 * mbcnt(b1) + 4 * mbcnt(b2) + 8 * mbcnt(b3);
-      wbytes += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) + 8 * __popcll(b3);
-      if (nb == 0) continue;
-      // the words are re-read here (L2 / Infinity-Cache hit) instead of being
-      // held in 16 VGPRs across the passes: 2 workgroups per CU instead of 1
-      const uint64_t v = src[k0 + s * 64];
-      const uint32_t l = (uint32_t)v, h = (uint32_t)(v >> 32), m = x & 0xffu;
-      uint32_t d0, d1, d2;
-      if (x & (1u << 10)) {  // literal-run member: 8 bytes verbatim
-        d0 = l;
-        d1 = h;
-        d2 = 0;
-      } else {  // tag + nonzero bytes (+ count after 0x00 / 0xFF tags)
-        const uint64_t sel = lut[m];
-        const uint32_t c0 = __builtin_amdgcn_perm(h, l, (uint32_t)sel);
-        const uint32_t c1 = __builtin_amdgcn_perm(h, l, (uint32_t)(sel >> 32));
-        const uint32_t cnt = (x >> 16) & 0xffu;
-        d0 = m | (c0 << 8);
-        d1 = (c0 >> 24) | (c1 << 8);
-        d2 = c1 >> 24;
-        if (m == 0) d0 |= cnt << 8;
-        else if (m == 0xffu) d2 |= cnt << 8;
-      }
-      // place bytes [o, o + nb): dword-shift the 3-dword string
-      const uint32_t sh = (uint32_t)(o & 3) * 8u;
-      const uint64_t s01 = (uint64_t)d0 | ((uint64_t)d1 << 32);
-      const uint64_t lo64 = s01 << sh;
-      const uint64_t hi64 = ((uint64_t)d2 << sh) | (sh ? (s01 >> (64 - sh)) : 0ull);
-      uint32_t *dst = stage32 + (o >> 2);
-      // four unconditional ORs into the zeroed stage (the bytes past the
-      // string are zero): no exec-mask branches around the LDS ops
-      atomicOr(&dst[0], (uint32_t)lo64);
-      atomicOr(&dst[1], (uint32_t)(lo64 >> 32));
-      atomicOr(&dst[2], (uint32_t)hi64);
-      atomicOr(&dst[3], (uint32_t)(hi64 >> 32));
-      __builtin_amdgcn_sched_barrier(0);  // one step at a time: bounds VGPRs
-    }
-    PH(5)
-
-    // ---- decoupled look-back (wave 0), overlapped with the compaction -----
-    if (w == 0) {
-      uint64_t b = lb_resolve(status, tau, (uint64_t)total);
-      if (lane == 0) {
-        *reinterpret_cast<uint64_t *>(&scr[66]) = b;
-        if (j == 0) out_off[seg] = b;
-        if (tau == T - 1) out_off[n] = b + (uint64_t)total;
-      }
-    }
-    __syncthreads();
-    PH(6)
-    // ---- store: 16-byte lines, byte stores at the two shared edges --------
-    // staged byte x is global byte base + x; line L covers global
-    // [A + 16L, A + 16L + 16), A = base & ~15, i.e. staged x = 16L - pad.
-    {
-      const uint64_t base = *reinterpret_cast<uint64_t *>(&scr[66]);
-      const int pad = (int)(base & 15);
-      const int tb = pad + total;
-      uint8_t *gbase = out + (base - (uint64_t)pad);
-      const int nl = (tb + 15) >> 4;
-      const uint32_t sh = (uint32_t)((16 - pad) & 3);  // (16L - pad) & 3
-      for (int c = tid; c < nl; c += kEncThreads) {
-        const int lo16 = c * 16, hi16 = lo16 + 16;
-        if (lo16 >= pad && hi16 <= tb) {
-          const uint32_t *a = stage32 + ((lo16 - pad) >> 2);
-          uint32_t e0 = a[0], e1 = a[1], e2 = a[2], e3 = a[3], e4 = sh ? a[4] : 0u;
-          uint4 v;
-          v.x = __builtin_amdgcn_alignbyte(e1, e0, sh);
-          v.y = __builtin_amdgcn_alignbyte(e2, e1, sh);
-          v.z = __builtin_amdgcn_alignbyte(e3, e2, sh);
-          v.w = __builtin_amdgcn_alignbyte(e4, e3, sh);
-          *reinterpret_cast<uint4 *>(gbase + lo16) = v;
-        } else {
-          const int bb0 = max(lo16, pad), bb1 = min(hi16, tb);
-          for (int b = bb0; b < bb1; ++b) gbase[b] = stage[b - pad];
-        }
-      }
-    }
-    PH(7)
-#undef SMASK
-#undef DMASK
-  }
-  PH_FLUSH(0)
-}
-
-// ------------------------------------------------------------ encoder v2
-// Wave-per-tile encoder: no workgroup barriers.  A wave takes the next tile
-// (1024 words of a piece, in stream order) from an ordered ticket and
-//   1. loads its words (one per lane per 64-word step) and classifies them:
-//      nonzero-byte mask, group, run-start / D ballots (a wave-private LDS
-//      row per step), plus a 256-word look-ahead for the end of the run
-//      crossing the tile end;
-//   2. publishes its exit run state (tile_exit_state) and, when its first
-//      run continues the previous tile's, resolves its entry state;
-//   3. walks the 16 steps in order with wave-uniform carries -- run start,
-//      last D, last 0xFF head of the current stretch -- and gives every word
-//      its role (PackedOutputStream.java:64-193 restated per word, see
-//      DESIGN.md): within one 64-word step a stretch that continues from
-//      before has at most one new head (heads are >= 256 words apart) and a
-//      stretch that starts in the step has its first D as head;
-//   4. publishes its packed size and resolves its output offset by
-//      decoupled look-back;
-//   5. builds each word's packed string (tag + v_perm-compacted bytes +
-//      count), ORs it into a 1 KiB wave-private LDS ring at its output
-//      offset, and streams complete 16-byte lines to memory; only the lines
-//      shared with the neighbouring tiles take byte stores.
-// Per-word state lives in LDS between the passes (rolled loops keep the
-// registers at <= 64 per lane).
-constexpr int kE2Words = 1024;                 // words per tile (multiple of 256)
-constexpr int kE2Steps = kE2Words / 64;        // 16
-constexpr int kE2Threads = 256;                // 4 independent waves
-constexpr uint32_t kE2Ring = 1024;             // output ring per wave (bytes)
-constexpr uint32_t kE2Info = kE2Ring;                      // u32[16][64] per-word roles
-constexpr uint32_t kE2Mks = kE2Info + kE2Words * 4;        // u64[16][2] {S, D}
-constexpr uint32_t kE2Nxs = kE2Mks + kE2Steps * 16;        // int[16] first start after step
-constexpr uint32_t kE2WaveLds = kE2Nxs + kE2Steps * 4;     // 5,440
-constexpr uint32_t kE2Lds = 2048 + 4 * kE2WaveLds;         // 23,808 B
-#ifndef CPK_E2_WPE
-#define CPK_E2_WPE 6  // LDS (23.8 KB per workgroup) allows 6 workgroups per CU
-#endif
-
-// stores bytes [lo, hi) of global line L from the ring, then clears them
-__device__ __forceinline__ void e2_store_partial(uint8_t *out, uint8_t *ring, uint64_t L, int lo,
-                                                 int hi) {
-  const int lane = lane_id();
-  if (lane >= lo && lane < hi) {
-    const uint32_t rp = (uint32_t)((L * 16 + lane) & (kE2Ring - 1));
-    out[L * 16 + lane] = ring[rp];
-    ring[rp] = 0;
-  }
-}
-
-__global__ __launch_bounds__(kE2Threads, CPK_E2_WPE) void encode2_kernel(
-    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
-    uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status,
-    uint32_t *ticket, const uint32_t *__restrict__ tmap, const uint64_t *__restrict__ toff,
-    uint64_t *tstate) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint64_t *lut = reinterpret_cast<uint64_t *>(smem);
-  const int lane = lane_id(), w = wave_id();
-  uint8_t *wl = smem + 2048 + w * kE2WaveLds;
-  uint8_t *ring = wl;
-  uint32_t *ring32 = reinterpret_cast<uint32_t *>(ring);
-  uint32_t *inf = reinterpret_cast<uint32_t *>(wl + kE2Info);  // [s * 64 + lane]
-  uint64_t *mks = reinterpret_cast<uint64_t *>(wl + kE2Mks);   // [2s] S, [2s+1] D
-  int *nxs = reinterpret_cast<int *>(wl + kE2Nxs);
-  fill_luts(lut, false);
-  for (int i = lane; i < (int)(kE2Ring / 16); i += 64)
-    reinterpret_cast<uint4 *>(ring)[i] = uint4{0u, 0u, 0u, 0u};
-  __syncthreads();  // the only block-wide barrier: LUT ready
-  const uint32_t T = (uint32_t)toff[n];
-  // ordered tickets; the next one is requested while the current tile runs
-  uint32_t tnext = take_ordered(ticket);
-  WPH_INIT
-  for (;;) {
-    const uint32_t tau = tnext;
-    if (tau >= T) break;
-    tnext = take_ordered(ticket);
-    const uint32_t seg = (uint32_t)__builtin_amdgcn_readfirstlane((int)tmap[tau]);
-    const int j = (int)(tau - (uint32_t)toff[seg]);
-    const uint64_t p0 = swo[seg], pw = swo[seg + 1] - p0;
-    const uint64_t tb = (uint64_t)j * kE2Words, rem = pw - tb;
-    const int W = rem < (uint64_t)kE2Words ? (int)rem : kE2Words;
-    const bool lastTile = rem <= (uint64_t)kE2Words;
-    const int rl = (int)min(rem - (uint64_t)W, (uint64_t)256);  // look-ahead words
-    const uint64_t *src = in + p0 + tb;
-    int k0 = lane;
-    asm volatile("" : "+v"(k0));  // keep per-lane addresses out of the loop head
-    const int kl = max(W - 1, 0);
-    WPH(0)
-
-    // ---- 1: loads, classes, ballots ----------------------------------------
-    int gm1 = 3;  // group of the word before the tile (3: none)
-    if (j > 0) {
-      const uint64_t v = src[-1];
-      gm1 = grp_of(word_mask((uint32_t)v, (uint32_t)(v >> 32)));
-    }
-    int gprev = gm1, sF = -1;
-    bool allD = true;
-    {
-      uint64_t wv[kE2Steps];
-#pragma unroll
-      for (int s = 0; s < kE2Steps; ++s) wv[s] = W ? src[min(k0 + 64 * s, kl)] : 0ull;
-#pragma unroll
-      for (int s = 0; s < kE2Steps; ++s) {
-        const int k = k0 + 64 * s;
-        const uint64_t v = k < W ? wv[s] : 0ull;
-        const uint32_t m = word_mask((uint32_t)v, (uint32_t)(v >> 32));
-        const int g = k < W ? grp_of(m) : 3;
-        const uint64_t S = __ballot(g != 3 && g != wave_shr1(g, gprev));
-        const uint64_t D = __ballot(k < W && m == 0xffu);
-        if (lane == 0) {
-          mks[2 * s] = S;
-          mks[2 * s + 1] = D;
-        }
-        allD = allD && D == ~0ull;
-        if (S) sF = 64 * s + hi_bit(S);
-        gprev = readlane(g, 63);
-        inf[64 * s + lane] = m | ((uint32_t)g << 8);
-      }
-    }
-    const int gF = gprev;  // group of word 1023 (full tiles)
-    int look = W;          // first run start after the tile, capped 256 on
-    if (!lastTile) {
-      uint64_t la[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) la[r] = src[W + min(64 * r + k0, rl - 1)];
-      look = W + 256;
-      int gp = gprev;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int g = 64 * r + lane < rl ? grp_of(word_mask((uint32_t)la[r], (uint32_t)(la[r] >> 32))) : 3;
-        const uint64_t b = __ballot(g != wave_shr1(g, gp));
-        if (b && look == W + 256) look = W + 64 * r + lo_bit(b);
-        gp = readlane(g, 63);
-      }
-    }
-    wave_lds_sync();
-    // nxs[s] := first run start after step s
-    if (lane == 0) {
-      int r = look;
-      for (int s = kE2Steps - 1; s >= 0; --s) {
-        nxs[s] = r;
-        const uint64_t S = mks[2 * s];
-        if (S) r = 64 * s + lo_bit(S);
-      }
-    }
-
-    // ---- 2: exit state out, entry state in ----------------------------------
-    WPH(1)
-    uint64_t outv = 0;
-    if (!lastTile) {
-      outv = tile_exit_state(mks, W, gF, sF, allD);
-      if (outv && lane == 0) st_status(&tstate[tau], outv);
-    }
-    const int g0 = __builtin_amdgcn_readfirstlane((int)inf[0]) >> 8 & 3;
-    const bool cont = j > 0 && W > 0 && g0 == gm1;
-    int rsC = 0, hC = kNoHead;  // run start / last 0xFF head before the step
-    if (cont && g0 != 2) {
-      const uint32_t x = tile_entry_state(tstate, tau, g0);
-      if (g0 == 0) {
-        rsC = -(int)x;
-        if (!lastTile && outv == kStPass && lane == 0) st_status(&tstate[tau], kStLocal | (uint64_t)x);
-      } else {
-        hC = x ? -(int)x : kNoHead;
-        if (!lastTile && (outv >> 62) == 2 && lane == 0)
-          st_status(&tstate[tau], kStLocal | (1ull << 32) | (uint64_t)((x == 0 || x > 256) ? 256u : x));
-      }
-    }
-    if (!lastTile && !outv) {
-      outv = kStLocal | (1ull << 32) | (uint64_t)enc_chain_dist(mks, max(hC + 256, 0), W);
-      if (lane == 0) st_status(&tstate[tau], outv);
-    }
-    wave_lds_sync();
-
-    // ---- 3: roles (PackedOutputStream.java:64-193 per word) -----------------
-    WPH(2)
-    const uint64_t le = lanemask_le(), lt = le >> 1;
-    int gC = gm1, rdC = -kBig, total = 0;
-#pragma unroll 1
-    for (int s = 0; s < kE2Steps; ++s) {
-      const int base = 64 * s;
-      const int k = k0 + base;
-      const uint64_t S = mks[2 * s], D = mks[2 * s + 1];
-      const int nx = nxs[s];
-      const uint32_t x = inf[base + lane];
-      const uint32_t m = x & 0xffu;
-      const int g = (int)((x >> 8) & 3);
-      const int fst = S ? lo_bit(S) : 64;  // first run start in the step
-      // the D/L stretch continuing into the step: its new head, if any, is
-      // the first D at or after hC + 256 before the step's first run start
-      int hNew = kNoHead;
-      if (gC == 1 && fst > 0) {
-        const int t0 = hC == kNoHead ? 0 : max(hC + 256 - base, 0);
-        if (t0 < fst) {
-          const uint64_t sg = (fst == 64 ? ~0ull : ((1ull << fst) - 1)) & (~0ull << t0);
-          const uint64_t c = D & sg;
-          if (c) hNew = base + lo_bit(c);
-        }
-      }
-      const uint64_t sle = S & le, sgt = S & ~le, dlt = D & lt;
-      const int rs = sle ? base + hi_bit(sle) : rsC;
-      const int re = sgt ? base + lo_bit(sgt) : nx;
-      const int rd = dlt ? base + hi_bit(dlt) : rdC;
-      uint32_t flags = 0;
-      int nb = 0;
-      if (g == 0) {
-        // a 0x00 head every 256 words of a zero run (the 255 cap, :119-131)
-        if (((k - rs) & 255) == 0) {
-          flags = 1u << 11;
-          nb = 2;
-        }
-      } else if (g == 1) {
-        bool mem;
-        if (lane < fst) {  // stretch continuing from before the step
-          mem = k != hNew && ((hC != kNoHead && k <= hC + 255) || (hNew != kNoHead && k > hNew));
-        } else {           // stretch started in this step: its first D heads
-          mem = rd >= rs;
-        }
-        flags = mem ? (1u << 10) : 0u;
-        nb = mem ? 8 : (m == 0xffu ? 10 : 8);
-      } else if (g == 2) {
-        nb = 1 + __builtin_popcount(m);
-      }
-      const uint32_t cnt = (uint32_t)min(255, max(re - k - 1, 0));
-      inf[base + lane] = m | flags | ((uint32_t)nb << 12) | (cnt << 16);
-      total += __popcll(__ballot(nb & 1)) + 2 * __popcll(__ballot(nb & 2)) +
-               4 * __popcll(__ballot(nb & 4)) + 8 * __popcll(__ballot(nb & 8));
-      // carries into the next step
-      const int gL = readlane(g, 63);
-      if (gL == 1) {
-        if (S) {
-          const uint64_t dm = D & (~0ull << hi_bit(S));
-          hC = dm ? base + lo_bit(dm) : kNoHead;
-        } else if (hNew != kNoHead) {
-          hC = hNew;
-        }
-      } else {
-        hC = kNoHead;
-      }
-      if (S) rsC = base + hi_bit(S);
-      if (D) rdC = base + hi_bit(D);
-      gC = gL;
-    }
-
-    // ---- 4: output offset by look-back --------------------------------------
-    WPH(3)
-    if (lane == 0) lb_publish(status, tau, (uint64_t)total);
-    const uint64_t obase = lb_resolve(status, tau, (uint64_t)total);
-    if (lane == 0) {
-      if (j == 0) out_off[seg] = obase;
-      if (tau == T - 1) out_off[n] = obase + (uint64_t)total;
-    }
-    wave_lds_sync();
-
-    // ---- 5: strings -> LDS ring -> 16-byte lines ---------------------------
-    WPH(4)
-    const int pad = (int)(obase & 15);
-    const uint64_t L0 = obase >> 4;
-    uint64_t fl = (obase + 15) >> 4;  // next whole line to store
-    bool headDone = pad == 0;
-    int off = 0;
-    // the words again (L2 / Infinity-Cache hits: the tile was read moments
-    // ago), one step ahead
-    uint64_t vn = W ? src[min(k0, kl)] : 0ull;
-#pragma unroll 1
-    for (int s = 0; s < kE2Steps; ++s) {
-      const uint64_t v = vn;
-      if (s + 1 < kE2Steps) vn = W ? src[min(k0 + 64 * (s + 1), kl)] : 0ull;
-      const uint32_t x = inf[64 * s + lane];
-      const int nb = (int)((x >> 12) & 15u);
-      const int incl = wave_incl_add(nb);
-      const int o = off + incl - nb;
-      off += readlane(incl, 63);
-      if (nb) {
-        const uint32_t l = (uint32_t)v, h = (uint32_t)(v >> 32), m = x & 0xffu;
-        uint32_t d0, d1, d2;
-        if (x & (1u << 10)) {  // literal-run member: 8 bytes verbatim
-          d0 = l;
-          d1 = h;
-          d2 = 0;
-        } else {  // tag + nonzero bytes (+ count after 0x00 / 0xFF tags)
-          const uint64_t sel = lut[m];
-          const uint32_t c0 = __builtin_amdgcn_perm(h, l, (uint32_t)sel);
-          const uint32_t c1 = __builtin_amdgcn_perm(h, l, (uint32_t)(sel >> 32));
-          const uint32_t cnt = (x >> 16) & 0xffu;
-          d0 = m | (c0 << 8);
-          d1 = (c0 >> 24) | (c1 << 8);
-          d2 = c1 >> 24;
-          if (m == 0) d0 |= cnt << 8;
-          else if (m == 0xffu) d2 |= cnt << 8;
-        }
-        const uint32_t rp = (uint32_t)((obase + (uint64_t)o) & (kE2Ring - 1));
-        const uint32_t sh = (rp & 3) * 8u;
-        const uint64_t s01 = (uint64_t)d0 | ((uint64_t)d1 << 32);
-        const uint64_t lo64 = s01 << sh;
-        const uint64_t hi64 = ((uint64_t)d2 << sh) | (sh ? (s01 >> (64 - sh)) : 0ull);
-        const uint32_t q = rp >> 2;
-        const int end = (int)(rp & 3) + nb;
-        constexpr uint32_t kMask = kE2Ring / 4 - 1;
-        atomicOr(&ring32[q], (uint32_t)lo64);
-        if (end > 4) atomicOr(&ring32[(q + 1) & kMask], (uint32_t)(lo64 >> 32));
-        if (end > 8) atomicOr(&ring32[(q + 2) & kMask], (uint32_t)hi64);
-        if (end > 12) atomicOr(&ring32[(q + 3) & kMask], (uint32_t)(hi64 >> 32));
-      }
-      wave_lds_sync();
-      if (!headDone && off >= 16 - pad) {
-        e2_store_partial(out, ring, L0, pad, 16);
-        headDone = true;
-      }
-      const uint64_t le16 = (obase + (uint64_t)off) >> 4;  // lines below are complete
-      for (uint64_t L = fl + (uint64_t)lane; L < le16; L += 64) {
-        uint4 *rl4 = reinterpret_cast<uint4 *>(ring + ((L * 16) & (kE2Ring - 1)));
-        *reinterpret_cast<uint4 *>(out + L * 16) = *rl4;
-        *rl4 = uint4{0u, 0u, 0u, 0u};
-      }
-      if (le16 > fl) fl = le16;
-      wave_lds_sync();
-    }
-    // the tail line (shared with the next tile) and a head line never filled
-    const uint64_t done = obase + (uint64_t)total;
-    if (!headDone) {
-      if (total) e2_store_partial(out, ring, L0, pad, pad + total);
-    } else if (done & 15) {
-      e2_store_partial(out, ring, done >> 4, 0, (int)(done & 15));
-    }
-    wave_lds_sync();
-    WPH(5)
-  }
-  WPH_FLUSH(32)
-}
-
-// Tile plan for the tiled encoder: toff[i] = first tile of piece i (one tile
-// per 8192 words, at least one per piece), toff[n] = T, tmap[tau] = piece of
-// tile tau.  Single pass: 8192 pieces per workgroup, in ticket order, block
-// prefixes by look-back.  Tiles beyond `cap` (a wrong max_seg_words hint) are
-// reported in *err and not planned.
-constexpr int kPlanThreads = 1024, kPlanPer = 8;
-template <int kTW>
-__global__ __launch_bounds__(kPlanThreads) void tile_plan_kernel(
-    const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ toff,
-    uint32_t *__restrict__ tmap, uint64_t cap, uint64_t *pstatus, uint32_t *ticket,
-    uint32_t *err) {
-  __shared__ int wsum[kPlanThreads / 64];
-  __shared__ uint32_t blk_s;
-  __shared__ uint64_t base_s;
-  const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
-  if (tid == 0) blk_s = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const uint32_t blk = blk_s;
-  const uint64_t i0 = (uint64_t)blk * (kPlanThreads * kPlanPer) + (uint64_t)tid * kPlanPer;
-  int c[kPlanPer];
-  int t = 0;
-#pragma unroll
-  for (int q = 0; q < kPlanPer; ++q) {
-    const uint64_t i = i0 + q;
-    c[q] = 0;
-    if (i < n) {
-      const uint64_t pw = swo[i + 1] - swo[i];
-      c[q] = pw == 0 ? 1 : (int)((pw + kTW - 1) / kTW);
-    }
-    t += c[q];
-  }
-  const int incl = wave_incl_add(t);
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int wex = 0, tot = 0;
-  for (int q = 0; q < kPlanThreads / 64; ++q) {
-    if (q < w) wex += wsum[q];
-    tot += wsum[q];
-  }
-  if (tid == 0) lb_publish(pstatus, blk, (uint64_t)tot);
-  if (w == 0) {
-    const uint64_t b = lb_resolve(pstatus, blk, (uint64_t)tot);
-    if (lane == 0) base_s = b;
-  }
-  __syncthreads();
-  uint64_t o = base_s + (uint64_t)(wex + incl - t);
-#pragma unroll
-  for (int q = 0; q < kPlanPer; ++q) {
-    const uint64_t i = i0 + q;
-    if (i < n) {
-      toff[i] = o;
-      for (int k = 0; k < c[q]; ++k) {
-        if (o + k < cap) tmap[o + k] = (uint32_t)i;
-        else atomicOr(err, 2u);
-      }
-      if (i == n - 1) toff[n] = o + c[q] < cap ? o + c[q] : cap;
-      o += c[q];
-    }
-  }
 }
 
 // ------------------------------------------------------------ decoder
@@ -2074,7 +989,6 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
 }
 
-#include "encode_v3.hip"
 #include "encode_v4.hip"
 
 }  // namespace cpk
@@ -2088,15 +1002,6 @@ struct cpk_ctx_s {
   uint64_t *status;       // look-back words
   uint64_t status_cap;    // entries
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
-  void *plan;             // tiled encode: toff | tmap | pstatus | tstate
-  uint64_t plan_cap;      // bytes
-  int encoder;            // 4: size + emit passes (default); 1-3: earlier encoders
-  uint32_t *e3_tfirst;    // encoder v3: tile -> first piece starting in it
-  uint64_t *e3_status;    //   look-back word per tile
-  uint64_t *e3_tstate;    //   exit run state per tile
-  uint64_t e3_cap;        //   tiles the arrays hold (+2)
-  uint32_t epoch;         //   launch epoch tagging the look-back words, 1..65535
-  int e3_grid;            //   workgroups of encode3_kernel resident at once
   uint64_t *e4_bv;        // encoder v4: run boundaries per 64-word step
   uint64_t e4_bv_cap;     //   entries
   HostPipe *pipe;         // cpk_encode_host / cpk_decode_host staging (lazy)
@@ -2129,78 +1034,6 @@ int ensure_status(cpk_ctx ctx, uint64_t n) {
   }
   ctx->status_cap = cap;
   return CPK_OK;
-}
-int ensure_plan(cpk_ctx ctx, uint64_t bytes) {
-  if (bytes <= ctx->plan_cap) return CPK_OK;
-  if (ctx->plan) hipFree(ctx->plan);
-  ctx->plan = nullptr;
-  uint64_t cap = bytes + bytes / 4;
-  if (hipMalloc(&ctx->plan, cap) != hipSuccess) {
-    ctx->plan_cap = 0;
-    return CPK_ENOMEM;
-  }
-  ctx->plan_cap = cap;
-  return CPK_OK;
-}
-uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
-
-// Encoder v3 (encode_v3.hip): plan kernel + persistent tile kernel.  The
-// tile count is bounded from the size hint (or read back when there is none);
-// a batch larger than the bound is reported through the error word.
-int e3_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, uint64_t hint,
-              void *d_out, uint64_t *d_out_off, hipStream_t s) {
-  const uint64_t TW = cpk::kE3TileWords;
-  uint64_t ntb;
-  if (hint) {
-    ntb = ((uint64_t)n * hint + TW - 1) / TW;
-  } else {
-    uint64_t ends[2];
-    if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return CPK_EDEVICE;
-    ntb = (ends[1] - ends[0] + TW - 1) / TW;
-  }
-  if (ntb > 0xfffffff0ull) return CPK_EUNSUPPORTED;
-  bool fresh = false;
-  if (ntb + 2 > ctx->e3_cap) {
-    if (ctx->e3_tfirst) hipFree(ctx->e3_tfirst);
-    if (ctx->e3_status) hipFree(ctx->e3_status);
-    if (ctx->e3_tstate) hipFree(ctx->e3_tstate);
-    ctx->e3_tfirst = nullptr;
-    ctx->e3_status = ctx->e3_tstate = nullptr;
-    ctx->e3_cap = 0;
-    uint64_t cap = ntb + 2 + (ntb + 2) / 4;
-    if (cap < 1024) cap = 1024;
-    if (hipMalloc(&ctx->e3_tfirst, cap * 4) != hipSuccess ||
-        hipMalloc(&ctx->e3_status, cap * 16) != hipSuccess ||  // tile sizes | round bases
-        hipMalloc(&ctx->e3_tstate, cap * 8) != hipSuccess)
-      return CPK_ENOMEM;
-    ctx->e3_cap = cap;
-    fresh = true;
-  }
-  if (++ctx->epoch > 0xffffu) {
-    ctx->epoch = 1;
-    fresh = true;
-  }
-  if (fresh && (hipMemsetAsync(ctx->e3_status, 0, ctx->e3_cap * 16, s) != hipSuccess ||
-                hipMemsetAsync(ctx->e3_tstate, 0, ctx->e3_cap * 8, s) != hipSuccess))
-    return CPK_EDEVICE;
-  uint32_t *err = ctx->tickets + cpk::kTkErr;
-  uint64_t pb = ((uint64_t)n + 2 + 255) / 256;
-  if (pb > 4096) pb = 4096;
-  hipLaunchKernelGGL(cpk::e3_plan_kernel, dim3((unsigned)pb), dim3(256), 0, s, d_swo, n,
-                     (uint32_t)ntb, ctx->e3_tfirst, d_out_off, hint, err);
-  if (ntb == 0) return hip_ok(hipGetLastError());
-  uint64_t grid = (uint64_t)ctx->e3_grid;
-  if (grid > (uint64_t)cpk::kE3Threads * cpk::kE3MaxPer) grid = (uint64_t)cpk::kE3Threads * cpk::kE3MaxPer;
-  if (grid > ntb) grid = ntb;
-  hipLaunchKernelGGL(cpk::encode3_kernel, dim3((unsigned)grid), dim3(cpk::kE3Threads), cpk::kE3Lds,
-                     s, (const uint64_t *)d_in, d_swo, n, (uint32_t)ntb,
-                     (const uint32_t *)ctx->e3_tfirst, (uint8_t *)d_out, d_out_off,
-                     ctx->e3_status, ctx->e3_status + ctx->e3_cap, ctx->e3_tstate, ctx->epoch,
-                     err);
-  return hip_ok(hipGetLastError());
 }
 }  // namespace
 
@@ -2252,12 +1085,6 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
   cpk_ctx c = (cpk_ctx)calloc(1, sizeof(cpk_ctx_s));
   if (!c) return CPK_ENOMEM;
   c->device = device;
-  {
-    const char *e = getenv("CPK_ENCODER");
-    // CPK_ENCODER selects an encoder for A/B runs; v4 (size + emit passes,
-    // wave per piece) is the default, measured fastest on every config
-    c->encoder = (e && e[0] == '1') ? 1 : (e && e[0] == '3') ? 3 : (e && e[0] == '2') ? 2 : 4;
-  }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
   if (hipMalloc(&c->tickets, cpk::kTkWords * 4) != hipSuccess ||
@@ -2265,34 +1092,11 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     free(c);
     return CPK_ENOMEM;
   }
-  if (hipFuncSetAttribute((const void *)cpk::encode_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kEncLds) != hipSuccess ||
-      hipFuncSetAttribute((const void *)cpk::encode_kernel<true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kEncLds) != hipSuccess ||
-      hipFuncSetAttribute((const void *)cpk::encode2_kernel,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kE2Lds) != hipSuccess ||
-      hipFuncSetAttribute((const void *)cpk::decode_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess ||
-      hipFuncSetAttribute((const void *)cpk::encode3_kernel,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kE3Lds) != hipSuccess) {
+  if (hipFuncSetAttribute((const void *)cpk::decode_kernel<false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess) {
     hipFree(c->tickets);
     free(c);
     return CPK_EDEVICE;
-  }
-  {
-    // persistent grid of encode3_kernel: every workgroup resident at once
-    // (its look-back waits on other workgroups).  The occupancy answer can be
-    // one block per CU high for SGPR-heavy kernels (MI355X_MICROARCH.md,
-    // Residency), so one block per CU is kept in reserve.
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)cpk::encode3_kernel,
-                                                     cpk::kE3Threads, cpk::kE3Lds) != hipSuccess ||
-        occ < 1)
-      occ = 1;
-    const char *rs = getenv("CPK_E3_RESERVE");  // blocks per CU kept in reserve (tuning)
-    const int reserve = rs ? atoi(rs) : 1;
-    if (occ > reserve) occ -= reserve;
-    c->e3_grid = occ * c->cus;
   }
   *out = c;
   return CPK_OK;
@@ -2302,11 +1106,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (!ctx) return;
   DeviceGuard g(ctx->device);
   if (ctx->status) hipFree(ctx->status);
-  if (ctx->plan) hipFree(ctx->plan);
   if (ctx->tickets) hipFree(ctx->tickets);
-  if (ctx->e3_tfirst) hipFree(ctx->e3_tfirst);
-  if (ctx->e3_status) hipFree(ctx->e3_status);
-  if (ctx->e3_tstate) hipFree(ctx->e3_tstate);
   if (ctx->e4_bv) hipFree(ctx->e4_bv);
   pipe_destroy(ctx->pipe);
   free(ctx);
@@ -2424,80 +1224,7 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
-  if (ctx->encoder == 3) return e3_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
-  if (ctx->encoder == 4) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
-  // counters (not the error word: that is cleared by cpk_ctx_take_error)
-  if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
-  const bool v2 = ctx->encoder == 2;
-  if (!v2 && max_seg_words != 0 && max_seg_words <= (uint64_t)cpk::kTileWords) {
-    // one workgroup per piece
-    int rc = ensure_status(ctx, n);
-    if (rc) return rc;
-    if (hipMemsetAsync(ctx->status, 0, (size_t)n * 8, s) != hipSuccess) return CPK_EDEVICE;
-    unsigned grid = (unsigned)(2 * ctx->cus);
-    if (grid > n) grid = n;
-    hipLaunchKernelGGL(cpk::encode_kernel<false>, dim3(grid), dim3(cpk::kEncThreads), cpk::kEncLds,
-                       s, (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
-                       ctx->tickets, (const uint32_t *)nullptr, (const uint64_t *)nullptr,
-                       (uint64_t *)nullptr, ctx->tickets + cpk::kTkErr);
-    return hip_ok(hipGetLastError());
-  }
-  // tiled: pieces cut into tiles (1024 words for the wave-per-tile encoder,
-  // 8192 for the workgroup one); the tile count is bounded from the hint, or
-  // from the batch's word count when there is no hint
-  const uint64_t tw = v2 ? (uint64_t)cpk::kE2Words : (uint64_t)cpk::kTileWords;
-  uint64_t tiles;
-  if (max_seg_words) {
-    tiles = (uint64_t)n * ((max_seg_words + tw - 1) / tw);
-  } else {
-    uint64_t ends[2];
-    if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return CPK_EDEVICE;
-    tiles = (uint64_t)n + (ends[1] - ends[0]) / tw;
-  }
-  const uint64_t blocks = ((uint64_t)n + cpk::kPlanThreads * cpk::kPlanPer - 1) /
-                          (cpk::kPlanThreads * cpk::kPlanPer);
-  const uint64_t o_tmap = align256(((uint64_t)n + 1) * 8);
-  const uint64_t o_pst = o_tmap + align256(tiles * 4);
-  const uint64_t o_tst = o_pst + align256(blocks * 8);
-  const uint64_t bytes = o_tst + align256(tiles * 8);
-  int rc = ensure_plan(ctx, bytes);
-  if (rc) return rc;
-  rc = ensure_status(ctx, tiles);
-  if (rc) return rc;
-  uint8_t *plan = (uint8_t *)ctx->plan;
-  uint64_t *toff = (uint64_t *)plan;
-  uint32_t *tmap = (uint32_t *)(plan + o_tmap);
-  uint64_t *pst = (uint64_t *)(plan + o_pst);
-  uint64_t *tst = (uint64_t *)(plan + o_tst);
-  if (hipMemsetAsync(pst, 0, blocks * 8, s) != hipSuccess ||
-      hipMemsetAsync(tst, 0, tiles * 8, s) != hipSuccess ||
-      hipMemsetAsync(ctx->status, 0, tiles * 8, s) != hipSuccess)
-    return CPK_EDEVICE;
-  if (v2) {
-    hipLaunchKernelGGL(cpk::tile_plan_kernel<cpk::kE2Words>, dim3((unsigned)blocks),
-                       dim3(cpk::kPlanThreads), 0, s, d_swo, n, toff, tmap, tiles, pst,
-                       ctx->tickets + cpk::kTkPlan, ctx->tickets + cpk::kTkErr);
-    // persistent: 6 workgroups of 4 independent waves per CU
-    unsigned grid = (unsigned)(6 * ctx->cus);
-    if (grid > (tiles + 3) / 4) grid = (unsigned)((tiles + 3) / 4);
-    hipLaunchKernelGGL(cpk::encode2_kernel, dim3(grid), dim3(cpk::kE2Threads), cpk::kE2Lds, s,
-                       (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
-                       ctx->tickets, (const uint32_t *)tmap, (const uint64_t *)toff, tst);
-    return hip_ok(hipGetLastError());
-  }
-  hipLaunchKernelGGL(cpk::tile_plan_kernel<cpk::kTileWords>, dim3((unsigned)blocks),
-                     dim3(cpk::kPlanThreads), 0, s, d_swo, n, toff, tmap, tiles, pst,
-                     ctx->tickets + cpk::kTkPlan, ctx->tickets + cpk::kTkErr);
-  unsigned grid = (unsigned)(2 * ctx->cus);
-  if (grid > tiles) grid = (unsigned)tiles;
-  hipLaunchKernelGGL(cpk::encode_kernel<true>, dim3(grid), dim3(cpk::kEncThreads), cpk::kEncLds, s,
-                     (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->status,
-                     ctx->tickets, (const uint32_t *)tmap, (const uint64_t *)toff, tst,
-                     ctx->tickets + cpk::kTkErr);
-  return hip_ok(hipGetLastError());
+  return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
 }
 
 int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
@@ -2509,9 +1236,8 @@ int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
       hipStreamSynchronize(s) != hipSuccess)
     return CPK_EDEVICE;
   if (e && hipMemsetAsync(ctx->tickets + cpk::kTkErr, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
-  // bits 0, 1: a piece over its size hint (encoder / tile plan); bit 2: a
-  // cross-workgroup wait timed out (a grid larger than the device holds at
-  // once -- cannot happen by design)
+  // bit 0: a piece over its size hint; bit 2: a cross-workgroup wait timed
+  // out (cannot happen by design: every wave it waits on is resident)
   return e ? ((e & 4u) ? CPK_EDEVICE : CPK_EINVAL) : CPK_OK;
 }
 

@@ -52,3 +52,38 @@ def test_reduce_over_gloo_world2():
         assert p.exitcode == 0
     for rank, mx, sm in got:
         assert mx == [2.0, 10.0] and sm == [3.0, 10.0]
+
+
+@pytest.mark.parametrize("config,segments", [(2, 48), (3, 12)])
+def test_bench_launcher_spawns_ranks(config, segments):
+    """bench.py --gpus 2 starts two rank processes itself (no torchrun) and
+    drives the shard plan + round trip + max/sum reduction end to end; here
+    with the oracle as the kernel (--stub, gloo).  Config 3's ragged messages
+    are split by bytes."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2", "--stub",
+                          "--config", str(config), "--segments", str(segments), "--seg-words", "512",
+                          "--steps", "2"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["errors"] == 0
+    per_msg = 4 if config == 3 else 1
+    assert line["pieces_total"] == 2 * segments * per_msg
+    b = line["shard_bounds"]
+    assert b[0] == 0 and b[-1] == 2 * segments and 0 < b[1] < 2 * segments
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2", "--stub"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2

@@ -1,0 +1,52 @@
+"""The single-pass encoder's mask algebra (tools/step_model.py, the model of
+csrc/encode_sp.hip's role pass) against the oracle: per-step role masks from
+a carried state, per-wave entry states recomputed from earlier steps' masks,
+pieces processed in chunks with the state carried between them.  Small wave /
+chunk sizes put many wave and chunk seams inside each piece."""
+import numpy as np
+import pytest
+
+import step_model as sm
+
+
+@pytest.mark.parametrize("ws,nw", [(32, 4), (1, 2), (2, 3), (4, 1)])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_mask_algebra_matches_oracle(oracle, ws, nw, seed):
+    rng = np.random.default_rng(seed * 100 + ws)
+    for _ in range(6):
+        d = sm.rand_piece(rng, int(rng.integers(1, 3000)))
+        assert sm.encode_model(d, ws, nw) == oracle.pack(d)
+
+
+@pytest.mark.parametrize("ws,nw", [(32, 4), (1, 1), (2, 2), (3, 1)])
+def test_mask_algebra_edge_pieces(oracle, ws, nw):
+    D = np.full(8, 7, np.uint8)
+    L = np.array([0, 1, 2, 3, 4, 5, 6, 7], np.uint8)
+    Z = np.zeros(8, np.uint8)
+    M = np.array([0, 0, 9, 0, 1, 0, 0, 0], np.uint8)
+    cases = [
+        [Z] * 2000, [D] * 2000, [L] * 2000, [Z] * 256, [Z] * 257, [Z] * 512 + [M],
+        [L] * 300 + [D] + [L] * 1700, [D] * 511 + [L] * 700 + [D] * 900,
+        [Z] * 255 + [D] * 1030 + [Z] * 257, [L] * 255 + [D] * 2 + [L] * 1000,
+        [D] * 256 + [L] * 3 + [D] * 300, [D] * 193 + [M] + [D] * 70,
+        [L] * 64 + [D] + [L] * 255 + [D] * 2 + [L] * 600 + [D] * 5,
+        [M, D, Z, D, L, L, Z, Z, M] * 40,
+    ]
+    for c in cases:
+        d = np.concatenate(c).tobytes()
+        assert sm.encode_model(d, ws, nw) == oracle.pack(d), [len(x) for x in c][:4]
+
+
+def test_state_at_equals_sequential_state():
+    rng = np.random.default_rng(7)
+    for _ in range(5):
+        d = sm.rand_piece(rng, int(rng.integers(200, 2500)))
+        w = np.frombuffer(d, np.uint8).reshape(-1, 8)
+        tags = ((w != 0) * (1 << np.arange(8))).sum(1)
+        ns = (len(w) + 63) // 64
+        masks = [sm.step_masks(tags, len(w), s) for s in range(ns)]
+        st = (0, False, 0)
+        for s in range(ns):
+            assert sm.state_at(masks, s, (0, False, 0)) == st, s
+            _, Z, DL, D = masks[s]
+            st = sm.roles(Z, DL, D, st)[3]
