@@ -1,0 +1,820 @@
+// encode_sp.hip -- single-pass encoder (the default).  Included from
+// packed_codec.hip (namespace cpk); uses encode_v4.hip's e4_tag.
+//
+// One 256-thread workgroup per piece, pieces taken in order from a ticket,
+// the piece held in VGPRs: wave w owns the 64-word steps [32w, 32w + 32) of an
+// 8192-word chunk, lane = word.  Per piece:
+//   A1  load the wave's steps (32 x 8 B per lane, all in flight); per word the
+//       nonzero-byte tag m (PackedOutputStream.java:64-117; kept packed four
+//       per VGPR); per step the Z / DL / D ballots (zero word, <= 1 zero
+//       byte, tag 0xff), stashed lane-per-step and copied to LDS for the
+//       other waves;
+//   A2  the roles PackedOutputStream.write gives each word, per step, from
+//       mask arithmetic and a carried state (scalar ALU): zero-run heads
+//       (:119-131), literal-run members (:133-193: a carry-add smears each
+//       0xFF head over the rest of its D/L stretch), 0xFF heads, run ends.
+//       Each wave recomputes the state entering its first step from the
+//       earlier steps' masks.  The packed bytes of the wave follow from
+//       popcounts.  tools/step_model.py is this algebra in Python, checked
+//       against the oracle (tests/test_step_model.py);
+//   look-back  the piece's size is published and its offset found by a
+//       decoupled look-back over the pieces before it (epoch-tagged 8-byte
+//       status words);
+//   B   each word's string (tag + v_perm-compacted bytes + count, or the 8
+//       bytes of a literal-run member) OR-ed into a per-wave LDS ring at its
+//       offset from a wave scan; complete 16-byte lines stream out.
+// Traffic U + P: the piece is read once.  A piece over one chunk is sized
+// chunk by chunk (run state carried from chunk to chunk), then read again
+// and emitted: 2U + P for those pieces only.
+
+constexpr int kSpWaves = 4;
+constexpr int kSpThreads = 64 * kSpWaves;
+constexpr int kSpWS = 32;                      // steps per wave
+constexpr int kSpCS = kSpWaves * kSpWS;        // steps per chunk (8192 words)
+constexpr uint32_t kSpRing = 2048;             // output ring per wave (bytes)
+constexpr uint32_t kSpRingLines = kSpRing / 16;
+constexpr uint32_t kSpRingStride = kSpRing + 16;  // + one overhang line (line 0's spill)
+constexpr uint32_t kSpoLut = 0;                                      // u64[256]
+constexpr uint32_t kSpoMsk = 2048;                                   // u64[kSpCS][3]
+constexpr uint32_t kSpoRing = kSpoMsk + kSpCS * 24;                  // per wave
+constexpr uint32_t kSpoScr = kSpoRing + kSpWaves * kSpRingStride;    // u64[16]
+constexpr uint32_t kSpLds = kSpoScr + 16 * 8;                        // 13,504 B
+static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
+// scratch words: [0] ticket, [1..4] wave bytes, [5] piece offset,
+// [6..9] chunk exit state (two parities x {zl, dlo | hd << 1})
+// Steps are scheduled one at a time: hoisting later steps' LUT reads and
+// lane reads ahead would keep them all live at once (VGPR spills).
+#ifndef CPK_SP_FENCE
+#define CPK_SP_FENCE 1
+#endif
+#if CPK_SP_FENCE
+#define CPK_SP_STEP_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define CPK_SP_STEP_FENCE()
+#endif
+#ifndef CPK_SP_WPE
+#define CPK_SP_WPE 2  // waves per SIMD the registers must allow (2 workgroups per CU)
+#endif
+
+// status word per piece: [63:62] flag (1 aggregate, 2 inclusive prefix),
+// [61:46] launch epoch, [45:0] value (a relaxed 8-byte agent-scope granule:
+// the data is the flag, cdna_hip_programming.md Guideline 16 form R2)
+constexpr uint64_t kSpValMask = (1ull << 46) - 1;
+__device__ __forceinline__ uint64_t sp_word(uint32_t ep, uint32_t flag, uint64_t v) {
+  return ((uint64_t)flag << 62) | ((uint64_t)(ep & 0xffffu) << 46) | (v & kSpValMask);
+}
+__device__ __forceinline__ uint32_t sp_flag(uint64_t w, uint32_t ep) {
+  return (uint32_t)((w >> 46) & 0xffffu) == (ep & 0xffffu) ? (uint32_t)(w >> 62) : 0u;
+}
+
+struct SpSt {
+  uint32_t zl;   // zero run ending at the step start (0: none)
+  uint32_t dlo;  // the word before the step is a D/L word
+  uint32_t hd;   // distance back to that stretch's last 0xFF head (0: none), <= 256
+};
+
+__device__ __forceinline__ uint64_t sp_uni(uint64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t sp_rl(uint32_t lo, uint32_t hi, int j) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, j) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, j) << 32);
+}
+// v_writelane_b32 (the LLVM intrinsic; clang exposes no builtin for it)
+extern "C" __device__ int cpk_llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t sp_wl(uint32_t old, uint32_t v, int j) {
+  return (uint32_t)cpk_llvm_writelane((int)v, j, (int)old);
+}
+// per lane: mask bit set ? b : a (one v_cndmask on the SGPR mask)
+__device__ __forceinline__ uint32_t sp_sel(uint32_t a, uint32_t b, uint64_t mask) {
+  uint32_t r;
+  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
+  return r;
+}
+
+// Roles of one step from its masks and the state entering it; the state
+// entering the next step replaces st (tools/step_model.py: roles).
+__device__ __forceinline__ void sp_roles(uint64_t Z, uint64_t DL, uint64_t D, SpSt &st,
+                                         uint64_t &Zh, uint64_t &Mem) {
+  // zero runs: a head at each run start and every 256 words after it
+  Zh = Z & ~((Z << 1) | (st.zl ? 1ull : 0ull));
+  if (st.zl && (Z & 1)) {
+    const uint32_t j0 = (256u - (st.zl & 255u)) & 255u;
+    if (j0 < 64) {
+      const uint64_t pre = j0 == 63 ? ~0ull : ((2ull << j0) - 1);
+      if ((Z & pre) == pre) Zh |= 1ull << j0;
+    }
+  }
+  const uint64_t nz = ~Z;
+  const uint32_t zl2 = nz ? (uint32_t)__builtin_clzll(nz) : st.zl + 64;
+  // D/L stretches: each head's literal run covers up to 255 following words
+  if (st.dlo && (DL & 1) && st.hd >= 193) {
+    // the carried head's coverage ends inside this step: the next head is
+    // the first D >= that head + 256 (:143-161)
+    const uint64_t ndl = ~DL;
+    const int f = ndl ? __builtin_ctzll(ndl) : 64;
+    const uint64_t rng = f >= 64 ? ~0ull : ((1ull << f) - 1);
+    const uint64_t A = (D << 1) & DL;
+    const uint64_t C = (DL + A) ^ DL ^ A;
+    Mem = DL & (A | C) & ~rng;
+    const int c = 255 - (int)st.hd;
+    uint64_t cm = 0;
+    if (c >= 0) {
+      const int k = min(c + 1, f);
+      cm = k >= 64 ? ~0ull : ((1ull << k) - 1);
+    }
+    const int x = max(c + 1, 0);
+    const uint64_t dc = x >= 64 ? 0ull : (D & rng & (~0ull << x));
+    if (dc) {
+      const int h1 = __builtin_ctzll(dc);
+      cm |= rng & (h1 >= 63 ? 0ull : (~0ull << (h1 + 1)));
+    }
+    Mem |= cm;
+  } else {
+    const uint64_t cin = (st.dlo && (DL & 1) && st.hd) ? 1ull : 0ull;
+    const uint64_t A = ((D << 1) | cin) & DL;
+    const uint64_t C = (DL + A) ^ DL ^ A;
+    Mem = DL & (A | C);
+  }
+  uint32_t hd2 = 0, dlo2 = 0;
+  if (DL >> 63) {
+    dlo2 = 1;
+    const uint64_t nd = ~DL;
+    const int t = nd ? 64 - __builtin_clzll(nd) : 0;  // start of the run reaching bit 63
+    const uint64_t H = D & ~Mem & (~0ull << t);
+    if (H) hd2 = 1u + (uint32_t)__builtin_clzll(H);
+    else if (t == 0 && st.dlo && st.hd) hd2 = min(st.hd + 64u, 256u);
+  }
+  st.zl = zl2;
+  st.dlo = dlo2;
+  st.hd = hd2;
+}
+
+__device__ __forceinline__ uint64_t sp_ld(const uint64_t *p) { return sp_uni(*p); }
+
+// first D word at chunk position >= x and < lim, else lim
+__device__ int sp_first_d(const uint64_t *msk, int x, int lim) {
+  if (x >= lim) return lim;
+  int q = x >> 6;
+  uint64_t m = sp_ld(&msk[3 * q + 2]) & (~0ull << (x & 63));
+  while (!m) {
+    ++q;
+    if (q * 64 >= lim) return lim;
+    m = sp_ld(&msk[3 * q + 2]);
+  }
+  return min(q * 64 + __builtin_ctzll(m), lim);
+}
+
+// State entering chunk step s0 from the masks of the steps before it and
+// the chunk's entering state (tools/step_model.py: state_at)
+__device__ SpSt sp_state_at(const uint64_t *msk, int s0, SpSt cst) {
+  if (s0 == 0) return cst;
+  SpSt st = {0u, 0u, 0u};
+  const uint64_t Zp = sp_ld(&msk[3 * (s0 - 1)]), DLp = sp_ld(&msk[3 * (s0 - 1) + 1]);
+  if (Zp >> 63) {
+    int q = s0 - 1;
+    uint32_t zl = 0;
+    uint64_t z = Zp;
+    while (z == ~0ull) {
+      zl += 64;
+      if (--q < 0) break;
+      z = sp_ld(&msk[3 * q]);
+    }
+    st.zl = zl + (q >= 0 ? (uint32_t)__builtin_clzll(~z) : cst.zl);
+  }
+  if (!(DLp >> 63)) return st;
+  st.dlo = 1;
+  int q = s0 - 1;
+  uint64_t d = DLp;
+  while (d == ~0ull) {
+    if (--q < 0) break;
+    d = sp_ld(&msk[3 * q + 1]);
+  }
+  const int P = 64 * s0;
+  int h;
+  if (q >= 0 || !cst.dlo || !cst.hd) {
+    const int start = q >= 0 ? 64 * q + 64 - __builtin_clzll(~d) : 0;
+    h = sp_first_d(msk, start, P);
+    if (h >= P) return st;
+  } else {
+    h = -(int)cst.hd;
+  }
+  for (;;) {
+    const int h2 = sp_first_d(msk, max(h + 256, 0), P);
+    if (h2 >= P) break;
+    h = h2;
+  }
+  st.hd = (uint32_t)min(P - h, 256);
+  return st;
+}
+
+// words of class cls (0: Z, 1: DL) from chunk step s on (<= 256); la: the
+// count continuing past the chunk's end
+__device__ uint32_t sp_cont(const uint64_t *msk, int s, int cs, int cls, uint32_t la) {
+  uint32_t r = 0;
+  for (int q = s; r < 256; ++q) {
+    if (q >= cs) {
+      r += la;
+      break;
+    }
+    const uint64_t m = sp_ld(&msk[3 * q + cls]);
+    if (m != ~0ull) {
+      r += (uint32_t)__builtin_ctzll(~m);
+      break;
+    }
+    r += 64;
+  }
+  return min(r, 256u);
+}
+
+struct SpRegs {
+  uint64_t v[kSpWS];       // the words, step j in v[j]
+  uint32_t mp[kSpWS / 4];  // tags, four per register
+  uint32_t zl, zh, dll, dlh, dl_, dh_;                 // A1 stash: Z, DL, D (lane = step)
+  uint32_t ozl, ozh, oml, omh, ohl, ohh, oel, oeh;     // A2 stash: ZO, Mem, HC, E
+  uint32_t ox;                                         //   X: words past the step to the next run end
+};
+
+// A1: the wave's cnt steps at src (wrem piece words from src on); returns
+// this lane's nonzero-byte count
+__device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict__ src, uint32_t wrem,
+                                          int cnt, int lane) {
+  // loads clamped to the piece, not predicated: step j's lanes read
+  // min(lane, last valid lane of the step) (one lane register for all steps)
+#pragma unroll
+  for (int j = 0; j < kSpWS; ++j)
+    if (j < cnt) R.v[j] = (src + j * 64)[min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < kSpWS; ++j) {
+    if (j < cnt) {
+      // (lane vs a scalar bound: no per-step lane constants kept in registers)
+      const bool valid = (uint32_t)lane < wrem - 64u * j;
+      const uint32_t m = valid ? e4_tag(R.v[j]) : 0u;
+      if (j & 3) R.mp[j >> 2] |= m << (8 * (j & 3));
+      else R.mp[j >> 2] = m;
+      const uint32_t pc = (uint32_t)__builtin_popcount(m);
+      acc += pc;
+      const uint64_t Z = __ballot(valid && m == 0), DL = __ballot(pc >= 7), D = __ballot(m == 0xffu);
+      R.zl = sp_wl(R.zl, (uint32_t)Z, j);
+      R.zh = sp_wl(R.zh, (uint32_t)(Z >> 32), j);
+      R.dll = sp_wl(R.dll, (uint32_t)DL, j);
+      R.dlh = sp_wl(R.dlh, (uint32_t)(DL >> 32), j);
+      R.dl_ = sp_wl(R.dl_, (uint32_t)D, j);
+      R.dh_ = sp_wl(R.dh_, (uint32_t)(D >> 32), j);
+    }
+    CPK_SP_STEP_FENCE();
+  }
+  return acc;
+}
+
+// the wave's masks to LDS (lane j = step sa + j)
+__device__ __forceinline__ void sp_put_masks(const SpRegs &R, uint64_t *msk, int sa, int cnt, int lane) {
+  if (lane < cnt) {
+    uint64_t *m = msk + 3 * (sa + lane);
+    m[0] = (uint64_t)R.zl | ((uint64_t)R.zh << 32);
+    m[1] = (uint64_t)R.dll | ((uint64_t)R.dlh << 32);
+    m[2] = (uint64_t)R.dl_ | ((uint64_t)R.dh_ << 32);
+  }
+}
+
+// A2, sequential form (scalar ALU, one step at a time): the roles of the
+// wave's steps from the state entering its first step; stashes ZO (no
+// output: zero-run members, past the end), Mem, HC (heads with a count byte)
+// and E (run ends) at lane = step; returns the steps' packed bytes beyond
+// their nonzero bytes.  nz0 / ndl0: bit 0 of the step after the wave's last.
+// Used when a D/L stretch longer than 192 words enters a step (a literal run
+// may end inside it); sp_a2p otherwise.
+__device__ uint32_t sp_a2_seq(SpRegs &R, int cnt, uint32_t wrem, SpSt st, uint32_t nz0, uint32_t ndl0) {
+  uint32_t bytes = 0;
+  for (int j = 0; j < cnt; ++j) {
+    const uint64_t Z = sp_rl(R.zl, R.zh, j), DL = sp_rl(R.dll, R.dlh, j), D = sp_rl(R.dl_, R.dh_, j);
+    const uint32_t vr = wrem - 64u * j;
+    const uint64_t V = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
+    uint64_t Zh, Mem;
+    sp_roles(Z, DL, D, st, Zh, Mem);
+    const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~V;
+    bytes += (uint32_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
+                        __builtin_popcountll(HC));
+    uint64_t z0 = nz0, d0 = ndl0;
+    if (j + 1 < cnt) {
+      z0 = (uint32_t)__builtin_amdgcn_readlane((int)R.zl, j + 1) & 1u;
+      d0 = (uint32_t)__builtin_amdgcn_readlane((int)R.dll, j + 1) & 1u;
+    }
+    const uint64_t E = (Z & ~((Z >> 1) | (z0 << 63))) | (DL & ~((DL >> 1) | (d0 << 63)));
+    R.ozl = sp_wl(R.ozl, (uint32_t)ZO, j);
+    R.ozh = sp_wl(R.ozh, (uint32_t)(ZO >> 32), j);
+    R.oml = sp_wl(R.oml, (uint32_t)Mem, j);
+    R.omh = sp_wl(R.omh, (uint32_t)(Mem >> 32), j);
+    R.ohl = sp_wl(R.ohl, (uint32_t)HC, j);
+    R.ohh = sp_wl(R.ohh, (uint32_t)(HC >> 32), j);
+    R.oel = sp_wl(R.oel, (uint32_t)E, j);
+    R.oeh = sp_wl(R.oeh, (uint32_t)(E >> 32), j);
+  }
+  return bytes;
+}
+
+// value of v at lane src
+__device__ __forceinline__ uint32_t sp_from(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+
+// A2, lane-parallel form: lane j computes step j's roles with 64-bit vector
+// ops; what carries from step to step (the zero run's length, whether the
+// D/L stretch entering a step already has its 0xFF head) comes from ballots
+// over the steps.  Exact while every literal run that enters a step covers
+// it to its end, i.e. no D/L stretch longer than 192 words enters a step:
+// returns false (nothing written) when one does.  Same stash as sp_a2_seq.
+__device__ __forceinline__ bool sp_a2p(SpRegs &R, int cnt, uint32_t wrem, SpSt st, uint32_t nz0,
+                                       uint32_t ndl0, int lane, uint32_t &bytes) {
+  const bool act = lane < cnt;
+  const uint64_t Z = act ? ((uint64_t)R.zl | ((uint64_t)R.zh << 32)) : 0ull;
+  const uint64_t DL = act ? ((uint64_t)R.dll | ((uint64_t)R.dlh << 32)) : 0ull;
+  const uint64_t D = act ? ((uint64_t)R.dl_ | ((uint64_t)R.dh_ << 32)) : 0ull;
+  const uint64_t below = (1ull << lane) - 1;  // steps before this one
+  // ---- D/L stretch entering the step: its length (bounds the distance to
+  // its last head) and whether it has a head yet
+  const uint32_t dlo = (uint32_t)wave_shr1((int)(uint32_t)(DL >> 63), (int)st.dlo);
+  const uint32_t topdl = DL == ~0ull ? 64u : (uint32_t)__builtin_clzll(~DL);
+  const uint64_t notall = __ballot(!act || DL != ~0ull);
+  const uint64_t kdm = notall & below;
+  const int kd = kdm ? 63 - __builtin_clzll(kdm) : -1;  // last step before with a non-D/L word
+  const uint32_t topdl_k = sp_from(topdl, kd < 0 ? 0 : kd);
+  const uint32_t len = kd >= 0 ? topdl_k + 64u * (uint32_t)(lane - 1 - kd)
+                               : (st.dlo ? st.hd : 0u) + 64u * (uint32_t)lane;
+  const bool cont = act && dlo && (DL & 1);
+  if (__ballot(cont && len > 192)) return false;
+  const uint64_t anyD = __ballot(act && D != 0);
+  const bool topd = topdl > 0 && (D >> (64 - topdl)) != 0;
+  const uint64_t TD = __ballot(act && topd);
+  const uint64_t btw = anyD & below & (kd >= 0 ? (~0ull << kd) << 1 : ~0ull);
+  const bool head = btw != 0 || (kd >= 0 ? ((TD >> kd) & 1) != 0 : (st.dlo && st.hd));
+  const uint64_t cin = (cont && head) ? 1ull : 0ull;
+  const uint64_t A = ((D << 1) | cin) & DL;
+  const uint64_t C = (DL + A) ^ DL ^ A;
+  const uint64_t Mem = DL & (A | C);
+  // ---- zero runs: heads at run starts and every 256 words
+  const uint32_t zc = (uint32_t)wave_shr1((int)(uint32_t)(Z >> 63), st.zl ? 1 : 0);
+  uint64_t Zh = Z & ~((Z << 1) | zc);
+  {
+    const uint32_t topz = Z == ~0ull ? 64u : (uint32_t)__builtin_clzll(~Z);
+    const uint64_t kzm = __ballot(!act || Z != ~0ull) & below;
+    const int kz = kzm ? 63 - __builtin_clzll(kzm) : -1;
+    const uint32_t topz_k = sp_from(topz, kz < 0 ? 0 : kz);
+    const uint32_t zl = kz >= 0 ? topz_k + 64u * (uint32_t)(lane - 1 - kz) : st.zl + 64u * (uint32_t)lane;
+    const uint32_t j0 = (256u - (zl & 255u)) & 255u;
+    if (__ballot(act && zc && (Z & 1) && j0 < 64)) {
+      const uint64_t pre = j0 >= 63 ? ~0ull : ((2ull << j0) - 1);
+      if (act && zc && (Z & 1) && j0 < 64 && (Z & pre) == pre) Zh |= 1ull << j0;
+    }
+  }
+  // ---- per step: output masks, run ends, bytes
+  const uint32_t vr = act ? wrem - 64u * (uint32_t)lane : 0u;
+  const uint64_t V = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
+  const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~V;
+  // bit 0 of the next step (lane + 1; the wave's last step: nz0 / ndl0)
+  uint32_t zn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)Z, 0x130, 0xf, 0xf, false) & 1u;
+  uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)DL, 0x130, 0xf, 0xf, false) & 1u;
+  if (lane == cnt - 1) {
+    zn = nz0;
+    dn = ndl0;
+  }
+  const uint64_t E = (Z & ~((Z >> 1) | ((uint64_t)zn << 63))) | (DL & ~((DL >> 1) | ((uint64_t)dn << 63)));
+  uint32_t b = act ? (uint32_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
+                                __builtin_popcountll(HC))
+                   : 0u;
+  bytes = (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)b), 63);
+  R.ozl = (uint32_t)ZO;
+  R.ozh = (uint32_t)(ZO >> 32);
+  R.oml = (uint32_t)Mem;
+  R.omh = (uint32_t)(Mem >> 32);
+  R.ohl = (uint32_t)HC;
+  R.ohh = (uint32_t)(HC >> 32);
+  R.oel = (uint32_t)E;
+  R.oeh = (uint32_t)(E >> 32);
+  return true;
+}
+
+// X per step (lane = step): words past the step's end to the first run end
+// after it (a head's count reaches that far), from the next step with a run
+// end; past the wave's last step, Xlast.  At most 256.
+__device__ __forceinline__ void sp_xs(SpRegs &R, int cnt, uint32_t Xlast, int lane) {
+  const bool act = lane < cnt;
+  const uint64_t E = (uint64_t)R.oel | ((uint64_t)R.oeh << 32);
+  const uint64_t en = __ballot(act && E != 0);
+  const uint64_t km = lane == 63 ? 0ull : (en & (~0ull << (lane + 1)));
+  const int k = km ? __builtin_ctzll(km) : 64;
+  const uint32_t ce = E ? (uint32_t)__builtin_ctzll(E) : 64u;
+  const uint32_t ce_k = sp_from(ce, k & 63);
+  uint32_t X = k < cnt ? 64u * (uint32_t)(k - lane - 1) + ce_k : 64u * (uint32_t)(cnt - 1 - lane) + Xlast;
+  R.ox = min(X, 256u);
+}
+
+// ---- the output ring -----------------------------------------------------------
+// Line L of the piece's output lives at ring line L % 128; a string crossing
+// the ring's end spills into the overhang line, which belongs to line 0.
+__device__ __forceinline__ uint4 sp_take_line(uint32_t *ring, uint64_t L) {
+  uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kSpRingLines - 1));
+  uint4 v = *rl;
+  *rl = make_uint4(0u, 0u, 0u, 0u);
+  if ((L & (kSpRingLines - 1)) == 0) {
+    uint4 *ov = reinterpret_cast<uint4 *>(ring) + kSpRingLines;
+    const uint4 o = *ov;
+    *ov = make_uint4(0u, 0u, 0u, 0u);
+    v.x |= o.x;
+    v.y |= o.y;
+    v.z |= o.z;
+    v.w |= o.w;
+  }
+  return v;
+}
+// bytes [j0, j1) of line L (a line shared with a neighbour's bytes)
+__device__ __forceinline__ void sp_store_bytes(uint8_t *out, uint32_t *ring, uint64_t L, int j0, int j1,
+                                               int lane, uint64_t ocap) {
+  const uint4 *rl = reinterpret_cast<const uint4 *>(ring) + (L & (kSpRingLines - 1));
+  uint4 val = *rl;
+  if ((L & (kSpRingLines - 1)) == 0) {
+    const uint4 o = reinterpret_cast<const uint4 *>(ring)[kSpRingLines];
+    val.x |= o.x;
+    val.y |= o.y;
+    val.z |= o.z;
+    val.w |= o.w;
+  }
+  if (lane >= j0 && lane < j1 && L * 16 + lane < ocap) {
+    const uint32_t d = (lane & 8) ? ((lane & 4) ? val.w : val.z) : ((lane & 4) ? val.y : val.x);
+    out[L * 16 + lane] = (uint8_t)(d >> (8 * (lane & 3)));
+  }
+  wave_lds_order();
+  if (lane == 0) sp_take_line(ring, L);
+  wave_lds_order();
+}
+// stores the complete lines [fl, upto); bytes below lo are a neighbour's
+// (ocap: a bound on the output buffer -- stores past it are dropped, so a
+// corrupted offset cannot fault the device)
+__device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t &fl, uint64_t upto,
+                                         uint64_t lo, int lane, uint64_t ocap) {
+  if (fl >= upto) return;
+  if (fl * 16 < lo) {
+    sp_store_bytes(out, ring, fl, (int)(lo - fl * 16), 16, lane, ocap);
+    ++fl;
+  }
+  for (uint64_t L0 = fl; L0 < upto; L0 += 64) {
+    const uint64_t L = L0 + lane;
+    if (L < upto) {
+      const uint4 v = sp_take_line(ring, L);
+      if (L * 16 + 16 <= ocap) *reinterpret_cast<uint4 *>(out + L * 16) = v;
+    }
+  }
+  fl = upto;
+}
+
+// B: the wave's strings from output byte obase on.  Xlast: words past the
+// wave's last step to the first run end after it, minus one (<= 255).
+__device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut,
+                                     uint32_t *ring, uint8_t *out, uint64_t obase, int lane,
+                                     uint64_t ocap) {
+  uint64_t rpos = obase, fl = obase >> 4;
+  const uint32_t l64 = 64u - (uint32_t)lane;
+#pragma unroll
+  for (int j = 0; j < kSpWS; ++j) {
+    if (j < cnt) {
+      const uint64_t ZO = sp_rl(R.ozl, R.ozh, j), Mem = sp_rl(R.oml, R.omh, j);
+      const uint64_t HC = sp_rl(R.ohl, R.ohh, j);
+      const uint32_t m = (R.mp[j >> 2] >> (8 * (j & 3))) & 0xffu;
+      const uint32_t lo = (uint32_t)R.v[j], hi = (uint32_t)(R.v[j] >> 32);
+      const uint64_t sel = lut[m];
+      const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
+      const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+      uint32_t cz = 0, cd = 0;
+      if (HC) {
+        // a head's count: words to its run's end, at most 255 (:119-131, :143-164)
+        const uint32_t X = (uint32_t)__builtin_amdgcn_readlane((int)R.ox, j);
+        const uint64_t E = sp_rl(R.oel, R.oeh, j);
+        const uint64_t e = E >> lane;
+        // ctz of e, 0xffffffff when e == 0 (the next run end is past the step)
+        const uint32_t z_lo = (uint32_t)e ? (uint32_t)__builtin_ctz((uint32_t)e) : 0xffffffffu;
+        const uint32_t z_hi = (uint32_t)(e >> 32) ? (uint32_t)__builtin_ctz((uint32_t)(e >> 32)) + 32u
+                                                  : 0xffffffffu;
+        uint32_t t = min(min(z_lo, z_hi), l64 + X);
+        t = min(t, 255u);
+        const uint32_t cn = sp_sel(0u, t, HC);
+        cz = m == 0 ? cn : 0u;
+        cd = cn - cz;
+      }
+      // the string: tag, the nonzero bytes, the count after a 0x00 / 0xFF tag
+      // (c0 is zero for a zero word); a literal-run member is its 8 bytes
+      const uint32_t c0p = c0 | cz;
+      uint32_t s0 = m | (c0p << 8);
+      uint32_t s1 = __builtin_amdgcn_alignbyte(c1, c0p, 3);
+      uint32_t s2 = __builtin_amdgcn_alignbyte(cd, c1, 3);
+      s0 = sp_sel(s0, lo, Mem);
+      s1 = sp_sel(s1, hi, Mem);
+      s2 = sp_sel(s2, 0u, Mem);
+      uint32_t nb = (uint32_t)__builtin_popcount(m) + sp_sel(1u, 2u, HC);
+      nb = sp_sel(nb, 8u, Mem);
+      nb = sp_sel(nb, 0u, ZO);
+      const int incl = wave_incl_add((int)nb);
+      const uint32_t o = (uint32_t)incl - nb;
+      const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+      if (stot) {
+        const uint32_t p = (uint32_t)rpos + o;
+        const uint32_t sh = (p & 3) * 8;
+        const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
+        const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
+        const uint32_t d3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
+        uint32_t *rp = ring + ((p >> 2) & (kSpRing / 4 - 1));
+        atomicOr(rp, (uint32_t)a01);
+        atomicOr(rp + 1, (uint32_t)(a01 >> 32));
+        atomicOr(rp + 2, (uint32_t)(a12 >> 32));
+        atomicOr(rp + 3, d3);
+        rpos += stot;
+        // complete lines leave 64 at a time (one full-wave store); the ring
+        // holds at most 63 + 41 lines
+        if ((uint32_t)(rpos >> 4) - (uint32_t)fl >= 64u) {
+          wave_lds_order();
+          sp_flush(out, ring, fl, fl + 64, obase, lane, ocap);
+        }
+      }
+    }
+    CPK_SP_STEP_FENCE();
+  }
+  wave_lds_order();
+  sp_flush(out, ring, fl, rpos >> 4, obase, lane, ocap);
+  if (rpos > fl * 16) {
+    const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
+    sp_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane, ocap);
+  }
+}
+
+// Look-ahead past a chunk: the zero run / D/L stretch continuing from the
+// chunk's end (<= 256 words each), from the next 4 steps' words.
+__device__ __forceinline__ void sp_lookahead(const uint64_t *__restrict__ src, uint32_t avail, int lane,
+                                             uint32_t &laz, uint32_t &ladl) {
+  uint32_t rz = 0, rd = 0;
+  bool oz = true, od = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool valid = (uint32_t)lane < (avail > 64u * j ? avail - 64u * j : 0u);
+    const uint64_t x = valid ? (src + 64 * j)[lane] : 0ull;
+    const uint32_t m = valid ? e4_tag(x) : 0u;
+    const uint64_t Z = __ballot(valid && m == 0), DL = __ballot(__builtin_popcount(m) >= 7);
+    if (oz) {
+      if (Z == ~0ull) rz += 64;
+      else { rz += (uint32_t)__builtin_ctzll(~Z); oz = false; }
+    }
+    if (od) {
+      if (DL == ~0ull) rd += 64;
+      else { rd += (uint32_t)__builtin_ctzll(~DL); od = false; }
+    }
+  }
+  laz = rz;
+  ladl = rd;
+}
+
+// the decoupled look-back (wave 0, all lanes): publishes the aggregate,
+// returns the exclusive prefix, publishes the inclusive one
+__device__ uint64_t sp_lookback(uint64_t *status, uint32_t p, uint64_t agg, uint32_t ep, uint32_t *err,
+                                int lane) {
+  if (lane == 0) st_status(&status[p], sp_word(ep, p == 0 ? 2u : 1u, agg));
+  if (p == 0) return 0;
+  uint64_t excl = 0;
+  int64_t top = (int64_t)p - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    uint64_t v[4];
+    int fi = 4;  // first inclusive among this lane's four (nearest first)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t idx = top - 4 * lane - i;
+      v[i] = idx >= 0 ? ld_status(&status[idx]) : sp_word(ep, 2u, 0);
+    }
+#pragma unroll
+    for (int i = 3; i >= 0; --i)
+      if (sp_flag(v[i], ep) == 2) fi = i;
+    const uint64_t has = __ballot(fi < 4);
+    const int fln = has ? __builtin_ctzll(has) : 64;
+    const int firstPos = fln < 64 ? 4 * fln + __builtin_amdgcn_readlane(fi, fln) : 256;
+    bool z = false;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (4 * lane + i <= firstPos) {
+        z = z || sp_flag(v[i], ep) == 0;
+        sum += v[i] & kSpValMask;
+      }
+    }
+    if (__ballot(z)) {
+      if (++spins > (1u << 22)) {  // cannot happen: every predecessor is held by a running workgroup
+        if (lane == 0) atomicOr(err, 4u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    excl += sum;
+    if (firstPos < 256) break;
+    top -= 256;
+  }
+  if (lane == 0) st_status(&status[p], sp_word(ep, 2u, excl + agg));
+  return excl;
+}
+
+__device__ __forceinline__ SpSt sp_get_state(const uint64_t *scr, int par) {
+  const uint64_t a = sp_ld(&scr[6 + 2 * par]), b = sp_ld(&scr[7 + 2 * par]);
+  SpSt s = {(uint32_t)a, (uint32_t)(b & 1), (uint32_t)(b >> 1)};
+  return s;
+}
+
+// One chunk's A1 + A2 for this wave (all waves call it; two barriers).
+// Returns the chunk's packed bytes (all waves); wbefore: bytes of the waves
+// before this one.  cst: the state entering the chunk -> leaving it.
+__device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restrict__ pw, uint32_t W,
+                                             uint32_t c, uint64_t *msk, uint64_t *scr, SpSt &cst,
+                                             int w, int lane, bool kEmit, int &cnt, uint32_t &Xlast,
+                                             uint64_t &wbefore) {
+  const uint32_t ns = (W + 63) >> 6;
+  const uint32_t cs0 = c * kSpCS;
+  const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
+  const int sa = w * kSpWS;
+  cnt = max(0, min(kSpWS, cs - sa));
+  const uint32_t wfirst = (cs0 + (uint32_t)sa) * 64;  // the wave's first word
+  const uint32_t wrem = cnt ? W - wfirst : 0;
+  uint32_t acc = 0;
+  if (cnt) {
+    acc = sp_a1(R, pw + wfirst, wrem, cnt, lane);
+    sp_put_masks(R, msk, sa, cnt, lane);
+  }
+  __syncthreads();  // the chunk's masks in LDS
+  SpSt st = cst;
+  uint32_t bytes = 0;
+  const bool last = cnt && sa + cnt == cs;  // this wave holds the chunk's last step
+  if (cnt) {
+    st = sp_state_at(msk, sa, cst);
+    uint32_t nz0 = 0, ndl0 = 0;
+    Xlast = 0;
+    if (kEmit) {
+      // the step after the wave's last: in the chunk, or past it (look-ahead)
+      uint32_t laz = 0, ladl = 0;
+      const uint32_t wend = wfirst + 64u * cnt;
+      if (last && wend < W) sp_lookahead(pw + wend, W - wend, lane, laz, ladl);
+      if (sa + cnt < cs) {
+        nz0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt)]) & 1u;
+        ndl0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt) + 1]) & 1u;
+      } else {
+        nz0 = laz ? 1u : 0u;
+        ndl0 = ladl ? 1u : 0u;
+      }
+      const uint64_t Zl = sp_rl(R.zl, R.zh, cnt - 1), DLl = sp_rl(R.dll, R.dlh, cnt - 1);
+      const int cls = (Zl >> 63) ? 0 : ((DLl >> 63) ? 1 : -1);
+      if (cls >= 0) {
+        const uint32_t r = sp_cont(msk, sa + cnt, cs, cls, cls ? ladl : laz);
+        Xlast = r ? r - 1 : 0;
+      }
+    }
+    uint32_t rb = 0;
+    if (!sp_a2p(R, cnt, wrem, st, nz0, ndl0, lane, rb)) rb = sp_a2_seq(R, cnt, wrem, st, nz0, ndl0);
+    if (kEmit) sp_xs(R, cnt, Xlast, lane);
+    bytes = rb + (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)acc), 63);
+  }
+  if (last) st = sp_state_at(msk, cs, cst);  // the state leaving the chunk
+  if (lane == 0) {
+    scr[1 + w] = bytes;
+    if (last) {
+      scr[6 + 2 * (c & 1)] = st.zl;
+      scr[7 + 2 * (c & 1)] = (uint64_t)st.dlo | ((uint64_t)st.hd << 1);
+    }
+  }
+  __syncthreads();  // wave bytes and the exit state in LDS
+  uint64_t tot = 0;
+  wbefore = 0;
+#pragma unroll
+  for (int q = 0; q < kSpWaves; ++q) {
+    const uint64_t b = sp_ld(&scr[1 + q]);
+    if (q < w) wbefore += b;
+    tot += b;
+  }
+  cst = sp_get_state(scr, c & 1);
+  return tot;
+}
+
+// kMsg = false: piece p is words [swo[p], swo[p+1]) of `in`.  kMsg = true:
+// pdesc[2p] = first word (bit 63: of `tin`, the segment tables) and
+// pdesc[2p+1] = words.
+template <bool kMsg>
+__global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
+    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo,
+    const uint64_t *__restrict__ pdesc, const uint64_t *__restrict__ tin, uint32_t n,
+    uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status, uint32_t ep,
+    uint32_t *ticket, uint32_t ppt, uint64_t hint, uint32_t *err, const uint64_t *ocapp) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // a bound on the output buffer's size: sum of 9 w + 1 over the pieces
+  // (cpk_packed_bound(w) <= 9 w + 1), + 16
+  const uint64_t ocap = kMsg ? *ocapp : 9 * (swo[n] - swo[0]) + n + 16;
+  uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kSpoLut);
+  uint64_t *msk = reinterpret_cast<uint64_t *>(smem + kSpoMsk);
+  uint64_t *scr = reinterpret_cast<uint64_t *>(smem + kSpoScr);
+  const int lane0 = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kSpoRing + w * kSpRingStride);
+  fill_luts(lut, false);
+  for (uint32_t i = lane0; i < kSpRingStride / 16; i += 64)
+    reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
+  SpRegs R;
+  R.zl = R.zh = R.dll = R.dlh = R.dl_ = R.dh_ = 0;
+  R.ozl = R.ozh = R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = 0;
+  for (;;) {
+    if (threadIdx.x == 0) scr[0] = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t t = (uint32_t)sp_ld(&scr[0]);
+    __syncthreads();  // (scr[0] read by all before the next ticket)
+    const uint64_t pfirst = (uint64_t)t * ppt;
+    if (pfirst >= n) break;
+    const uint32_t plast = (uint32_t)min(pfirst + ppt, (uint64_t)n);
+    for (uint32_t p = (uint32_t)pfirst; p < plast; ++p) {
+      // an opaque copy of the lane id: nothing lane-dependent is hoisted out
+      // of the piece loop into registers that stay live across it
+      int lane = lane0;
+      asm volatile("" : "+v"(lane));
+      uint64_t w0, W64;
+      const uint64_t *base = in;
+      if (kMsg) {
+        w0 = pdesc[2 * (uint64_t)p];
+        W64 = pdesc[2 * (uint64_t)p + 1];
+        if (w0 >> 63) base = tin;
+        w0 &= ~(1ull << 63);
+      } else {
+        w0 = swo[p];
+        W64 = swo[p + 1] - w0;
+      }
+      bool bad = W64 >= (1ull << 31);
+      if ((bad || (hint && W64 > hint)) && threadIdx.x == 0) atomicOr(err, 1u);
+      const uint32_t W = bad ? 0u : (uint32_t)W64;  // (unsupported: sized 0, output undefined)
+      const uint64_t *pw = base + w0;
+      const uint32_t nch = (((W + 63) >> 6) + kSpCS - 1) / kSpCS;
+      int cnt = 0;
+      uint32_t Xlast = 0;
+      uint64_t wbefore = 0, total = 0, cbase = 0;
+      SpSt cst = {0u, 0u, 0u};
+      // one chunk: A1, A2, offset, B.  More: every chunk sized (pass 0),
+      // the offset, every chunk read again and emitted (pass 1).  One copy
+      // of each phase in the code (uniform branches).
+      const uint32_t iters = nch > 1 ? 2 * nch : 1;
+      for (uint32_t it = 0; it < iters; ++it) {
+        const bool emit = nch <= 1 || it >= nch;
+        const uint32_t c = nch > 1 ? (emit ? it - nch : it) : 0;
+        if (emit && c == 0) cst = SpSt{0u, 0u, 0u};
+        const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, cst, w, lane, emit, cnt, Xlast, wbefore);
+        if (!emit) {
+          total += ct;
+          continue;
+        }
+        if (c == 0) {
+          // ---- offset: look-back over the pieces before p ----
+          if (nch <= 1) total = ct;
+          if (w == 0) {
+            const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
+            if (lane == 0) {
+              scr[5] = excl;
+              out_off[p] = excl;
+              if (p + 1 == n) out_off[n] = excl + total;
+            }
+          }
+          __syncthreads();
+          cbase = sp_ld(&scr[5]);
+        }
+        if (cnt) sp_b(R, cnt, lut, ring, out, cbase + wbefore, lane, ocap);
+        cbase += ct;
+      }
+    }
+  }
+}
+
+// piece descriptors in message order (table, segments; next message) and the
+// tables' words (Serialize.java:256-273): message m's table goes to word
+// mseg[m] / 2 + m of tbuf (room for (count + 2) / 2 words)
+__global__ void sp_msg_prep_kernel(const uint64_t *__restrict__ swo, const uint64_t *__restrict__ mseg,
+                                   uint32_t nm, uint64_t *__restrict__ pdesc, uint64_t *__restrict__ tbuf,
+                                   uint64_t *__restrict__ ocap) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m == 0) {
+    // output bound: segments 9 w + 1 each, tables (<= nseg / 2 + nm words) likewise, + 16
+    const uint64_t nseg = mseg[nm];
+    *ocap = 9 * (swo[nseg] - swo[0]) + nseg + 9 * (nseg / 2 + nm) + nm + 16;
+  }
+  if (m >= nm) return;
+  const uint64_t s0 = mseg[m], s1 = mseg[m + 1];
+  const uint32_t count = (uint32_t)(s1 - s0);
+  const uint32_t tw = table_words(count);
+  const uint64_t to = s0 / 2 + m;
+  for (uint32_t k = 0; k < tw; ++k) tbuf[to + k] = table_word(swo, s0, count, k);
+  uint64_t *d = pdesc + 2 * (s0 + m);
+  d[0] = (1ull << 63) | to;
+  d[1] = tw;
+  for (uint64_t s = s0; s < s1; ++s) {
+    d[2 * (1 + s - s0)] = swo[s];
+    d[2 * (1 + s - s0) + 1] = swo[s + 1] - swo[s];
+  }
+}

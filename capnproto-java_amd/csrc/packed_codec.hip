@@ -990,6 +990,7 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 }
 
 #include "encode_v4.hip"
+#include "encode_sp.hip"
 
 }  // namespace cpk
 
@@ -1002,6 +1003,12 @@ struct cpk_ctx_s {
   uint64_t *status;       // look-back words
   uint64_t status_cap;    // entries
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
+  int encoder;            // 0: single pass (encode_sp.hip, default); 4: size + emit passes (CPK_ENCODER=4)
+  uint64_t *sp_status;    // single pass: look-back word per piece
+  uint64_t sp_cap;        //   entries
+  uint32_t sp_epoch;      //   launch epoch tagging the look-back words, 1..65535
+  uint64_t *sp_desc;      //   message batches: piece descriptors | segment tables
+  uint64_t sp_desc_cap;   //   u64 entries
   uint64_t *e4_bv;        // encoder v4: run boundaries per 64-word step
   uint64_t e4_bv_cap;     //   entries
   HostPipe *pipe;         // cpk_encode_host / cpk_decode_host staging (lazy)
@@ -1085,6 +1092,12 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
   cpk_ctx c = (cpk_ctx)calloc(1, sizeof(cpk_ctx_s));
   if (!c) return CPK_ENOMEM;
   c->device = device;
+  {
+    // CPK_ENCODER=0 selects the single-pass encoder (encode_sp.hip), 4 the
+    // two-pass one; the default is whichever measured faster
+    const char *e = getenv("CPK_ENCODER");
+    c->encoder = (e && e[0] == '0') ? 0 : 4;
+  }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
   if (hipMalloc(&c->tickets, cpk::kTkWords * 4) != hipSuccess ||
@@ -1108,11 +1121,54 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->status) hipFree(ctx->status);
   if (ctx->tickets) hipFree(ctx->tickets);
   if (ctx->e4_bv) hipFree(ctx->e4_bv);
+  if (ctx->sp_status) hipFree(ctx->sp_status);
+  if (ctx->sp_desc) hipFree(ctx->sp_desc);
   pipe_destroy(ctx->pipe);
   free(ctx);
 }
 
 int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
+
+// Single-pass encoder (encode_sp.hip): one launch, the look-back words
+// epoch-tagged (cleared only when the epoch wraps or the array grows).
+int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64_t *pdesc,
+              const uint64_t *tin, uint32_t n, uint64_t hint, void *d_out, uint64_t *d_out_off,
+              hipStream_t s) {
+  bool fresh = false;
+  if (n > ctx->sp_cap) {
+    if (ctx->sp_status) hipFree(ctx->sp_status);
+    ctx->sp_status = nullptr;
+    ctx->sp_cap = 0;
+    const uint64_t cap = n < 4096 ? 4096 : (uint64_t)n + n / 4;
+    if (hipMalloc(&ctx->sp_status, cap * 8) != hipSuccess) return CPK_ENOMEM;
+    ctx->sp_cap = cap;
+    fresh = true;
+  }
+  if (++ctx->sp_epoch > 0xffffu) {
+    ctx->sp_epoch = 1;
+    fresh = true;
+  }
+  if (fresh && hipMemsetAsync(ctx->sp_status, 0, ctx->sp_cap * 8, s) != hipSuccess) return CPK_EDEVICE;
+  if (hipMemsetAsync(ctx->tickets + cpk::kTkEnc, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
+  // one piece per ticket: a workgroup holding two pieces would publish the
+  // second's size only after emitting the first, and the pieces after it
+  // would wait on that (a serial chain through the tickets)
+  const uint32_t ppt = 1u;
+  unsigned grid = (unsigned)(CPK_SP_WPE * ctx->cus);
+  const uint64_t tickets = ((uint64_t)n + ppt - 1) / ppt;
+  if (grid > tickets) grid = (unsigned)tickets;
+  if (pdesc)
+    hipLaunchKernelGGL(cpk::sp_encode_kernel<true>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
+                       (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
+                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkEnc, ppt, hint,
+                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr);
+  else
+    hipLaunchKernelGGL(cpk::sp_encode_kernel<false>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
+                       (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
+                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkEnc, ppt, hint,
+                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr);
+  return hip_ok(hipGetLastError());
+}
 
 // Encoder v4 (encode_v4.hip): size pass, scan, emit pass.  Pieces of any
 // size; a piece over the hint is reported (output undefined).  The size pass
@@ -1174,6 +1230,24 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
   if (nm == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
   const uint64_t np = (uint64_t)nm + nseg;  // pieces: a table per message + the segments
   if (np > 0xffffffffull) return CPK_EINVAL;
+  if (ctx->encoder != 4) {
+    // single pass: piece descriptors in message order + the tables' words
+    const uint64_t need = 2 * np + (uint64_t)nseg / 2 + nm + 2;
+    if (need > ctx->sp_desc_cap) {
+      if (ctx->sp_desc) hipFree(ctx->sp_desc);
+      ctx->sp_desc = nullptr;
+      ctx->sp_desc_cap = 0;
+      const uint64_t cap = need + need / 4;
+      if (hipMalloc(&ctx->sp_desc, cap * 8) != hipSuccess) return CPK_ENOMEM;
+      ctx->sp_desc_cap = cap;
+    }
+    // pdesc[2 np] | output bound | tables
+    uint64_t *pdesc = ctx->sp_desc, *tbuf = ctx->sp_desc + 2 * np + 1;
+    const unsigned tb = 256, tg = (nm + tb - 1) / tb;
+    hipLaunchKernelGGL(cpk::sp_msg_prep_kernel, dim3(tg), dim3(tb), 0, s, d_swo, d_msg_seg_off, nm, pdesc,
+                       tbuf, tbuf - 1);
+    return sp_launch(ctx, d_in, nullptr, pdesc, tbuf, (uint32_t)np, max_seg_words, d_out, d_out_off, s);
+  }
   const uint32_t nb = (uint32_t)((np + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
   // scratch: segment sizes | table sizes | message-order sizes | segment offsets | block sums
   int rc = ensure_status(ctx, (uint64_t)nseg + nm + np + nseg + nb + 1);
@@ -1224,7 +1298,8 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
-  return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
+  if (ctx->encoder == 4) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
+  return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s);
 }
 
 int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {

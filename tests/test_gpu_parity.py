@@ -15,13 +15,25 @@ pytestmark = pytest.mark.gpu
 GOLD = json.loads((Path(__file__).parent / "golden" / "reference_kats.json").read_text())
 
 
-@pytest.fixture(scope="module")
-def ctx():
+@pytest.fixture(scope="module", params=["4", "0"], ids=["enc-two-pass", "enc-single-pass"])
+def ctx(request):
+    """A context per encoder (CPK_ENCODER is read at context creation): every
+    parity case runs through both the two-pass (encode_v4.hip) and the
+    single-pass (encode_sp.hip) encoder."""
+    import os
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     import capnp_packed as cp
-    c = cp.Context(0)
+    old = os.environ.get("CPK_ENCODER")
+    os.environ["CPK_ENCODER"] = request.param
+    try:
+        c = cp.Context(0)
+    finally:
+        if old is None:
+            os.environ.pop("CPK_ENCODER")
+        else:
+            os.environ["CPK_ENCODER"] = old
     yield c
     c.close()
 
@@ -343,7 +355,7 @@ def test_short_stretch_after_long(ctx, oracle):
     _check_batch(ctx, oracle, data, _swo([len(p) // 8 for p in pieces]))
 
 
-@pytest.mark.parametrize("enc", ["default"])
+@pytest.mark.parametrize("enc", ["default", "0", "4"])
 def test_every_encoder_matches_oracle(oracle, enc, monkeypatch):
     """Every encoder on one mixed batch: pieces of 0..20000 words, long D/L
     stretches, long zero runs."""

@@ -50,3 +50,34 @@ def test_state_at_equals_sequential_state():
             assert sm.state_at(masks, s, (0, False, 0)) == st, s
             _, Z, DL, D = masks[s]
             st = sm.roles(Z, DL, D, st)[3]
+
+
+@pytest.mark.parametrize("ws", [32, 5, 2])
+def test_parallel_roles_equal_sequential(oracle, ws):
+    """sp_a2p's ballot formulation (tools/step_model.roles_parallel) gives the
+    sequential roles on every wave it accepts, from any entry state."""
+    rng = np.random.default_rng(ws)
+    accepted = fallbacks = 0
+    pieces = [sm.rand_piece(rng, int(rng.integers(100, 4000))) for _ in range(8)]
+    for cfg in (2, 3, 4):
+        swo = np.array([0, 8192], dtype=np.uint64)
+        op = oracle.preset(cfg)
+        op.cfg = cfg | (ws << 8)
+        pieces.append(oracle.generate(op, swo).tobytes())
+    for d in pieces:
+        w = np.frombuffer(d, np.uint8).reshape(-1, 8)
+        tags = ((w != 0) * (1 << np.arange(8))).sum(1)
+        ns = (len(w) + 63) // 64
+        masks = [sm.step_masks(tags, len(w), s) for s in range(ns)]
+        for a in range(0, ns, ws):
+            st = sm.state_at(masks, a, (0, False, 0))
+            par = sm.roles_parallel(masks[a:a + ws], st)
+            if par is None:
+                fallbacks += 1
+                continue
+            accepted += 1
+            s2 = st
+            for j, (V, Z, DL, D) in enumerate(masks[a:a + ws]):
+                Zh, Mem, _, s2 = sm.roles(Z, DL, D, s2)
+                assert par[j] == (Zh, Mem), (a, j)
+    assert accepted > 10

@@ -18,13 +18,11 @@ for f in sorted(root.glob("*/*_counter_collection.csv")):
         for r in csv.DictReader(fh):
             k = r["Kernel_Name"]
             short = ("e4_size_kernel" if "e4_size_kernel" in k else "e4_emit_kernel" if "e4_emit_kernel" in k
-                     else "encode_kernel" if "encode_kernel" in k else "decode_kernel" if "decode_kernel" in k
-                     else "encode3_kernel" if "encode3_kernel" in k else "encode2_kernel" if "encode2_kernel" in k
-                     else k.split("(")[0][-40:])
+                     else "sp_encode_kernel" if "sp_encode_kernel" in k
+                     else "decode_kernel" if "decode_kernel" in k else k.split("(")[0][-40:])
             vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
-for kern in ("encode_kernel", "encode2_kernel", "encode3_kernel", "e4_size_kernel", "e4_emit_kernel",
-                 "decode_kernel"):
+for kern in ("sp_encode_kernel", "e4_size_kernel", "e4_emit_kernel", "decode_kernel"):
     if kern not in vals:
         continue
     d = {c: sum(v) / len(v) for c, v in vals[kern].items()}
@@ -44,7 +42,9 @@ for kern in ("encode_kernel", "encode2_kernel", "encode3_kernel", "e4_size_kerne
 if len(sys.argv) > 3 and sys.argv[2] == "--json":
     traffic = {}
     # the v4 encode stage = size pass + emit pass: their traffic adds up
-    if "e4_size_kernel" in out and "e4_emit_kernel" in out:
+    if "sp_encode_kernel" in out:
+        out["encode_kernel"] = out["sp_encode_kernel"]
+    elif "e4_size_kernel" in out and "e4_emit_kernel" in out:
         out["encode_kernel"] = {c: out["e4_size_kernel"].get(c, 0) + out["e4_emit_kernel"].get(c, 0)
                                 for c in ("FETCH_SIZE", "WRITE_SIZE")}
     for kern, key in (("encode_kernel", "encode"), ("decode_kernel", "decode")):

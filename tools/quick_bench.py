@@ -27,7 +27,7 @@ for spec in libs:
     # "lib.so@3:CPK_E3_RESERVE=0,CPK_DECODER=3": encoder 3 plus env knobs read at ctx creation
     lp, _, enc = spec.partition("@")
     enc, _, envs = enc.partition(":")
-    os.environ["CPK_ENCODER"] = enc or "1"
+    os.environ["CPK_ENCODER"] = enc or "0"
     for kv in filter(None, envs.split(",")):
         k, _, v = kv.partition("=")
         os.environ[k] = v

@@ -275,3 +275,48 @@ def rand_piece(rng, n):
                 x[rng.random(8) < 0.5] = 0
                 out.append(x)
     return np.concatenate(out[:n]).tobytes()
+
+
+def roles_parallel(wmasks, st):
+    """The lane-parallel form of a wave's roles (csrc/encode_sp.hip sp_a2p):
+    step j's Zh / Mem from its own masks plus ballots over the wave's steps.
+    wmasks: [(V, Z, DL, D)] of the wave's steps; st: state entering the first.
+    -> [(Zh, Mem)] or None when a D/L stretch over 192 words enters a step
+    (the kernel then runs the sequential form)."""
+    cnt = len(wmasks)
+    Zs = [m[1] for m in wmasks]
+    DLs = [m[2] for m in wmasks]
+    Ds = [m[3] for m in wmasks]
+    zl_in, dlo_in, hd_in = st
+    notall_dl = [DLs[j] != M64 for j in range(cnt)]
+    topdl = [64 if DLs[j] == M64 else clz(~DLs[j] & M64) for j in range(cnt)]
+    anyD = [Ds[j] != 0 for j in range(cnt)]
+    topd = [topdl[j] > 0 and (Ds[j] >> (64 - topdl[j])) != 0 for j in range(cnt)]
+    notall_z = [Zs[j] != M64 for j in range(cnt)]
+    topz = [64 if Zs[j] == M64 else clz(~Zs[j] & M64) for j in range(cnt)]
+    out = []
+    for j in range(cnt):
+        Z, DL, D = Zs[j], DLs[j], Ds[j]
+        dlo = (DLs[j - 1] >> 63) & 1 if j else (1 if dlo_in else 0)
+        kd = max([k for k in range(j) if notall_dl[k]], default=-1)
+        ln = topdl[kd] + 64 * (j - 1 - kd) if kd >= 0 else (hd_in if dlo_in else 0) + 64 * j
+        cont = dlo and (DL & 1)
+        if cont and ln > 192:
+            return None
+        btw = any(anyD[k] for k in range(kd + 1, j))
+        head = btw or (topd[kd] if kd >= 0 else bool(dlo_in and hd_in))
+        cin = 1 if (cont and head) else 0
+        A = (((D << 1) & M64) | cin) & DL
+        C = ((DL + A) ^ DL ^ A) & M64
+        Mem = DL & (A | C)
+        zc = (Zs[j - 1] >> 63) & 1 if j else (1 if zl_in else 0)
+        Zh = Z & ~(((Z << 1) | zc) & M64)
+        kz = max([k for k in range(j) if notall_z[k]], default=-1)
+        zl = topz[kz] + 64 * (j - 1 - kz) if kz >= 0 else zl_in + 64 * j
+        j0 = (256 - (zl & 255)) & 255
+        if zc and (Z & 1) and j0 < 64:
+            pre = (2 << j0) - 1
+            if Z & pre == pre:
+                Zh |= 1 << j0
+        out.append((Zh, Mem))
+    return out
