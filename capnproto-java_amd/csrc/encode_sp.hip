@@ -38,10 +38,12 @@ constexpr uint32_t kSpoLut = 0;                                      // u64[256]
 constexpr uint32_t kSpoMsk = 2048;                                   // u64[kSpCS][3]
 constexpr uint32_t kSpoRing = kSpoMsk + kSpCS * 24;                  // per wave
 constexpr uint32_t kSpoScr = kSpoRing + kSpWaves * kSpRingStride;    // u64[16]
-constexpr uint32_t kSpLds = kSpoScr + 16 * 8;                        // 13,504 B
+constexpr uint32_t kSpoBuf = kSpoScr + 16 * 8;                      // staging: one chunk
+constexpr uint32_t kSpLds = kSpoBuf + kSpCS * 64 * 8;                // 79,040 B: 2 per CU
 static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 // scratch words: [0] ticket, [1..4] wave bytes, [5] piece offset,
-// [6..9] chunk exit state (two parities x {zl, dlo | hd << 1})
+// [6..9] chunk exit state (two parities x {zl, dlo | hd << 1}), [10] the runs
+// continuing past the chunk's end (zero | D/L << 16)
 // Steps are scheduled one at a time: hoisting later steps' LUT reads and
 // lane reads ahead would keep them all live at once (VGPR spills).
 #ifndef CPK_SP_FENCE
@@ -237,15 +239,24 @@ struct SpRegs {
   uint32_t ox;                                         //   X: words past the step to the next run end
 };
 
-// A1: the wave's cnt steps at src (wrem piece words from src on); returns
-// this lane's nonzero-byte count
-__device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict__ src, uint32_t wrem,
-                                          int cnt, int lane) {
-  // loads clamped to the piece, not predicated: step j's lanes read
-  // min(lane, last valid lane of the step) (one lane register for all steps)
+// A1: the wave's cnt steps (wrem piece words from its first word on), staged
+// in LDS at stg (word i of the wave at stg[i]; the LDS-DMA of the previous
+// phase put them there); returns this lane's nonzero-byte count.  lastw:
+// the piece's last word when the DMA could not fetch it (an odd word count:
+// 16-byte pieces), fetched here by its lane.
+__device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *stg, const uint64_t *__restrict__ gsrc,
+                                          uint32_t wrem, int cnt, int lane) {
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j)
-    if (j < cnt) R.v[j] = (src + j * 64)[min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))];
+    if (j < cnt) R.v[j] = stg[j * 64 + lane];
+  if ((wrem & 1) && wrem <= 64u * kSpWS) {
+    // (wrem <= the wave's words: the piece ends in this wave)
+    const uint32_t k = wrem - 1;
+    const uint64_t x = (uint32_t)lane == (k & 63) ? gsrc[k] : 0ull;
+#pragma unroll
+    for (int j = 0; j < kSpWS; ++j)
+      if ((uint32_t)j == (k >> 6) && (uint32_t)lane == (k & 63)) R.v[j] = x;
+  }
   uint32_t acc = 0;
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j) {
@@ -287,7 +298,7 @@ __device__ __forceinline__ void sp_put_masks(const SpRegs &R, uint64_t *msk, int
 // their nonzero bytes.  nz0 / ndl0: bit 0 of the step after the wave's last.
 // Used when a D/L stretch longer than 192 words enters a step (a literal run
 // may end inside it); sp_a2p otherwise.
-__device__ uint32_t sp_a2_seq(SpRegs &R, int cnt, uint32_t wrem, SpSt st, uint32_t nz0, uint32_t ndl0) {
+__device__ __forceinline__ uint32_t sp_a2_seq(SpRegs &R, int cnt, uint32_t wrem, SpSt st, uint32_t nz0, uint32_t ndl0) {
   uint32_t bytes = 0;
   for (int j = 0; j < cnt; ++j) {
     const uint64_t Z = sp_rl(R.zl, R.zh, j), DL = sp_rl(R.dll, R.dlh, j), D = sp_rl(R.dl_, R.dh_, j);
@@ -628,77 +639,58 @@ __device__ __forceinline__ SpSt sp_get_state(const uint64_t *scr, int par) {
   return s;
 }
 
-// One chunk's A1 + A2 for this wave (all waves call it; two barriers).
-// Returns the chunk's packed bytes (all waves); wbefore: bytes of the waves
-// before this one.  cst: the state entering the chunk -> leaving it.
-__device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restrict__ pw, uint32_t W,
-                                             uint32_t c, uint64_t *msk, uint64_t *scr, SpSt &cst,
-                                             int w, int lane, bool kEmit, int &cnt, uint32_t &Xlast,
-                                             uint64_t &wbefore) {
-  const uint32_t ns = (W + 63) >> 6;
-  const uint32_t cs0 = c * kSpCS;
-  const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
-  const int sa = w * kSpWS;
-  cnt = max(0, min(kSpWS, cs - sa));
-  const uint32_t wfirst = (cs0 + (uint32_t)sa) * 64;  // the wave's first word
-  const uint32_t wrem = cnt ? W - wfirst : 0;
-  uint32_t acc = 0;
-  if (cnt) {
-    acc = sp_a1(R, pw + wfirst, wrem, cnt, lane);
-    sp_put_masks(R, msk, sa, cnt, lane);
-  }
-  __syncthreads();  // the chunk's masks in LDS
-  SpSt st = cst;
-  uint32_t bytes = 0;
-  const bool last = cnt && sa + cnt == cs;  // this wave holds the chunk's last step
-  if (cnt) {
-    st = sp_state_at(msk, sa, cst);
-    uint32_t nz0 = 0, ndl0 = 0;
-    Xlast = 0;
-    if (kEmit) {
-      // the step after the wave's last: in the chunk, or past it (look-ahead)
-      uint32_t laz = 0, ladl = 0;
-      const uint32_t wend = wfirst + 64u * cnt;
-      if (last && wend < W) sp_lookahead(pw + wend, W - wend, lane, laz, ladl);
-      if (sa + cnt < cs) {
-        nz0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt)]) & 1u;
-        ndl0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt) + 1]) & 1u;
-      } else {
-        nz0 = laz ? 1u : 0u;
-        ndl0 = ladl ? 1u : 0u;
-      }
-      const uint64_t Zl = sp_rl(R.zl, R.zh, cnt - 1), DLl = sp_rl(R.dll, R.dlh, cnt - 1);
-      const int cls = (Zl >> 63) ? 0 : ((DLl >> 63) ? 1 : -1);
-      if (cls >= 0) {
-        const uint32_t r = sp_cont(msk, sa + cnt, cs, cls, cls ? ladl : laz);
-        Xlast = r ? r - 1 : 0;
-      }
-    }
-    uint32_t rb = 0;
-    if (!sp_a2p(R, cnt, wrem, st, nz0, ndl0, lane, rb)) rb = sp_a2_seq(R, cnt, wrem, st, nz0, ndl0);
-    if (kEmit) sp_xs(R, cnt, Xlast, lane);
-    bytes = rb + (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)acc), 63);
-  }
-  if (last) st = sp_state_at(msk, cs, cst);  // the state leaving the chunk
-  if (lane == 0) {
-    scr[1 + w] = bytes;
-    if (last) {
-      scr[6 + 2 * (c & 1)] = st.zl;
-      scr[7 + 2 * (c & 1)] = (uint64_t)st.dlo | ((uint64_t)st.hd << 1);
-    }
-  }
-  __syncthreads();  // wave bytes and the exit state in LDS
-  uint64_t tot = 0;
-  wbefore = 0;
-#pragma unroll
-  for (int q = 0; q < kSpWaves; ++q) {
-    const uint64_t b = sp_ld(&scr[1 + q]);
-    if (q < w) wbefore += b;
-    tot += b;
-  }
-  cst = sp_get_state(scr, c & 1);
-  return tot;
+// ---- LDS-DMA staging of the next chunk ----------------------------------------
+// A chunk's words go global -> LDS by global_load_lds_dwordx4 (1 KiB per wave
+// instruction, no VGPRs), issued by waves 1-3 as soon as the previous chunk
+// has been read out of the buffer, so the load overlaps that chunk's roles,
+// look-back and emission.  Wave 0 issues none: it does the look-back, whose
+// global loads would otherwise wait (vmcnt) for its DMA.  Barriers while a
+// DMA is in flight are raw s_barrier + lgkmcnt(0) (__syncthreads would drain
+// vmcnt).
+__device__ __forceinline__ void sp_bar() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
 }
+__device__ __forceinline__ void sp_stage(const uint64_t *__restrict__ cw, uint32_t wc, uint8_t *buf, int w,
+                                         int lane) {
+  // chunk words [0, wc) -> buf; 16-byte pieces, the whole ones only (an odd
+  // last word is fetched by A1)
+  if (w == 0) return;
+  const uint32_t blocks = (wc + 127) >> 7;
+  for (uint32_t b = (uint32_t)w - 1; b < blocks; b += kSpWaves - 1) {
+    const uint32_t k = b * 128 + 2 * (uint32_t)lane;
+    if (k + 2 <= wc)
+      __builtin_amdgcn_global_load_lds((const void *)(cw + k),
+                                       (void __attribute__((address_space(3))) *)(buf + b * 1024), 16, 0, 0);
+  }
+}
+
+struct SpPiece {
+  const uint64_t *pw;  // first word
+  uint32_t W;          // words (0 for an unsupported piece: error flagged)
+};
+template <bool kMsg>
+__device__ __forceinline__ SpPiece sp_piece_desc(const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo,
+                                                 const uint64_t *__restrict__ pdesc,
+                                                 const uint64_t *__restrict__ tin, uint32_t p, uint64_t hint,
+                                                 uint32_t *err, bool report) {
+  uint64_t w0, W64;
+  const uint64_t *base = in;
+  if (kMsg) {
+    w0 = pdesc[2 * (uint64_t)p];
+    W64 = pdesc[2 * (uint64_t)p + 1];
+    if (w0 >> 63) base = tin;
+    w0 &= ~(1ull << 63);
+  } else {
+    w0 = swo[p];
+    W64 = swo[p + 1] - w0;
+  }
+  const bool bad = W64 >= (1ull << 31);
+  if (report && (bad || (hint && W64 > hint)) && threadIdx.x == 0) atomicOr(err, 1u);
+  SpPiece d = {base + w0, bad ? 0u : (uint32_t)W64};  // (unsupported: sized 0, output undefined)
+  return d;
+}
+__device__ __forceinline__ uint32_t sp_nch(uint32_t W) { return (((W + 63) >> 6) + kSpCS - 1) / kSpCS; }
 
 // kMsg = false: piece p is words [swo[p], swo[p+1]) of `in`.  kMsg = true:
 // pdesc[2p] = first word (bit 63: of `tin`, the segment tables) and
@@ -716,6 +708,7 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kSpoLut);
   uint64_t *msk = reinterpret_cast<uint64_t *>(smem + kSpoMsk);
   uint64_t *scr = reinterpret_cast<uint64_t *>(smem + kSpoScr);
+  uint8_t *buf = smem + kSpoBuf;
   const int lane0 = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kSpoRing + w * kSpRingStride);
@@ -724,55 +717,135 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
   SpRegs R;
   R.zl = R.zh = R.dll = R.dlh = R.dl_ = R.dh_ = 0;
-  R.ozl = R.ozh = R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = 0;
-  for (;;) {
-    if (threadIdx.x == 0) scr[0] = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t t = (uint32_t)sp_ld(&scr[0]);
-    __syncthreads();  // (scr[0] read by all before the next ticket)
-    const uint64_t pfirst = (uint64_t)t * ppt;
-    if (pfirst >= n) break;
-    const uint32_t plast = (uint32_t)min(pfirst + ppt, (uint64_t)n);
-    for (uint32_t p = (uint32_t)pfirst; p < plast; ++p) {
-      // an opaque copy of the lane id: nothing lane-dependent is hoisted out
-      // of the piece loop into registers that stay live across it
-      int lane = lane0;
-      asm volatile("" : "+v"(lane));
-      uint64_t w0, W64;
-      const uint64_t *base = in;
-      if (kMsg) {
-        w0 = pdesc[2 * (uint64_t)p];
-        W64 = pdesc[2 * (uint64_t)p + 1];
-        if (w0 >> 63) base = tin;
-        w0 &= ~(1ull << 63);
-      } else {
-        w0 = swo[p];
-        W64 = swo[p + 1] - w0;
+  R.ozl = R.ozh = R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = R.ox = 0;
+  (void)ppt;
+  // the first piece: ticket, staged synchronously
+  if (threadIdx.x == 0) scr[0] = atomicAdd(ticket, 1u);
+  __syncthreads();
+  uint32_t p = (uint32_t)sp_ld(&scr[0]);
+  SpPiece cur = {nullptr, 0u};
+  if (p < n) {
+    cur = sp_piece_desc<kMsg>(in, swo, pdesc, tin, p, hint, err, true);
+    sp_stage(cur.pw, min(cur.W, (uint32_t)(kSpCS * 64)), buf, w, lane0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  WPH_INIT
+  while (p < n) {
+    // an opaque copy of the lane id: nothing lane-dependent is hoisted out
+    // of the piece loop into registers that stay live across it
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const uint32_t W = cur.W;
+    const uint32_t ns = (W + 63) >> 6;
+    const uint32_t nch = sp_nch(W);
+    // one chunk: A1, A2, offset, B.  More: every chunk sized (pass 0), the
+    // offset, every chunk read again and emitted (pass 1)
+    const uint32_t iters = nch > 1 ? 2 * nch : 1;
+    uint64_t total = 0, cbase = 0;
+    SpSt cst = {0u, 0u, 0u};
+    uint32_t q = n;  // the next piece
+    SpPiece nxt = {nullptr, 0u};
+    for (uint32_t it = 0; it < iters; ++it) {
+      const bool emit = nch <= 1 || it >= nch;
+      const uint32_t c = nch > 1 ? (emit ? it - nch : it) : 0;
+      if (emit && c == 0) cst = SpSt{0u, 0u, 0u};
+      const uint32_t cs0 = c * kSpCS;
+      const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
+      const int sa = w * kSpWS;
+      const int cnt = max(0, min(kSpWS, cs - sa));
+      const uint32_t wfirst = (cs0 + (uint32_t)sa) * 64;  // the wave's first word
+      const uint32_t wrem = cnt ? W - wfirst : 0;
+      const uint32_t cend = (cs0 + (uint32_t)cs) * 64;    // the chunk's end (piece word)
+      // ---- A1 (this chunk is staged in buf) ----
+      WPH(7)
+      uint32_t acc = 0;
+      if (cnt) {
+        acc = sp_a1(R, reinterpret_cast<const uint64_t *>(buf) + (uint32_t)sa * 64, cur.pw + wfirst, wrem, cnt,
+                    lane);
+        sp_put_masks(R, msk, sa, cnt, lane);
       }
-      bool bad = W64 >= (1ull << 31);
-      if ((bad || (hint && W64 > hint)) && threadIdx.x == 0) atomicOr(err, 1u);
-      const uint32_t W = bad ? 0u : (uint32_t)W64;  // (unsupported: sized 0, output undefined)
-      const uint64_t *pw = base + w0;
-      const uint32_t nch = (((W + 63) >> 6) + kSpCS - 1) / kSpCS;
-      int cnt = 0;
-      uint32_t Xlast = 0;
-      uint64_t wbefore = 0, total = 0, cbase = 0;
-      SpSt cst = {0u, 0u, 0u};
-      // one chunk: A1, A2, offset, B.  More: every chunk sized (pass 0),
-      // the offset, every chunk read again and emitted (pass 1).  One copy
-      // of each phase in the code (uniform branches).
-      const uint32_t iters = nch > 1 ? 2 * nch : 1;
-      for (uint32_t it = 0; it < iters; ++it) {
-        const bool emit = nch <= 1 || it >= nch;
-        const uint32_t c = nch > 1 ? (emit ? it - nch : it) : 0;
-        if (emit && c == 0) cst = SpSt{0u, 0u, 0u};
-        const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, cst, w, lane, emit, cnt, Xlast, wbefore);
-        if (!emit) {
-          total += ct;
-          continue;
+      if (w == 0 && emit && cend < W) {
+        // the zero run / D/L stretch continuing past the chunk's end
+        uint32_t laz, ladl;
+        sp_lookahead(cur.pw + cend, W - cend, lane, laz, ladl);
+        if (lane == 0) scr[10] = laz | (ladl << 16);
+      }
+      WPH(0)
+      if (it + 1 == iters && threadIdx.x == 0) scr[0] = atomicAdd(ticket, 1u);
+      sp_bar();  // the masks in LDS; buf read out; the next ticket
+      WPH(1)
+      // ---- stage the next chunk (this piece's, or the next piece's first) ----
+      if (it + 1 < iters) {
+        const uint32_t c2 = nch > 1 ? (it + 1 >= nch ? it + 1 - nch : it + 1) : 0;
+        sp_stage(cur.pw + c2 * (uint32_t)(kSpCS * 64), min(W - c2 * (uint32_t)(kSpCS * 64), (uint32_t)(kSpCS * 64)),
+                 buf, w, lane);
+      } else {
+        q = (uint32_t)sp_ld(&scr[0]);
+        if (q < n) {
+          nxt = sp_piece_desc<kMsg>(in, swo, pdesc, tin, q, hint, err, true);
+          sp_stage(nxt.pw, min(nxt.W, (uint32_t)(kSpCS * 64)), buf, w, lane);
         }
+      }
+      // ---- A2 ----
+      WPH(2)
+      uint32_t bytes = 0, Xlast = 0;
+      SpSt st = cst;
+      const bool last = cnt && sa + cnt == cs;  // this wave holds the chunk's last step
+      if (cnt) {
+        st = sp_state_at(msk, sa, cst);
+        uint32_t nz0 = 0, ndl0 = 0;
+        if (emit) {
+          // the step after the wave's last: in the chunk, or past it
+          uint32_t laz = 0, ladl = 0;
+          if (last && cend < W) {
+            const uint32_t la = (uint32_t)sp_ld(&scr[10]);
+            laz = la & 0xffffu;
+            ladl = la >> 16;
+          }
+          if (sa + cnt < cs) {
+            nz0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt)]) & 1u;
+            ndl0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt) + 1]) & 1u;
+          } else {
+            nz0 = laz ? 1u : 0u;
+            ndl0 = ladl ? 1u : 0u;
+          }
+          const uint64_t Zl = sp_rl(R.zl, R.zh, cnt - 1), DLl = sp_rl(R.dll, R.dlh, cnt - 1);
+          const int cls = (Zl >> 63) ? 0 : ((DLl >> 63) ? 1 : -1);
+          if (cls >= 0) {
+            const uint32_t r = sp_cont(msk, sa + cnt, cs, cls, cls ? ladl : laz);
+            Xlast = r ? r - 1 : 0;
+          }
+        }
+        uint32_t rb = 0;
+        if (!sp_a2p(R, cnt, wrem, st, nz0, ndl0, lane, rb)) rb = sp_a2_seq(R, cnt, wrem, st, nz0, ndl0);
+        if (emit) sp_xs(R, cnt, Xlast, lane);
+        bytes = rb + (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)acc), 63);
+      }
+      if (last) st = sp_state_at(msk, cs, cst);  // the state leaving the chunk
+      if (lane == 0) {
+        scr[1 + w] = bytes;
+        if (last) {
+          scr[6 + 2 * (c & 1)] = st.zl;
+          scr[7 + 2 * (c & 1)] = (uint64_t)st.dlo | ((uint64_t)st.hd << 1);
+        }
+      }
+      WPH(3)
+      sp_bar();  // wave bytes and the exit state
+      WPH(4)
+      uint64_t ct = 0, wbefore = 0;
+#pragma unroll
+      for (int k = 0; k < kSpWaves; ++k) {
+        const uint64_t b = sp_ld(&scr[1 + k]);
+        if (k < w) wbefore += b;
+        ct += b;
+      }
+      cst = sp_get_state(scr, c & 1);
+      if (!emit) {
+        total += ct;
+      } else {
         if (c == 0) {
-          // ---- offset: look-back over the pieces before p ----
+          // ---- offset: look-back over the pieces before p (wave 0: no DMA in flight) ----
           if (nch <= 1) total = ct;
           if (w == 0) {
             const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
@@ -782,14 +855,22 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
               if (p + 1 == n) out_off[n] = excl + total;
             }
           }
-          __syncthreads();
+          sp_bar();
           cbase = sp_ld(&scr[5]);
         }
+        WPH(5)
+        // ---- B ----
         if (cnt) sp_b(R, cnt, lut, ring, out, cbase + wbefore, lane, ocap);
         cbase += ct;
+        WPH(6)
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
+      sp_bar();                                           // ... and every wave's
     }
+    p = q;
+    cur = nxt;
   }
+  WPH_FLUSH(32)
 }
 
 // piece descriptors in message order (table, segments; next message) and the
