@@ -31,19 +31,18 @@ constexpr int kSpWaves = 4;
 constexpr int kSpThreads = 64 * kSpWaves;
 constexpr int kSpWS = 32;                      // steps per wave
 constexpr int kSpCS = kSpWaves * kSpWS;        // steps per chunk (8192 words)
-constexpr uint32_t kSpRing = 2048;             // output ring per wave (bytes)
+constexpr uint32_t kSpRing = 8192;             // output ring per wave (bytes)
 constexpr uint32_t kSpRingLines = kSpRing / 16;
 constexpr uint32_t kSpRingStride = kSpRing + 16;  // + one overhang line (line 0's spill)
 constexpr uint32_t kSpoLut = 0;                                      // u64[256]
 constexpr uint32_t kSpoMsk = 2048;                                   // u64[kSpCS][3]
 constexpr uint32_t kSpoRing = kSpoMsk + kSpCS * 24;                  // per wave
 constexpr uint32_t kSpoScr = kSpoRing + kSpWaves * kSpRingStride;    // u64[16]
-constexpr uint32_t kSpoBuf = kSpoScr + 16 * 8;                      // staging: one chunk
-constexpr uint32_t kSpLds = kSpoBuf + kSpCS * 64 * 8;                // 79,040 B: 2 per CU
+constexpr uint32_t kSpLds = kSpoScr + 16 * 8;                        // 37,504 B
 static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 // scratch words: [0] ticket, [1..4] wave bytes, [5] piece offset,
-// [6..9] chunk exit state (two parities x {zl, dlo | hd << 1}), [10] the runs
-// continuing past the chunk's end (zero | D/L << 16)
+// [6..9] chunk exit state (two parities x {zl, dlo | hd << 1}), [11] the piece
+// (+ 1) whose offset [5] holds
 // Steps are scheduled one at a time: hoisting later steps' LUT reads and
 // lane reads ahead would keep them all live at once (VGPR spills).
 #ifndef CPK_SP_FENCE
@@ -55,7 +54,7 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #define CPK_SP_STEP_FENCE()
 #endif
 #ifndef CPK_SP_WPE
-#define CPK_SP_WPE 2  // waves per SIMD the registers must allow (2 workgroups per CU)
+#define CPK_SP_WPE 3  // waves per SIMD the registers must allow (3 workgroups per CU)
 #endif
 
 // status word per piece: [63:62] flag (1 aggregate, 2 inclusive prefix),
@@ -239,24 +238,15 @@ struct SpRegs {
   uint32_t ox;                                         //   X: words past the step to the next run end
 };
 
-// A1: the wave's cnt steps (wrem piece words from its first word on), staged
-// in LDS at stg (word i of the wave at stg[i]; the LDS-DMA of the previous
-// phase put them there); returns this lane's nonzero-byte count.  lastw:
-// the piece's last word when the DMA could not fetch it (an odd word count:
-// 16-byte pieces), fetched here by its lane.
-__device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *stg, const uint64_t *__restrict__ gsrc,
-                                          uint32_t wrem, int cnt, int lane) {
+// A1: the wave's cnt steps at src (wrem piece words from src on); returns
+// this lane's nonzero-byte count
+__device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict__ src, uint32_t wrem,
+                                          int cnt, int lane) {
+  // loads clamped to the piece, not predicated: step j's lanes read
+  // min(lane, last valid lane of the step) (one lane register for all steps)
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j)
-    if (j < cnt) R.v[j] = stg[j * 64 + lane];
-  if ((wrem & 1) && wrem <= 64u * kSpWS) {
-    // (wrem <= the wave's words: the piece ends in this wave)
-    const uint32_t k = wrem - 1;
-    const uint64_t x = (uint32_t)lane == (k & 63) ? gsrc[k] : 0ull;
-#pragma unroll
-    for (int j = 0; j < kSpWS; ++j)
-      if ((uint32_t)j == (k >> 6) && (uint32_t)lane == (k & 63)) R.v[j] = x;
-  }
+    if (j < cnt) R.v[j] = (src + j * 64)[min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))];
   uint32_t acc = 0;
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j) {
@@ -424,16 +414,18 @@ __device__ __forceinline__ void sp_xs(SpRegs &R, int cnt, uint32_t Xlast, int la
 }
 
 // ---- the output ring -----------------------------------------------------------
-// Line L of the piece's output lives at ring line L % 128; a string crossing
-// the ring's end spills into the overhang line, which belongs to line 0.
-__device__ __forceinline__ uint4 sp_take_line(uint32_t *ring, uint64_t L) {
-  uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kSpRingLines - 1));
-  uint4 v = *rl;
-  *rl = make_uint4(0u, 0u, 0u, 0u);
-  if ((L & (kSpRingLines - 1)) == 0) {
-    uint4 *ov = reinterpret_cast<uint4 *>(ring) + kSpRingLines;
-    const uint4 o = *ov;
-    *ov = make_uint4(0u, 0u, 0u, 0u);
+// A wave lays its strings out relative to its first output byte: relative
+// line i (bytes [16 i, 16 i + 16)) lives at ring line i % kSpRingLines; a
+// string crossing the ring's end spills into the overhang line, which belongs
+// to ring line 0.  Its offset g0 in the output may not be known yet (the
+// look-back): the flush shifts relative lines onto the global ones -- global
+// line (g0 >> 4) + t holds relative bytes [16 t - k, 16 t - k + 16), k = g0 & 15,
+// i.e. the last k bytes of relative line t - 1 and the first 16 - k of line t.
+__device__ __forceinline__ uint4 sp_ring_line(const uint32_t *ring, uint32_t i) {
+  const uint4 *rl = reinterpret_cast<const uint4 *>(ring);
+  uint4 v = rl[i & (kSpRingLines - 1)];
+  if ((i & (kSpRingLines - 1)) == 0) {
+    const uint4 o = rl[kSpRingLines];
     v.x |= o.x;
     v.y |= o.y;
     v.z |= o.z;
@@ -441,56 +433,93 @@ __device__ __forceinline__ uint4 sp_take_line(uint32_t *ring, uint64_t L) {
   }
   return v;
 }
-// bytes [j0, j1) of line L (a line shared with a neighbour's bytes)
-__device__ __forceinline__ void sp_store_bytes(uint8_t *out, uint32_t *ring, uint64_t L, int j0, int j1,
-                                               int lane, uint64_t ocap) {
-  const uint4 *rl = reinterpret_cast<const uint4 *>(ring) + (L & (kSpRingLines - 1));
-  uint4 val = *rl;
-  if ((L & (kSpRingLines - 1)) == 0) {
-    const uint4 o = reinterpret_cast<const uint4 *>(ring)[kSpRingLines];
-    val.x |= o.x;
-    val.y |= o.y;
-    val.z |= o.z;
-    val.w |= o.w;
-  }
-  if (lane >= j0 && lane < j1 && L * 16 + lane < ocap) {
-    const uint32_t d = (lane & 8) ? ((lane & 4) ? val.w : val.z) : ((lane & 4) ? val.y : val.x);
-    out[L * 16 + lane] = (uint8_t)(d >> (8 * (lane & 3)));
-  }
-  wave_lds_order();
-  if (lane == 0) sp_take_line(ring, L);
-  wave_lds_order();
+__device__ __forceinline__ void sp_ring_clear(uint32_t *ring, uint32_t i) {
+  uint4 *rl = reinterpret_cast<uint4 *>(ring);
+  rl[i & (kSpRingLines - 1)] = make_uint4(0u, 0u, 0u, 0u);
+  if ((i & (kSpRingLines - 1)) == 0) rl[kSpRingLines] = make_uint4(0u, 0u, 0u, 0u);
 }
-// stores the complete lines [fl, upto); bytes below lo are a neighbour's
+// global line (g0 >> 4) + t from relative lines t - 1 and t
+__device__ __forceinline__ uint4 sp_gline(const uint32_t *ring, uint32_t t, uint32_t k) {
+  const uint4 b = sp_ring_line(ring, t);
+  if (k == 0) return b;
+  const uint4 a = t ? sp_ring_line(ring, t - 1) : make_uint4(0u, 0u, 0u, 0u);
+  // (a || b)[16 - k .. 32 - k)
+  const uint32_t q = 16u - k, s = q & 3;
+  uint4 r;
+  switch (q >> 2) {
+    case 0:
+      r = make_uint4(__builtin_amdgcn_alignbyte(a.y, a.x, s), __builtin_amdgcn_alignbyte(a.z, a.y, s),
+                     __builtin_amdgcn_alignbyte(a.w, a.z, s), __builtin_amdgcn_alignbyte(b.x, a.w, s));
+      break;
+    case 1:
+      r = make_uint4(__builtin_amdgcn_alignbyte(a.z, a.y, s), __builtin_amdgcn_alignbyte(a.w, a.z, s),
+                     __builtin_amdgcn_alignbyte(b.x, a.w, s), __builtin_amdgcn_alignbyte(b.y, b.x, s));
+      break;
+    case 2:
+      r = make_uint4(__builtin_amdgcn_alignbyte(a.w, a.z, s), __builtin_amdgcn_alignbyte(b.x, a.w, s),
+                     __builtin_amdgcn_alignbyte(b.y, b.x, s), __builtin_amdgcn_alignbyte(b.z, b.y, s));
+      break;
+    default:
+      r = make_uint4(__builtin_amdgcn_alignbyte(b.x, a.w, s), __builtin_amdgcn_alignbyte(b.y, b.x, s),
+                     __builtin_amdgcn_alignbyte(b.z, b.y, s), __builtin_amdgcn_alignbyte(b.w, b.z, s));
+      break;
+  }
+  return r;
+}
+// bytes [j0, j1) of global line (g0 >> 4) + t (a line shared with a neighbour)
 // (ocap: a bound on the output buffer -- stores past it are dropped, so a
 // corrupted offset cannot fault the device)
-__device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t &fl, uint64_t upto,
-                                         uint64_t lo, int lane, uint64_t ocap) {
-  if (fl >= upto) return;
-  if (fl * 16 < lo) {
-    sp_store_bytes(out, ring, fl, (int)(lo - fl * 16), 16, lane, ocap);
-    ++fl;
+__device__ __forceinline__ void sp_store_bytes(uint8_t *out, const uint32_t *ring, uint64_t g0, uint32_t t,
+                                               int j0, int j1, int lane, uint64_t ocap) {
+  const uint4 val = sp_gline(ring, t, (uint32_t)(g0 & 15));
+  const uint64_t a = ((g0 >> 4) + t) * 16 + (uint32_t)lane;
+  if (lane >= j0 && lane < j1 && a < ocap) {
+    const uint32_t d = (lane & 8) ? ((lane & 4) ? val.w : val.z) : ((lane & 4) ? val.y : val.x);
+    out[a] = (uint8_t)(d >> (8 * (lane & 3)));
   }
-  for (uint64_t L0 = fl; L0 < upto; L0 += 64) {
-    const uint64_t L = L0 + lane;
-    if (L < upto) {
-      const uint4 v = sp_take_line(ring, L);
-      if (L * 16 + 16 <= ocap) *reinterpret_cast<uint4 *>(out + L * 16) = v;
+}
+// the complete global lines [ft, upto) (relative numbering t); their
+// relative lines before the last are cleared
+__device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t g0, uint32_t &ft, uint32_t upto,
+                                         int lane, uint64_t ocap) {
+  if (ft >= upto) return;
+  const uint32_t k = (uint32_t)(g0 & 15);
+  const uint64_t L0 = g0 >> 4;
+  if (ft == 0 && k) {
+    // the first line holds the previous wave's / piece's bytes below k
+    sp_store_bytes(out, ring, g0, 0, (int)k, 16, lane, ocap);
+    ft = 1;
+  }
+  for (uint32_t t0 = ft; t0 < upto; t0 += 64) {
+    const uint32_t t = t0 + (uint32_t)lane;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (t < upto) v = sp_gline(ring, t, k);
+    wave_lds_order();
+    if (t < upto) {
+      if ((L0 + t) * 16 + 16 <= ocap) *reinterpret_cast<uint4 *>(out + (L0 + t) * 16) = v;
+      if (t) sp_ring_clear(ring, t - 1);
     }
+    wave_lds_order();
   }
-  fl = upto;
+  ft = upto;
 }
 
-// B: the wave's strings from output byte obase on.  Xlast: words past the
-// wave's last step to the first run end after it, minus one (<= 255).
-__device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut,
-                                     uint32_t *ring, uint8_t *out, uint64_t obase, int lane,
-                                     uint64_t ocap) {
-  uint64_t rpos = obase, fl = obase >> 4;
+// B: the wave's strings, laid out relative to its first output byte.  Its
+// offset is given (known) or fetched once kSpDefer steps are in the ring
+// (getbase: wave 0 runs the piece's look-back meanwhile -- the other waves
+// have had that many steps of work before they wait for it).
+#ifndef CPK_SP_DEFER
+#define CPK_SP_DEFER 12  // steps laid out before the offset is needed (12 x 640 B < kSpRing)
+#endif
+constexpr int kSpDefer = CPK_SP_DEFER;
+static_assert(kSpDefer * 640 + 16 <= (int)kSpRing, "deferred steps must fit the ring");
+template <class GetBase>
+__device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, uint32_t *ring, uint8_t *out,
+                                     bool known, uint64_t g0, int lane, uint64_t ocap, GetBase getbase) {
+  uint32_t rel = 0, ft = 0;
   const uint32_t l64 = 64u - (uint32_t)lane;
-#pragma unroll
-  for (int j = 0; j < kSpWS; ++j) {
-    if (j < cnt) {
+  auto step = [&](const int j) __attribute__((always_inline)) {
+    {
       const uint64_t ZO = sp_rl(R.ozl, R.ozh, j), Mem = sp_rl(R.oml, R.omh, j);
       const uint64_t HC = sp_rl(R.ohl, R.ohh, j);
       const uint32_t m = (R.mp[j >> 2] >> (8 * (j & 3))) & 0xffu;
@@ -508,9 +537,9 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut,
         const uint32_t z_lo = (uint32_t)e ? (uint32_t)__builtin_ctz((uint32_t)e) : 0xffffffffu;
         const uint32_t z_hi = (uint32_t)(e >> 32) ? (uint32_t)__builtin_ctz((uint32_t)(e >> 32)) + 32u
                                                   : 0xffffffffu;
-        uint32_t t = min(min(z_lo, z_hi), l64 + X);
-        t = min(t, 255u);
-        const uint32_t cn = sp_sel(0u, t, HC);
+        uint32_t tt = min(min(z_lo, z_hi), l64 + X);
+        tt = min(tt, 255u);
+        const uint32_t cn = sp_sel(0u, tt, HC);
         cz = m == 0 ? cn : 0u;
         cd = cn - cz;
       }
@@ -530,33 +559,60 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut,
       const uint32_t o = (uint32_t)incl - nb;
       const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
       if (stot) {
-        const uint32_t p = (uint32_t)rpos + o;
+        const uint32_t p = rel + o;
         const uint32_t sh = (p & 3) * 8;
         const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
         const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
         const uint32_t d3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
         uint32_t *rp = ring + ((p >> 2) & (kSpRing / 4 - 1));
-        atomicOr(rp, (uint32_t)a01);
-        atomicOr(rp + 1, (uint32_t)(a01 >> 32));
-        atomicOr(rp + 2, (uint32_t)(a12 >> 32));
-        atomicOr(rp + 3, d3);
-        rpos += stot;
-        // complete lines leave 64 at a time (one full-wave store); the ring
-        // holds at most 63 + 41 lines
-        if ((uint32_t)(rpos >> 4) - (uint32_t)fl >= 64u) {
-          wave_lds_order();
-          sp_flush(out, ring, fl, fl + 64, obase, lane, ocap);
+        if (nb) {  // (zero-length strings would all hit one address)
+          atomicOr(rp, (uint32_t)a01);
+          atomicOr(rp + 1, (uint32_t)(a01 >> 32));
+          atomicOr(rp + 2, (uint32_t)(a12 >> 32));
+          atomicOr(rp + 3, d3);
+        }
+        rel += stot;
+        // complete lines leave 64 at a time (one full-wave store)
+        if (known) {
+          const uint32_t done = ((uint32_t)(g0 & 15) + rel) >> 4;
+          if (done - ft >= 64u) {
+            wave_lds_order();
+            sp_flush(out, ring, g0, ft, ft + 64, lane, ocap);
+          }
         }
       }
     }
     CPK_SP_STEP_FENCE();
+  };
+  // (two fully unrolled loops around the one place the offset may be fetched)
+#pragma unroll
+  for (int j = 0; j < kSpDefer; ++j)
+    if (j < cnt) step(j);
+  if (!known && cnt > kSpDefer) {
+    g0 = getbase();
+    known = true;
+  }
+#pragma unroll
+  for (int j = kSpDefer; j < kSpWS; ++j)
+    if (j < cnt) step(j);
+  if (!known) g0 = getbase();
+  wave_lds_order();
+  const uint32_t k = (uint32_t)(g0 & 15);
+  const uint32_t done = (k + rel) >> 4;
+  sp_flush(out, ring, g0, ft, done, lane, ocap);
+  const uint32_t rem = (k + rel) & 15;
+  if (rem) {
+    // the last, partial line (also the first when it is all there is)
+    sp_store_bytes(out, ring, g0, done, done == 0 ? (int)k : 0, (int)rem, lane, ocap);
   }
   wave_lds_order();
-  sp_flush(out, ring, fl, rpos >> 4, obase, lane, ocap);
-  if (rpos > fl * 16) {
-    const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
-    sp_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane, ocap);
+  // clear what is left: relative lines [ft - 1, done] (ft - 1: the line
+  // before the last flushed one, still in the ring for its tail)
+  {
+    const uint32_t c0 = ft ? ft - 1 : 0, c1 = done + 1;
+    for (uint32_t i = c0 + (uint32_t)lane; i < c1; i += 64) sp_ring_clear(ring, i);
   }
+  wave_lds_order();
 }
 
 // Look-ahead past a chunk: the zero run / D/L stretch continuing from the
@@ -616,7 +672,13 @@ __device__ uint64_t sp_lookback(uint64_t *status, uint32_t p, uint64_t agg, uint
         sum += v[i] & kSpValMask;
       }
     }
+#ifdef CPK_PHASE_STATS
+    if (lane == 0) atomicAdd(&g_phase[40], 1ull);  // polls
+#endif
     if (__ballot(z)) {
+#ifdef CPK_PHASE_STATS
+      if (lane == 0) atomicAdd(&g_phase[42], 1ull);  // polls that met an unpublished predecessor
+#endif
       if (++spins > (1u << 22)) {  // cannot happen: every predecessor is held by a running workgroup
         if (lane == 0) atomicOr(err, 4u);
         break;
@@ -639,58 +701,77 @@ __device__ __forceinline__ SpSt sp_get_state(const uint64_t *scr, int par) {
   return s;
 }
 
-// ---- LDS-DMA staging of the next chunk ----------------------------------------
-// A chunk's words go global -> LDS by global_load_lds_dwordx4 (1 KiB per wave
-// instruction, no VGPRs), issued by waves 1-3 as soon as the previous chunk
-// has been read out of the buffer, so the load overlaps that chunk's roles,
-// look-back and emission.  Wave 0 issues none: it does the look-back, whose
-// global loads would otherwise wait (vmcnt) for its DMA.  Barriers while a
-// DMA is in flight are raw s_barrier + lgkmcnt(0) (__syncthreads would drain
-// vmcnt).
-__device__ __forceinline__ void sp_bar() {
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-  __builtin_amdgcn_s_barrier();
-}
-__device__ __forceinline__ void sp_stage(const uint64_t *__restrict__ cw, uint32_t wc, uint8_t *buf, int w,
-                                         int lane) {
-  // chunk words [0, wc) -> buf; 16-byte pieces, the whole ones only (an odd
-  // last word is fetched by A1)
-  if (w == 0) return;
-  const uint32_t blocks = (wc + 127) >> 7;
-  for (uint32_t b = (uint32_t)w - 1; b < blocks; b += kSpWaves - 1) {
-    const uint32_t k = b * 128 + 2 * (uint32_t)lane;
-    if (k + 2 <= wc)
-      __builtin_amdgcn_global_load_lds((const void *)(cw + k),
-                                       (void __attribute__((address_space(3))) *)(buf + b * 1024), 16, 0, 0);
+// One chunk's A1 + A2 for this wave (all waves call it; two barriers).
+// Returns the chunk's packed bytes (all waves); wbefore: bytes of the waves
+// before this one.  cst: the state entering the chunk -> leaving it.
+__device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restrict__ pw, uint32_t W,
+                                             uint32_t c, uint64_t *msk, uint64_t *scr, SpSt &cst,
+                                             int w, int lane, bool kEmit, int &cnt, uint32_t &Xlast,
+                                             uint64_t &wbefore) {
+  const uint32_t ns = (W + 63) >> 6;
+  const uint32_t cs0 = c * kSpCS;
+  const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
+  const int sa = w * kSpWS;
+  cnt = max(0, min(kSpWS, cs - sa));
+  const uint32_t wfirst = (cs0 + (uint32_t)sa) * 64;  // the wave's first word
+  const uint32_t wrem = cnt ? W - wfirst : 0;
+  uint32_t acc = 0;
+  if (cnt) {
+    acc = sp_a1(R, pw + wfirst, wrem, cnt, lane);
+    sp_put_masks(R, msk, sa, cnt, lane);
   }
-}
-
-struct SpPiece {
-  const uint64_t *pw;  // first word
-  uint32_t W;          // words (0 for an unsupported piece: error flagged)
-};
-template <bool kMsg>
-__device__ __forceinline__ SpPiece sp_piece_desc(const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo,
-                                                 const uint64_t *__restrict__ pdesc,
-                                                 const uint64_t *__restrict__ tin, uint32_t p, uint64_t hint,
-                                                 uint32_t *err, bool report) {
-  uint64_t w0, W64;
-  const uint64_t *base = in;
-  if (kMsg) {
-    w0 = pdesc[2 * (uint64_t)p];
-    W64 = pdesc[2 * (uint64_t)p + 1];
-    if (w0 >> 63) base = tin;
-    w0 &= ~(1ull << 63);
-  } else {
-    w0 = swo[p];
-    W64 = swo[p + 1] - w0;
+  __syncthreads();  // the chunk's masks in LDS
+  SpSt st = cst;
+  uint32_t bytes = 0;
+  const bool last = cnt && sa + cnt == cs;  // this wave holds the chunk's last step
+  if (cnt) {
+    st = sp_state_at(msk, sa, cst);
+    uint32_t nz0 = 0, ndl0 = 0;
+    Xlast = 0;
+    if (kEmit) {
+      // the step after the wave's last: in the chunk, or past it (look-ahead)
+      uint32_t laz = 0, ladl = 0;
+      const uint32_t wend = wfirst + 64u * cnt;
+      if (last && wend < W) sp_lookahead(pw + wend, W - wend, lane, laz, ladl);
+      if (sa + cnt < cs) {
+        nz0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt)]) & 1u;
+        ndl0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt) + 1]) & 1u;
+      } else {
+        nz0 = laz ? 1u : 0u;
+        ndl0 = ladl ? 1u : 0u;
+      }
+      const uint64_t Zl = sp_rl(R.zl, R.zh, cnt - 1), DLl = sp_rl(R.dll, R.dlh, cnt - 1);
+      const int cls = (Zl >> 63) ? 0 : ((DLl >> 63) ? 1 : -1);
+      if (cls >= 0) {
+        const uint32_t r = sp_cont(msk, sa + cnt, cs, cls, cls ? ladl : laz);
+        Xlast = r ? r - 1 : 0;
+      }
+    }
+    uint32_t rb = 0;
+    if (!sp_a2p(R, cnt, wrem, st, nz0, ndl0, lane, rb)) rb = sp_a2_seq(R, cnt, wrem, st, nz0, ndl0);
+    if (kEmit) sp_xs(R, cnt, Xlast, lane);
+    bytes = rb + (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)acc), 63);
   }
-  const bool bad = W64 >= (1ull << 31);
-  if (report && (bad || (hint && W64 > hint)) && threadIdx.x == 0) atomicOr(err, 1u);
-  SpPiece d = {base + w0, bad ? 0u : (uint32_t)W64};  // (unsupported: sized 0, output undefined)
-  return d;
+  if (last) st = sp_state_at(msk, cs, cst);  // the state leaving the chunk
+  if (lane == 0) {
+    scr[1 + w] = bytes;
+    if (last) {
+      scr[6 + 2 * (c & 1)] = st.zl;
+      scr[7 + 2 * (c & 1)] = (uint64_t)st.dlo | ((uint64_t)st.hd << 1);
+    }
+  }
+  __syncthreads();  // wave bytes and the exit state in LDS
+  uint64_t tot = 0;
+  wbefore = 0;
+#pragma unroll
+  for (int q = 0; q < kSpWaves; ++q) {
+    const uint64_t b = sp_ld(&scr[1 + q]);
+    if (q < w) wbefore += b;
+    tot += b;
+  }
+  cst = sp_get_state(scr, c & 1);
+  return tot;
 }
-__device__ __forceinline__ uint32_t sp_nch(uint32_t W) { return (((W + 63) >> 6) + kSpCS - 1) / kSpCS; }
 
 // kMsg = false: piece p is words [swo[p], swo[p+1]) of `in`.  kMsg = true:
 // pdesc[2p] = first word (bit 63: of `tin`, the segment tables) and
@@ -708,7 +789,6 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kSpoLut);
   uint64_t *msk = reinterpret_cast<uint64_t *>(smem + kSpoMsk);
   uint64_t *scr = reinterpret_cast<uint64_t *>(smem + kSpoScr);
-  uint8_t *buf = smem + kSpoBuf;
   const int lane0 = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kSpoRing + w * kSpRingStride);
@@ -717,158 +797,99 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
   SpRegs R;
   R.zl = R.zh = R.dll = R.dlh = R.dl_ = R.dh_ = 0;
-  R.ozl = R.ozh = R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = R.ox = 0;
-  (void)ppt;
-  // the first piece: ticket, staged synchronously
-  if (threadIdx.x == 0) scr[0] = atomicAdd(ticket, 1u);
-  __syncthreads();
-  uint32_t p = (uint32_t)sp_ld(&scr[0]);
-  SpPiece cur = {nullptr, 0u};
-  if (p < n) {
-    cur = sp_piece_desc<kMsg>(in, swo, pdesc, tin, p, hint, err, true);
-    sp_stage(cur.pw, min(cur.W, (uint32_t)(kSpCS * 64)), buf, w, lane0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  R.ozl = R.ozh = R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = 0;
+  if (threadIdx.x == 0) scr[11] = 0;  // (LDS holds whatever the last kernel left)
   WPH_INIT
-  while (p < n) {
-    // an opaque copy of the lane id: nothing lane-dependent is hoisted out
-    // of the piece loop into registers that stay live across it
-    int lane = lane0;
-    asm volatile("" : "+v"(lane));
-    const uint32_t W = cur.W;
-    const uint32_t ns = (W + 63) >> 6;
-    const uint32_t nch = sp_nch(W);
-    // one chunk: A1, A2, offset, B.  More: every chunk sized (pass 0), the
-    // offset, every chunk read again and emitted (pass 1)
-    const uint32_t iters = nch > 1 ? 2 * nch : 1;
-    uint64_t total = 0, cbase = 0;
-    SpSt cst = {0u, 0u, 0u};
-    uint32_t q = n;  // the next piece
-    SpPiece nxt = {nullptr, 0u};
-    for (uint32_t it = 0; it < iters; ++it) {
-      const bool emit = nch <= 1 || it >= nch;
-      const uint32_t c = nch > 1 ? (emit ? it - nch : it) : 0;
-      if (emit && c == 0) cst = SpSt{0u, 0u, 0u};
-      const uint32_t cs0 = c * kSpCS;
-      const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
-      const int sa = w * kSpWS;
-      const int cnt = max(0, min(kSpWS, cs - sa));
-      const uint32_t wfirst = (cs0 + (uint32_t)sa) * 64;  // the wave's first word
-      const uint32_t wrem = cnt ? W - wfirst : 0;
-      const uint32_t cend = (cs0 + (uint32_t)cs) * 64;    // the chunk's end (piece word)
-      // ---- A1 (this chunk is staged in buf) ----
-      WPH(7)
-      uint32_t acc = 0;
-      if (cnt) {
-        acc = sp_a1(R, reinterpret_cast<const uint64_t *>(buf) + (uint32_t)sa * 64, cur.pw + wfirst, wrem, cnt,
-                    lane);
-        sp_put_masks(R, msk, sa, cnt, lane);
-      }
-      if (w == 0 && emit && cend < W) {
-        // the zero run / D/L stretch continuing past the chunk's end
-        uint32_t laz, ladl;
-        sp_lookahead(cur.pw + cend, W - cend, lane, laz, ladl);
-        if (lane == 0) scr[10] = laz | (ladl << 16);
-      }
-      WPH(0)
-      if (it + 1 == iters && threadIdx.x == 0) scr[0] = atomicAdd(ticket, 1u);
-      sp_bar();  // the masks in LDS; buf read out; the next ticket
-      WPH(1)
-      // ---- stage the next chunk (this piece's, or the next piece's first) ----
-      if (it + 1 < iters) {
-        const uint32_t c2 = nch > 1 ? (it + 1 >= nch ? it + 1 - nch : it + 1) : 0;
-        sp_stage(cur.pw + c2 * (uint32_t)(kSpCS * 64), min(W - c2 * (uint32_t)(kSpCS * 64), (uint32_t)(kSpCS * 64)),
-                 buf, w, lane);
+  for (;;) {
+    WPH(3)
+    if (threadIdx.x == 0) scr[0] = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t t = (uint32_t)sp_ld(&scr[0]);
+    __syncthreads();  // (scr[0] read by all before the next ticket)
+    const uint64_t pfirst = (uint64_t)t * ppt;
+    WPH(0)
+    if (pfirst >= n) break;
+    const uint32_t plast = (uint32_t)min(pfirst + ppt, (uint64_t)n);
+    for (uint32_t p = (uint32_t)pfirst; p < plast; ++p) {
+      // an opaque copy of the lane id: nothing lane-dependent is hoisted out
+      // of the piece loop into registers that stay live across it
+      int lane = lane0;
+      asm volatile("" : "+v"(lane));
+      uint64_t w0, W64;
+      const uint64_t *base = in;
+      if (kMsg) {
+        w0 = pdesc[2 * (uint64_t)p];
+        W64 = pdesc[2 * (uint64_t)p + 1];
+        if (w0 >> 63) base = tin;
+        w0 &= ~(1ull << 63);
       } else {
-        q = (uint32_t)sp_ld(&scr[0]);
-        if (q < n) {
-          nxt = sp_piece_desc<kMsg>(in, swo, pdesc, tin, q, hint, err, true);
-          sp_stage(nxt.pw, min(nxt.W, (uint32_t)(kSpCS * 64)), buf, w, lane);
+        w0 = swo[p];
+        W64 = swo[p + 1] - w0;
+      }
+      bool bad = W64 >= (1ull << 31);
+      if ((bad || (hint && W64 > hint)) && threadIdx.x == 0) atomicOr(err, 1u);
+      const uint32_t W = bad ? 0u : (uint32_t)W64;  // (unsupported: sized 0, output undefined)
+      const uint64_t *pw = base + w0;
+      const uint32_t nch = (((W + 63) >> 6) + kSpCS - 1) / kSpCS;
+      int cnt = 0;
+      uint32_t Xlast = 0;
+      uint64_t wbefore = 0, total = 0, cbase = 0;
+      SpSt cst = {0u, 0u, 0u};
+      // one chunk: A1, A2, offset, B.  More: every chunk sized (pass 0),
+      // the offset, every chunk read again and emitted (pass 1).  One copy
+      // of each phase in the code (uniform branches).
+      const uint32_t iters = nch > 1 ? 2 * nch : 1;
+      for (uint32_t it = 0; it < iters; ++it) {
+        const bool emit = nch <= 1 || it >= nch;
+        const uint32_t c = nch > 1 ? (emit ? it - nch : it) : 0;
+        if (emit && c == 0) cst = SpSt{0u, 0u, 0u};
+        const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, cst, w, lane, emit, cnt, Xlast, wbefore);
+        WPH(1)
+        if (!emit) {
+          total += ct;
+          continue;
         }
-      }
-      // ---- A2 ----
-      WPH(2)
-      uint32_t bytes = 0, Xlast = 0;
-      SpSt st = cst;
-      const bool last = cnt && sa + cnt == cs;  // this wave holds the chunk's last step
-      if (cnt) {
-        st = sp_state_at(msk, sa, cst);
-        uint32_t nz0 = 0, ndl0 = 0;
-        if (emit) {
-          // the step after the wave's last: in the chunk, or past it
-          uint32_t laz = 0, ladl = 0;
-          if (last && cend < W) {
-            const uint32_t la = (uint32_t)sp_ld(&scr[10]);
-            laz = la & 0xffffu;
-            ladl = la >> 16;
-          }
-          if (sa + cnt < cs) {
-            nz0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt)]) & 1u;
-            ndl0 = (uint32_t)sp_ld(&msk[3 * (sa + cnt) + 1]) & 1u;
-          } else {
-            nz0 = laz ? 1u : 0u;
-            ndl0 = ladl ? 1u : 0u;
-          }
-          const uint64_t Zl = sp_rl(R.zl, R.zh, cnt - 1), DLl = sp_rl(R.dll, R.dlh, cnt - 1);
-          const int cls = (Zl >> 63) ? 0 : ((DLl >> 63) ? 1 : -1);
-          if (cls >= 0) {
-            const uint32_t r = sp_cont(msk, sa + cnt, cs, cls, cls ? ladl : laz);
-            Xlast = r ? r - 1 : 0;
-          }
-        }
-        uint32_t rb = 0;
-        if (!sp_a2p(R, cnt, wrem, st, nz0, ndl0, lane, rb)) rb = sp_a2_seq(R, cnt, wrem, st, nz0, ndl0);
-        if (emit) sp_xs(R, cnt, Xlast, lane);
-        bytes = rb + (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)acc), 63);
-      }
-      if (last) st = sp_state_at(msk, cs, cst);  // the state leaving the chunk
-      if (lane == 0) {
-        scr[1 + w] = bytes;
-        if (last) {
-          scr[6 + 2 * (c & 1)] = st.zl;
-          scr[7 + 2 * (c & 1)] = (uint64_t)st.dlo | ((uint64_t)st.hd << 1);
-        }
-      }
-      WPH(3)
-      sp_bar();  // wave bytes and the exit state
-      WPH(4)
-      uint64_t ct = 0, wbefore = 0;
-#pragma unroll
-      for (int k = 0; k < kSpWaves; ++k) {
-        const uint64_t b = sp_ld(&scr[1 + k]);
-        if (k < w) wbefore += b;
-        ct += b;
-      }
-      cst = sp_get_state(scr, c & 1);
-      if (!emit) {
-        total += ct;
-      } else {
-        if (c == 0) {
-          // ---- offset: look-back over the pieces before p (wave 0: no DMA in flight) ----
-          if (nch <= 1) total = ct;
-          if (w == 0) {
-            const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
-            if (lane == 0) {
-              scr[5] = excl;
-              out_off[p] = excl;
-              if (p + 1 == n) out_off[n] = excl + total;
+        if (c == 0 && nch <= 1) total = ct;
+        WPH(2)
+        if (cnt) {
+          // the offset: known past chunk 0; for chunk 0 the look-back (wave 0)
+          // runs once the waves have laid out kSpDefer steps
+          auto getbase = [&]() -> uint64_t {
+            if (w == 0) {
+              const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
+              if (lane == 0) {
+                scr[5] = excl;
+                out_off[p] = excl;
+                if (p + 1 == n) out_off[n] = excl + total;
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // (the offset before the flag)
+                scr[11] = (uint64_t)p + 1;
+              }
+              return excl + wbefore;
             }
+            while ((uint32_t)sp_ld(&scr[11]) != p + 1) __builtin_amdgcn_s_sleep(1);
+            return sp_ld(&scr[5]) + wbefore;
+          };
+          sp_b(R, cnt, lut, ring, out, c != 0, cbase + wbefore, lane, ocap, getbase);
+        } else if (c == 0 && w == 0) {
+          // wave 0 runs the look-back even without steps (an empty piece)
+          const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
+          if (lane == 0) {
+            scr[5] = excl;
+            out_off[p] = excl;
+            if (p + 1 == n) out_off[n] = excl + total;
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            scr[11] = (uint64_t)p + 1;
           }
-          sp_bar();
+        }
+        if (c == 0) {
+          // (every wave knows the piece's offset from here on)
+          while ((uint32_t)sp_ld(&scr[11]) != p + 1) __builtin_amdgcn_s_sleep(1);
           cbase = sp_ld(&scr[5]);
         }
-        WPH(5)
-        // ---- B ----
-        if (cnt) sp_b(R, cnt, lut, ring, out, cbase + wbefore, lane, ocap);
         cbase += ct;
-        WPH(6)
+        WPH(4)
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed
-      sp_bar();                                           // ... and every wave's
     }
-    p = q;
-    cur = nxt;
   }
   WPH_FLUSH(32)
 }

@@ -1106,11 +1106,7 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     return CPK_ENOMEM;
   }
   if (hipFuncSetAttribute((const void *)cpk::decode_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess ||
-      hipFuncSetAttribute((const void *)cpk::sp_encode_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kSpLds) != hipSuccess ||
-      hipFuncSetAttribute((const void *)cpk::sp_encode_kernel<true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kSpLds) != hipSuccess) {
+                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess) {
     hipFree(c->tickets);
     free(c);
     return CPK_EDEVICE;
@@ -1158,7 +1154,7 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
   // second's size only after emitting the first, and the pieces after it
   // would wait on that (a serial chain through the tickets)
   const uint32_t ppt = 1u;
-  unsigned grid = (unsigned)(2 * ctx->cus);  // (LDS: 2 workgroups per CU)
+  unsigned grid = (unsigned)(CPK_SP_WPE * ctx->cus);
   const uint64_t tickets = ((uint64_t)n + ppt - 1) / ppt;
   if (grid > tickets) grid = (unsigned)tickets;
   if (pdesc)

@@ -33,10 +33,10 @@ L.cpk_debug_phase_stats(buf.ctypes.data)
 ctx.encode_batch(d_in, d_swo, 8192, d_pk, d_off)
 torch.cuda.synchronize()
 L.cpk_debug_phase_stats(buf.ctypes.data)
-names = ["A1 (LDS->regs, tags, masks)", "ticket + barrier 1", "stage next (DMA issue)", "A2 roles",
-         "barrier 2", "look-back + barrier 3", "B emit", "DMA wait + barrier 4"]
-v = buf[32:40].astype(float)
+names = ["ticket + barriers", "A1 + A2 (+2 barriers)", "look-back + barrier", "loop top", "B emit"]
+v = buf[32:37].astype(float)
 tot = v.sum()
 print(f"sp_encode config {cfg}: {tot / 1e6:.1f} Mcycles over all waves; per piece per wave {tot / n / 4:.0f} cyc")
 for nm, x in zip(names, v):
     print(f"   {nm:30s} {100 * x / max(tot, 1):6.2f} %   {x / n / 4:8.0f} cyc/piece/wave")
+print(f"look-back: {buf[40] / n:.2f} polls per piece, {buf[42] / n:.2f} of them retried")
