@@ -991,6 +991,7 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 
 #include "encode_v4.hip"
 #include "encode_sp.hip"
+#include "decode_v2.hip"
 
 }  // namespace cpk
 
@@ -1003,7 +1004,8 @@ struct cpk_ctx_s {
   uint64_t *status;       // look-back words
   uint64_t status_cap;    // entries
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
-  int encoder;            // 0: single pass (encode_sp.hip, default); 4: size + emit passes (CPK_ENCODER=4)
+  int encoder;            // 0: single pass (encode_sp.hip); 4: size + emit passes
+  int decoder;            // 2: record index (decode_v2.hip); 1: block map (decode_kernel)
   uint64_t *sp_status;    // single pass: look-back word per piece
   uint64_t sp_cap;        //   entries
   uint32_t sp_epoch;      //   launch epoch tagging the look-back words, 1..65535
@@ -1097,6 +1099,9 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     // two-pass one; the default is whichever measured faster
     const char *e = getenv("CPK_ENCODER");
     c->encoder = (e && e[0] == '0') ? 0 : 4;
+    // CPK_DECODER=1 selects the block-map decoder, 2 the record-index one
+    const char *d = getenv("CPK_DECODER");
+    c->decoder = (d && d[0] == '2') ? 2 : 1;
   }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
@@ -1316,6 +1321,34 @@ int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
   return e ? ((e & 4u) ? CPK_EDEVICE : CPK_EINVAL) : CPK_OK;
 }
 
+// one launch of the configured decoder (grid: as many workgroups per CU as
+// its LDS allows, at most 8; never more than the work needs)
+namespace {
+void dec_launch(cpk_ctx ctx, bool stream, unsigned want, const uint8_t *packed, uint64_t *in_off,
+                const uint64_t *swo, uint32_t n, uint64_t *out, int32_t *status, uint64_t avail,
+                cpk::DecStreams sd, hipStream_t s) {
+  const bool v2 = ctx->decoder == 2;
+  const uint32_t lds = v2 ? cpk::kD2Lds : cpk::kDecLds;
+  const unsigned per_cu = (unsigned)min(8u, 160u * 1024u / lds);
+  unsigned grid = per_cu * (unsigned)ctx->cus;
+  if (grid > want) grid = want;
+  if (grid == 0) grid = 1;
+  uint32_t *tk = ctx->tickets + cpk::kTkDec;
+  if (v2 && stream)
+    hipLaunchKernelGGL(cpk::decode2_kernel<true>, dim3(grid), dim3(cpk::kD2Threads), lds, s, packed, in_off, swo, n,
+                       out, status, tk, avail, sd);
+  else if (v2)
+    hipLaunchKernelGGL(cpk::decode2_kernel<false>, dim3(grid), dim3(cpk::kD2Threads), lds, s, packed, in_off, swo, n,
+                       out, status, tk, avail, sd);
+  else if (stream)
+    hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(grid), dim3(cpk::kDecThreads), lds, s, packed, in_off, swo, n,
+                       out, status, tk, avail, sd);
+  else
+    hipLaunchKernelGGL(cpk::decode_kernel<false>, dim3(grid), dim3(cpk::kDecThreads), lds, s, packed, in_off, swo, n,
+                       out, status, tk, avail, sd);
+}
+}  // namespace
+
 int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off,
                      const uint64_t *d_swo, uint32_t n, void *d_out, int32_t *d_status,
                      void *stream) {
@@ -1326,15 +1359,9 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
     return CPK_EDEVICE;
-  // persistent: up to 8 blocks of 4 independent waves per CU (32 pieces in
-  // flight), as many as the LDS holds
-  const unsigned per_cu = (unsigned)min(8u, 160u * 1024u / cpk::kDecLds);
-  unsigned grid = per_cu * (unsigned)ctx->cus;
-  if (grid > (n + 3) / 4) grid = (n + 3) / 4;
-  hipLaunchKernelGGL(cpk::decode_kernel<false>, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
-                     (const uint8_t *)d_packed, const_cast<uint64_t *>(d_in_off), d_swo, n,
-                     (uint64_t *)d_out, d_status, ctx->tickets + cpk::kTkDec, (uint64_t)0,
-                     cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr});
+  // persistent: blocks of 4 independent waves, as many per CU as the LDS holds
+  dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, const_cast<uint64_t *>(d_in_off), d_swo, n,
+             (uint64_t *)d_out, d_status, 0, cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr}, s);
   return hip_ok(hipGetLastError());
 }
 
@@ -1349,10 +1376,8 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
   if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
     return CPK_EDEVICE;
   // one stream: one wave works, the others find no ticket
-  hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds, s,
-                     (const uint8_t *)d_packed, d_in_off, d_swo, n, (uint64_t *)d_out, d_status,
-                     ctx->tickets + cpk::kTkDec, avail,
-                     cpk::DecStreams{nullptr, nullptr, nullptr, 1, d_in_off + n});
+  dec_launch(ctx, true, 1, (const uint8_t *)d_packed, d_in_off, d_swo, n, (uint64_t *)d_out, d_status, avail,
+             cpk::DecStreams{nullptr, nullptr, nullptr, 1, d_in_off + n}, s);
   return hip_ok(hipGetLastError());
 }
 
@@ -1402,15 +1427,10 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
   if (h_totals[1]) {
     if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
       return CPK_EDEVICE;
-    const unsigned per_cu = (unsigned)min(8u, 160u * 1024u / cpk::kDecLds);
-    unsigned grid = per_cu * (unsigned)ctx->cus;
-    if (grid > (nm + 3) / 4) grid = (nm + 3) / 4;
     // the stream ends overwrite the words array (no longer needed)
-    hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(grid), dim3(cpk::kDecThreads), cpk::kDecLds, s,
-                       (const uint8_t *)d_packed, d_seg_in_off, (const uint64_t *)d_seg_word_off,
-                       (uint32_t)h_totals[1], (uint64_t *)d_out, d_seg_status,
-                       ctx->tickets + cpk::kTkDec, (uint64_t)0,
-                       cpk::DecStreams{mbeg, d_msg_off + 1, d_msg_seg_off, nm, mwords});
+    dec_launch(ctx, true, (nm + 3) / 4, (const uint8_t *)d_packed, d_seg_in_off, (const uint64_t *)d_seg_word_off,
+               (uint32_t)h_totals[1], (uint64_t *)d_out, d_seg_status, 0,
+               cpk::DecStreams{mbeg, d_msg_off + 1, d_msg_seg_off, nm, mwords}, s);
     hipLaunchKernelGGL(cpk::msg_final_kernel, dim3(tg), dim3(tb), 0, s, d_msg_off, nm,
                        (const uint64_t *)d_msg_seg_off, (const uint64_t *)mwords,
                        (const int32_t *)d_seg_status, d_msg_status);

@@ -15,25 +15,29 @@ pytestmark = pytest.mark.gpu
 GOLD = json.loads((Path(__file__).parent / "golden" / "reference_kats.json").read_text())
 
 
-@pytest.fixture(scope="module", params=["4", "0"], ids=["enc-two-pass", "enc-single-pass"])
+@pytest.fixture(scope="module", params=[("4", "1"), ("0", "2")],
+                ids=["enc-two-pass+dec-blockmap", "enc-single-pass+dec-index"])
 def ctx(request):
-    """A context per encoder (CPK_ENCODER is read at context creation): every
-    parity case runs through both the two-pass (encode_v4.hip) and the
-    single-pass (encode_sp.hip) encoder."""
+    """A context per encoder / decoder pair (CPK_ENCODER, CPK_DECODER are read
+    at context creation): every parity case runs through the two-pass encoder
+    (encode_v4.hip) with the block-map decoder (decode_kernel), and through
+    the single-pass encoder (encode_sp.hip) with the record-index decoder
+    (decode_v2.hip)."""
     import os
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     import capnp_packed as cp
-    old = os.environ.get("CPK_ENCODER")
-    os.environ["CPK_ENCODER"] = request.param
+    saved = {k: os.environ.get(k) for k in ("CPK_ENCODER", "CPK_DECODER")}
+    os.environ["CPK_ENCODER"], os.environ["CPK_DECODER"] = request.param
     try:
         c = cp.Context(0)
     finally:
-        if old is None:
-            os.environ.pop("CPK_ENCODER")
-        else:
-            os.environ["CPK_ENCODER"] = old
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
     yield c
     c.close()
 

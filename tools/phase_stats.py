@@ -40,3 +40,20 @@ print(f"sp_encode config {cfg}: {tot / 1e6:.1f} Mcycles over all waves; per piec
 for nm, x in zip(names, v):
     print(f"   {nm:30s} {100 * x / max(tot, 1):6.2f} %   {x / n / 4:8.0f} cyc/piece/wave")
 print(f"look-back: {buf[40] / n:.2f} polls per piece, {buf[42] / n:.2f} of them retried")
+
+# ---- decoder phases (decode_kernel WPH slots 16..22) ----
+d_out = torch.empty_like(d_in)
+d_st = torch.empty(n, dtype=torch.int32, device="cuda")
+ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
+torch.cuda.synchronize()
+L.cpk_debug_phase_stats(buf.ctypes.data)
+ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
+torch.cuda.synchronize()
+L.cpk_debug_phase_stats(buf.ctypes.data)
+dnames = ["ticket+piece", "window load", "chunk walks", "lane chain", "count walk", "errors+blk map | index", "expand+store"]
+v = buf[16:16 + len(dnames)].astype(float)
+tot = v.sum()
+print(f"decode config {cfg}: total {tot / 1e6:.1f} Mcycles over all waves; per piece {tot / n:.0f} cyc")
+for nm, x in zip(dnames, v):
+    print(f"   {nm:22s} {100 * x / max(tot, 1):6.2f} %   {x / n:8.0f} cyc/piece")
+print("bad status", int((d_st != 0).sum().item()))

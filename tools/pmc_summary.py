@@ -19,10 +19,11 @@ for f in sorted(root.glob("*/*_counter_collection.csv")):
             k = r["Kernel_Name"]
             short = ("e4_size_kernel" if "e4_size_kernel" in k else "e4_emit_kernel" if "e4_emit_kernel" in k
                      else "sp_encode_kernel" if "sp_encode_kernel" in k
+                     else "decode2_kernel" if "decode2_kernel" in k
                      else "decode_kernel" if "decode_kernel" in k else k.split("(")[0][-40:])
             vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
-for kern in ("sp_encode_kernel", "e4_size_kernel", "e4_emit_kernel", "decode_kernel"):
+for kern in ("sp_encode_kernel", "e4_size_kernel", "e4_emit_kernel", "decode_kernel", "decode2_kernel"):
     if kern not in vals:
         continue
     d = {c: sum(v) / len(v) for c, v in vals[kern].items()}
@@ -47,6 +48,8 @@ if len(sys.argv) > 3 and sys.argv[2] == "--json":
     elif "e4_size_kernel" in out and "e4_emit_kernel" in out:
         out["encode_kernel"] = {c: out["e4_size_kernel"].get(c, 0) + out["e4_emit_kernel"].get(c, 0)
                                 for c in ("FETCH_SIZE", "WRITE_SIZE")}
+    if "decode2_kernel" in out:
+        out["decode_kernel"] = out["decode2_kernel"]
     for kern, key in (("encode_kernel", "encode"), ("decode_kernel", "decode")):
         d = out.get(kern, {})
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:

@@ -23,11 +23,12 @@ cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
 handles = []
 import os
 for spec in libs:
-    # "lib.so@1": context created with CPK_ENCODER=1 (workgroup-per-piece encoder)
-    # "lib.so@3:CPK_E3_RESERVE=0,CPK_DECODER=3": encoder 3 plus env knobs read at ctx creation
+    # "lib.so@0": context created with CPK_ENCODER=0 (single-pass encoder)
+    # "lib.so@4:CPK_DECODER=2": encoder 4 plus env knobs read at ctx creation
     lp, _, enc = spec.partition("@")
     enc, _, envs = enc.partition(":")
     os.environ["CPK_ENCODER"] = enc or "0"
+    os.environ.pop("CPK_DECODER", None)
     for kv in filter(None, envs.split(",")):
         k, _, v = kv.partition("=")
         os.environ[k] = v
