@@ -173,6 +173,18 @@ class Context:
                                         d_status.data_ptr(), self._stream(stream))
         _check(rc, "cpk_decode_batch")
 
+    def decode_stream(self, d_packed, avail: int, d_seg_word_off, d_out, d_in_off, d_status,
+                      stream=None):
+        """Serialize.read-style decode of pieces back to back from one packed
+        stream of `avail` bytes (cpk_decode_stream); d_in_off[n+1] gets the
+        piece boundaries found.  Synchronises `stream` once for streams of
+        256 KiB and more (they are cut into blocks and decoded in parallel)."""
+        n = d_seg_word_off.numel() - 1
+        rc = self._lib.cpk_decode_stream(self.handle, d_packed.data_ptr(), int(avail),
+                                         d_seg_word_off.data_ptr(), n, d_out.data_ptr(),
+                                         d_in_off.data_ptr(), d_status.data_ptr(), self._stream(stream))
+        _check(rc, "cpk_decode_stream")
+
     def encode_messages(self, d_in, d_seg_word_off, d_msg_seg_off, max_seg_words: int, d_out,
                         d_out_off, stream=None):
         """SerializePacked.write per message (cpk_encode_messages): the

@@ -27,9 +27,12 @@
 // chunk by chunk (run state carried from chunk to chunk), then read again
 // and emitted: 2U + P for those pieces only.
 
-constexpr int kSpWaves = 4;
+#ifndef CPK_SP_WAVES
+#define CPK_SP_WAVES 4
+#endif
+constexpr int kSpWaves = CPK_SP_WAVES;
 constexpr int kSpThreads = 64 * kSpWaves;
-constexpr int kSpWS = 32;                      // steps per wave
+constexpr int kSpWS = 128 / kSpWaves;          // steps per wave
 constexpr int kSpCS = kSpWaves * kSpWS;        // steps per chunk (8192 words)
 constexpr uint32_t kSpRing = 8192;             // output ring per wave (bytes)
 constexpr uint32_t kSpRingLines = kSpRing / 16;
@@ -37,10 +40,11 @@ constexpr uint32_t kSpRingStride = kSpRing + 16;  // + one overhang line (line 0
 constexpr uint32_t kSpoLut = 0;                                      // u64[256]
 constexpr uint32_t kSpoMsk = 2048;                                   // u64[kSpCS][3]
 constexpr uint32_t kSpoRing = kSpoMsk + kSpCS * 24;                  // per wave
-constexpr uint32_t kSpoScr = kSpoRing + kSpWaves * kSpRingStride;    // u64[16]
-constexpr uint32_t kSpLds = kSpoScr + 16 * 8;                        // 37,504 B
+constexpr uint32_t kSpoScr = kSpoRing + kSpWaves * kSpRingStride;    // u64[32]
+constexpr uint32_t kSpLds = kSpoScr + 32 * 8;                        // 37,632 B (4 waves)
+static_assert(kSpWaves <= 16 && kSpWS >= 4 && kSpWS <= 32 && kSpWS % 4 == 0, "wave count");
 static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
-// scratch words: [0] ticket, [1..4] wave bytes, [5] piece offset,
+// scratch words: [0] ticket, [16..16 + waves) wave bytes, [5] piece offset,
 // [6..9] chunk exit state (two parities x {zl, dlo | hd << 1}), [11] the piece
 // (+ 1) whose offset [5] holds
 // Steps are scheduled one at a time: hoisting later steps' LUT reads and
@@ -754,7 +758,7 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   }
   if (last) st = sp_state_at(msk, cs, cst);  // the state leaving the chunk
   if (lane == 0) {
-    scr[1 + w] = bytes;
+    scr[16 + w] = bytes;
     if (last) {
       scr[6 + 2 * (c & 1)] = st.zl;
       scr[7 + 2 * (c & 1)] = (uint64_t)st.dlo | ((uint64_t)st.hd << 1);
@@ -765,7 +769,7 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   wbefore = 0;
 #pragma unroll
   for (int q = 0; q < kSpWaves; ++q) {
-    const uint64_t b = sp_ld(&scr[1 + q]);
+    const uint64_t b = sp_ld(&scr[16 + q]);
     if (q < w) wbefore += b;
     tot += b;
   }

@@ -992,6 +992,7 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 #include "encode_v4.hip"
 #include "encode_sp.hip"
 #include "decode_v2.hip"
+#include "stream_split.hip"
 
 }  // namespace cpk
 
@@ -1014,6 +1015,8 @@ struct cpk_ctx_s {
   uint64_t *e4_bv;        // encoder v4: run boundaries per 64-word step
   uint64_t e4_bv_cap;     //   entries
   HostPipe *pipe;         // cpk_encode_host / cpk_decode_host staging (lazy)
+  uint64_t *ss_buf;       // parallel stream decode scratch (stream_split.hip)
+  uint64_t ss_cap;        //   u64 entries
 };
 
 namespace {
@@ -1128,6 +1131,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->e4_bv) hipFree(ctx->e4_bv);
   if (ctx->sp_status) hipFree(ctx->sp_status);
   if (ctx->sp_desc) hipFree(ctx->sp_desc);
+  if (ctx->ss_buf) hipFree(ctx->ss_buf);
   pipe_destroy(ctx->pipe);
   free(ctx);
 }
@@ -1159,6 +1163,16 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
   // second's size only after emitting the first, and the pieces after it
   // would wait on that (a serial chain through the tickets)
   const uint32_t ppt = 1u;
+  if (cpk::kSpLds > 65536) {  // (more than the default dynamic LDS limit)
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void *)cpk::sp_encode_kernel<true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)cpk::kSpLds);
+      hipFuncSetAttribute((const void *)cpk::sp_encode_kernel<false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)cpk::kSpLds);
+      attr = true;
+    }
+  }
   unsigned grid = (unsigned)(CPK_SP_WPE * ctx->cus);
   const uint64_t tickets = ((uint64_t)n + ppt - 1) / ppt;
   if (grid > tickets) grid = (unsigned)tickets;
@@ -1365,6 +1379,89 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   return hip_ok(hipGetLastError());
 }
 
+namespace {
+// streams of at least this many bytes (after the bound below) are cut into
+// blocks and decoded in parallel (stream_split.hip); shorter ones by one wave
+constexpr uint64_t kSsMin = 256 * 1024;
+
+// the bytes a stream of `words` words may take: 10 per word at most
+uint64_t ss_reach(uint64_t avail, uint64_t words) {
+  const uint64_t b = words > (~0ull - 16) / 10 ? ~0ull : 10 * words + 16;
+  return avail < b ? avail : b;
+}
+
+// parallel stream decode over at most `reach` bytes; enqueues the one-wave
+// decoder after it, which runs only if the parallel path met anything
+// irregular (it then decodes the whole stream, errors included)
+int ss_decode(cpk_ctx ctx, const uint8_t *pk, uint64_t avail, uint64_t reach, const uint64_t *swo, uint32_t n,
+              uint64_t *out, uint64_t *in_off, int32_t *status, hipStream_t s) {
+  using namespace cpk;
+  const uint64_t nb = (reach + kSsBlock - 1) / kSsBlock, ng = (nb + kSsGroup - 1) / kSsGroup;
+  // scratch layout (u64 entries)
+  const uint64_t need = 5 * nb + 3 * kSsCand * nb + (nb + 1) / 2 + 3 * kSsVar * ng + (kSsVar + 1) * nb +
+                        ((kSsVar + 1) * nb + 1) / 2 + (ng + 1) / 2 + ng + 4 * (nb + 1) + (nb + 1) / 2 + 2 + 2;
+  if (need > ctx->ss_cap) {
+    if (ctx->ss_buf) hipFree(ctx->ss_buf);
+    ctx->ss_buf = nullptr;
+    ctx->ss_cap = 0;
+    const uint64_t cap = need + need / 4;
+    if (hipMalloc(&ctx->ss_buf, cap * 8) != hipSuccess) return CPK_ENOMEM;
+    ctx->ss_cap = cap;
+  }
+  uint64_t *q = ctx->ss_buf;
+  auto take = [&](uint64_t k) {
+    uint64_t *r = q;
+    q += k;
+    return r;
+  };
+  SsBufs B;
+  B.X = take(nb);
+  B.W = take(nb);
+  B.C1 = take(nb);
+  B.L1 = take(nb);
+  B.WL1 = take(nb);
+  B.C2 = take(kSsCand * nb);
+  B.L2 = take(kSsCand * nb);
+  B.WL2 = take(kSsCand * nb);
+  B.N2 = (uint32_t *)take((nb + 1) / 2);
+  B.GE = take(kSsVar * ng);
+  B.GX = take(kSsVar * ng);
+  B.GW = take(kSsVar * ng);
+  B.VE = take((kSsVar + 1) * nb);
+  B.VW = (uint32_t *)take(((kSsVar + 1) * nb + 1) / 2);
+  B.GC = (uint32_t *)take((ng + 1) / 2);
+  B.GB = take(ng);
+  B.E = take(nb + 1);
+  B.WO = take(nb + 1);
+  B.sin = take(nb + 1);
+  B.sswo = take(nb + 1);
+  B.sst = (int32_t *)take((nb + 1) / 2);
+  B.flag = (uint32_t *)take(2);
+  B.lim = take(2);
+  if (hipMemsetAsync(B.N2, 0, 4 * nb, s) != hipSuccess || hipMemsetAsync(B.flag, 0, 8, s) != hipSuccess ||
+      hipMemsetAsync(ctx->tickets + kTkDec, 0, 8 * kTkStride * 4, s) != hipSuccess)
+    return CPK_EDEVICE;
+  const unsigned tb = 256, gb = (unsigned)((nb + tb - 1) / tb);
+  hipLaunchKernelGGL(ss_spec_kernel, dim3(gb), dim3(tb), 0, s, pk, reach, swo, n, nb, B);
+  hipLaunchKernelGGL(ss_land_kernel, dim3(gb), dim3(tb), 0, s, pk, nb, B);
+  hipLaunchKernelGGL(ss_land2_kernel, dim3((unsigned)((kSsCand * nb + tb - 1) / tb)), dim3(tb), 0, s, pk, nb, B);
+  hipLaunchKernelGGL(ss_group_kernel, dim3((unsigned)ng), dim3(64), 0, s, pk, nb, B);
+  hipLaunchKernelGGL(ss_top_kernel, dim3(1), dim3(64), 0, s, pk, nb, B);
+  hipLaunchKernelGGL(ss_cut_kernel, dim3(gb), dim3(tb), 0, s, nb, B);
+  hipLaunchKernelGGL(ss_bound_kernel, dim3((n + 1 + 63) / 64), dim3(64), 0, s, pk, swo, n, nb, in_off, B);
+  hipLaunchKernelGGL(ss_sub_kernel, dim3((unsigned)((nb + 1 + tb - 1) / tb)), dim3(tb), 0, s, swo, n, nb,
+                     (const uint64_t *)in_off, B);
+  dec_launch(ctx, false, (unsigned)((nb + 3) / 4), pk, B.sin, B.sswo, (uint32_t)nb, out, B.sst, 0,
+             DecStreams{nullptr, nullptr, nullptr, 0, nullptr}, s);
+  hipLaunchKernelGGL(ss_final_kernel, dim3(1), dim3(256), 0, s, n, nb, status, ctx->tickets + kTkDec, B,
+                     getenv("CPK_STREAM_NO_FALLBACK") ? 1 : 0);
+  // the one-wave decoder: no ticket unless the parallel path gave up
+  dec_launch(ctx, true, 1, pk, in_off, swo, n, out, status, avail,
+             DecStreams{nullptr, nullptr, nullptr, 1, in_off + n}, s);
+  return hip_ok(hipGetLastError());
+}
+}  // namespace
+
 int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
                       const uint64_t *d_swo, uint32_t n, void *d_out, uint64_t *d_in_off,
                       int32_t *d_status, void *stream) {
@@ -1373,6 +1470,19 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
   if (n == 0) return CPK_OK;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
+  if (avail >= kSsMin && !getenv("CPK_STREAM_ONE_WAVE")) {
+    // the stream's word count bounds the bytes worth cutting into blocks
+    // (the rest of `avail` may be later messages): read it back
+    uint64_t ends[2];
+    if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return CPK_EDEVICE;
+    const uint64_t reach = ss_reach(avail, ends[1] - ends[0]);
+    if (reach >= kSsMin)
+      return ss_decode(ctx, (const uint8_t *)d_packed, avail, reach, d_swo, n, (uint64_t *)d_out, d_in_off,
+                       d_status, s);
+  }
   if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
     return CPK_EDEVICE;
   // one stream: one wave works, the others find no ticket
@@ -1446,47 +1556,42 @@ int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
     h_in_off[0] = 0;
     return CPK_OK;
   }
-  DeviceGuard g(ctx->device);
-  uint64_t words = h_swo[n] - h_swo[0];
-  void *d_pk = nullptr, *d_out = nullptr;
-  uint64_t *d_swo = nullptr, *d_io = nullptr;
-  int32_t *d_st = nullptr;
-  int rc = CPK_OK;
-  std::vector<uint64_t> rs;
-  if (hipMalloc(&d_pk, avail + 64) != hipSuccess || hipMalloc(&d_out, words * 8 + 8) != hipSuccess ||
-      hipMalloc(&d_swo, (n + 1) * 8ull) != hipSuccess ||
-      hipMalloc(&d_io, (n + 1) * 8ull) != hipSuccess || hipMalloc(&d_st, n * 4ull) != hipSuccess) {
-    rc = CPK_ENOMEM;
-    goto done;
-  }
-  rs.resize(n + 1);
-  for (uint32_t i = 0; i <= n; ++i) rs[i] = h_swo[i] - h_swo[0];
-  if (hipMemset(d_pk, 0, avail + 64) ||
-      (avail && hipMemcpy(d_pk, h_packed, avail, hipMemcpyHostToDevice)) ||
-      hipMemcpy(d_swo, rs.data(), (n + 1) * 8ull, hipMemcpyHostToDevice)) {
-    rc = CPK_EDEVICE;
-    goto done;
-  }
-  rc = cpk_decode_stream(ctx, d_pk, avail, d_swo, n, d_out, d_io, d_st, nullptr);
-  if (rc) goto done;
-  if (hipMemcpy(h_status, d_st, n * 4ull, hipMemcpyDeviceToHost) ||
-      hipMemcpy(h_in_off, d_io, (n + 1) * 8ull, hipMemcpyDeviceToHost) ||
-      (words && hipMemcpy((uint8_t *)h_out + 8 * h_swo[0], d_out, words * 8, hipMemcpyDeviceToHost))) {
-    rc = CPK_EDEVICE;
-    goto done;
-  }
   for (uint32_t i = 0; i < n; ++i)
-    if (h_status[i] != CPK_OK) {
-      rc = h_status[i];
-      break;
-    }
-done:
-  if (d_pk) hipFree(d_pk);
-  if (d_out) hipFree(d_out);
-  if (d_swo) hipFree(d_swo);
-  if (d_io) hipFree(d_io);
-  if (d_st) hipFree(d_st);
-  return rc;
+    if (h_swo[i + 1] < h_swo[i]) return CPK_EINVAL;
+  const uint64_t words = h_swo[n] - h_swo[0];
+  if ((!h_packed && avail) || (!h_out && words)) return CPK_EINVAL;
+  DeviceGuard g(ctx->device);
+  // only the bytes the stream can reach are staged (the rest of `avail` may
+  // be later messages), through the context's pinned slot 0 (grow-only: no
+  // allocation once it is large enough)
+  const uint64_t R = ss_reach(avail, words);
+  HostPipe *p = nullptr;
+  // meta: swo | in_off | status (int32)
+  int rc = pipe_get(ctx, R, words * 8, 2 * (n + 1ull) + n / 2 + 1, &p);
+  if (rc) return rc;
+  HostSlot &sl = p->slot[0];
+  par_copy(sl.pin_in, h_packed, R);
+  memset((uint8_t *)sl.pin_in + R, 0, 64);  // (the decoder's read slack)
+  uint64_t *m = sl.pin_meta, *dm = sl.d_meta;
+  for (uint32_t i = 0; i <= n; ++i) m[i] = h_swo[i] - h_swo[0];
+  if (hipMemcpyAsync(sl.d_in, sl.pin_in, R + 64, hipMemcpyHostToDevice, p->sk) ||
+      hipMemcpyAsync(dm, m, (n + 1) * 8ull, hipMemcpyHostToDevice, p->sk))
+    return CPK_EDEVICE;
+  rc = cpk_decode_stream(ctx, sl.d_in, R, dm, n, sl.d_out, dm + n + 1, (int32_t *)(dm + 2 * (n + 1ull)), p->sk);
+  if (rc) {
+    pipe_drain(p);
+    return rc;
+  }
+  if (hipMemcpyAsync(m + n + 1, dm + n + 1, (n + 1) * 8ull + n * 4ull, hipMemcpyDeviceToHost, p->sk) ||
+      (words && hipMemcpyAsync(sl.pin_out, sl.d_out, words * 8, hipMemcpyDeviceToHost, p->sk)) ||
+      hipStreamSynchronize(p->sk))
+    return CPK_EDEVICE;
+  memcpy(h_in_off, m + n + 1, (n + 1) * 8ull);
+  memcpy(h_status, m + 2 * (n + 1ull), n * 4ull);
+  if (words) par_copy((uint8_t *)h_out + 8 * h_swo[0], sl.pin_out, words * 8);
+  for (uint32_t i = 0; i < n; ++i)
+    if (h_status[i] != CPK_OK) return h_status[i];
+  return CPK_OK;
 }
 
 int cpk_generate(cpk_ctx ctx, const cpk_gen_params *params, const uint64_t *d_swo, uint32_t n,

@@ -15,33 +15,6 @@ pytestmark = pytest.mark.gpu
 GOLD = json.loads((Path(__file__).parent / "golden" / "reference_kats.json").read_text())
 
 
-@pytest.fixture(scope="module", params=[("4", "1"), ("0", "2")],
-                ids=["enc-two-pass+dec-blockmap", "enc-single-pass+dec-index"])
-def ctx(request):
-    """A context per encoder / decoder pair (CPK_ENCODER, CPK_DECODER are read
-    at context creation): every parity case runs through the two-pass encoder
-    (encode_v4.hip) with the block-map decoder (decode_kernel), and through
-    the single-pass encoder (encode_sp.hip) with the record-index decoder
-    (decode_v2.hip)."""
-    import os
-    import torch
-    if not torch.cuda.is_available():
-        pytest.skip("needs a GPU")
-    import capnp_packed as cp
-    saved = {k: os.environ.get(k) for k in ("CPK_ENCODER", "CPK_DECODER")}
-    os.environ["CPK_ENCODER"], os.environ["CPK_DECODER"] = request.param
-    try:
-        c = cp.Context(0)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k)
-            else:
-                os.environ[k] = v
-    yield c
-    c.close()
-
-
 def _swo(sizes):
     return np.concatenate([[0], np.cumsum(np.asarray(sizes, dtype=np.uint64))]).astype(np.uint64)
 
