@@ -356,13 +356,17 @@ Context.encode_messages_host_gather = _encode_messages_host_gather
 Context.decode_messages_host = _decode_messages_host
 
 
-def _decode_stream_host(self, packed: np.ndarray, seg_word_off: np.ndarray):
+def _decode_stream_host(self, packed: np.ndarray, seg_word_off: np.ndarray, out: np.ndarray = None):
     """PackedInputStream.read per piece, back to back over one stream.
-    -> (decoded uint8 array, piece boundaries uint64[n+1], status int32[n])."""
+    -> (decoded uint8 array, piece boundaries uint64[n+1], status int32[n]).
+    `out`: a reusable uint8 buffer of at least 8 * seg_word_off[-1] bytes."""
     swo = np.ascontiguousarray(seg_word_off, dtype=np.uint64)
     n = len(swo) - 1
     pk = np.ascontiguousarray(packed, dtype=np.uint8)
-    out = np.zeros(int(8 * swo[-1]) + 8, dtype=np.uint8)
+    if out is None:
+        out = np.zeros(int(8 * swo[-1]) + 8, dtype=np.uint8)
+    elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < int(8 * swo[-1]):
+        raise ValueError("out: contiguous uint8, at least 8 * seg_word_off[-1] bytes")
     io = np.zeros(n + 1, dtype=np.uint64)
     st = np.zeros(max(n, 1), dtype=np.int32)
     rc = self._lib.cpk_decode_stream_host(self.handle, pk.ctypes.data if pk.size else None,

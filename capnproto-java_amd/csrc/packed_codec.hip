@@ -1441,19 +1441,26 @@ int ss_decode(cpk_ctx ctx, const uint8_t *pk, uint64_t avail, uint64_t reach, co
   if (hipMemsetAsync(B.N2, 0, 4 * nb, s) != hipSuccess || hipMemsetAsync(B.flag, 0, 8, s) != hipSuccess ||
       hipMemsetAsync(ctx->tickets + kTkDec, 0, 8 * kTkStride * 4, s) != hipSuccess)
     return CPK_EDEVICE;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void *)ss_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kSsLds) != hipSuccess)
+      return CPK_EDEVICE;
+    attr = true;
+  }
   const unsigned tb = 256, gb = (unsigned)((nb + tb - 1) / tb);
-  hipLaunchKernelGGL(ss_spec_kernel, dim3(gb), dim3(tb), 0, s, pk, reach, swo, n, nb, B);
-  hipLaunchKernelGGL(ss_land_kernel, dim3(gb), dim3(tb), 0, s, pk, nb, B);
-  hipLaunchKernelGGL(ss_land2_kernel, dim3((unsigned)((kSsCand * nb + tb - 1) / tb)), dim3(tb), 0, s, pk, nb, B);
+  const uint64_t nsub = (nb + kSsSub - 1) / kSsSub;
+  hipLaunchKernelGGL(ss_scan_kernel, dim3((unsigned)ng), dim3(kSsThreads), kSsLds, s, pk, reach, swo, n, nb, B);
   hipLaunchKernelGGL(ss_group_kernel, dim3((unsigned)ng), dim3(64), 0, s, pk, nb, B);
   hipLaunchKernelGGL(ss_top_kernel, dim3(1), dim3(64), 0, s, pk, nb, B);
   hipLaunchKernelGGL(ss_cut_kernel, dim3(gb), dim3(tb), 0, s, nb, B);
   hipLaunchKernelGGL(ss_bound_kernel, dim3((n + 1 + 63) / 64), dim3(64), 0, s, pk, swo, n, nb, in_off, B);
-  hipLaunchKernelGGL(ss_sub_kernel, dim3((unsigned)((nb + 1 + tb - 1) / tb)), dim3(tb), 0, s, swo, n, nb,
+  hipLaunchKernelGGL(ss_sub_kernel, dim3((unsigned)((nsub + 1 + tb - 1) / tb)), dim3(tb), 0, s, swo, n, nb,
                      (const uint64_t *)in_off, B);
-  dec_launch(ctx, false, (unsigned)((nb + 3) / 4), pk, B.sin, B.sswo, (uint32_t)nb, out, B.sst, 0,
+  dec_launch(ctx, false, (unsigned)((nsub + 3) / 4), pk, B.sin, B.sswo, (uint32_t)nsub, out, B.sst, 0,
              DecStreams{nullptr, nullptr, nullptr, 0, nullptr}, s);
-  hipLaunchKernelGGL(ss_final_kernel, dim3(1), dim3(256), 0, s, n, nb, status, ctx->tickets + kTkDec, B,
+  hipLaunchKernelGGL(ss_check_kernel, dim3((unsigned)((nsub + tb - 1) / tb)), dim3(tb), 0, s, nsub, B);
+  hipLaunchKernelGGL(ss_final_kernel, dim3((n + tb - 1) / tb), dim3(tb), 0, s, n, status, ctx->tickets + kTkDec, B,
                      getenv("CPK_STREAM_NO_FALLBACK") ? 1 : 0);
   // the one-wave decoder: no ticket unless the parallel path gave up
   dec_launch(ctx, true, 1, pk, in_off, swo, n, out, status, avail,

@@ -3,24 +3,27 @@
 // PackedInputStream, Serialize.java:165-175, PackedInputStream.java:35-140).
 // Included by packed_codec.hip.
 //
-// The stream is cut into 1 KiB blocks.  A record (tag, its bytes, the run
+// The stream is cut into 256-byte blocks.  A record (tag, its bytes, the run
 // count, the literal words) has a length that depends on its own bytes only,
 // so a walk from any true record start follows the true parse; the problem is
 // to know, per block, where the first true record in it starts.
-//   ss_spec   per block, a speculative walk from the block's first byte:
-//             exit X_b (first record start at/after the block end) and the
-//             words of the records it starts in the block, W_b.
-//   ss_land   per block, a walk from X_{b-1} (the guess of its true entry)
+//   ss_scan   per group of 256 blocks (bytes staged in LDS, a thread per
+//             block): a speculative walk from the block's first byte: exit
+//             X_b (first record start at/after the block end) and the words
+//             of the records it starts in the block, W_b; then a walk from
+//             X_{b-1} (the guess of its true entry)
 //             merged with the speculative walk: once the two meet they agree
 //             to the end of the block, so the exit is X_b and the words
 //             follow from W_b.  Non-meeting walks run to the block end.  A
 //             landing that skips blocks or misses the guess (long literal
 //             runs, non-convergence) registers its exit as a second guess of
-//             the block it lands in; ss_land2 walks those.
-//   ss_group  per 64 blocks (one wave), the blocks resolved one after another
-//             for each guess of the group's entry: a block whose entry lies
-//             past its end is crossed by a record (no words), an entry equal
-//             to a guess takes that walk's result, any other is walked here.
+//             the block it lands in, which is walked too.
+//   ss_group  per group (one wave), the blocks resolved in order for each
+//             guess of the group's entry, 64 at a time: runs of blocks whose
+//             entry is their first guess are taken at once; a block whose
+//             entry lies past its end is crossed by a record (no words), an
+//             entry equal to a second guess takes that walk's result, any
+//             other is walked here.
 //   ss_top    one wave chains the groups (a group whose entry was not guessed
 //             is resolved again with the true entry) and scans the words.
 //   ss_cut    per block its first record and first word, clamped to the end
@@ -33,8 +36,8 @@
 // gives the reference's exact error behaviour; on the good path its tickets
 // are taken away and it exits at once.
 
-constexpr uint32_t kSsBlock = 1024;   // bytes per block
-constexpr uint32_t kSsGroup = 64;     // blocks per group (one wave)
+constexpr uint32_t kSsBlock = 256;    // bytes per block
+constexpr uint32_t kSsGroup = 256;    // blocks per group (a workgroup's scan, a wave's resolution)
 constexpr uint32_t kSsCand = 2;       // second guesses kept per block
 constexpr uint32_t kSsVar = 1 + kSsCand;  // group variants: guess 1, second guesses
 constexpr uint64_t kSsInf = ~0ull;    // a walk that ran past the end of the bytes
@@ -57,10 +60,23 @@ struct SsBufs {
   uint64_t *lim;            // [0]: R, bytes the walks may read; [1]: words wanted
 };
 
+// byte sources for the walks: the stream in HBM, or a group's bytes staged
+// in LDS ([s0, s1) of the stream; every walk of the group stays inside)
+struct SsGlobal {
+  const uint8_t *pk;
+  uint64_t R;
+  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return pk[min(p, R - 1)]; }
+};
+struct SsLds {
+  const uint8_t *lds;
+  uint64_t s0, s1;
+  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return lds[min(p, s1 - 1) - s0]; }
+};
+
 // one record from p (< R): false if it runs past R
-__device__ __forceinline__ bool ss_step(const uint8_t *__restrict__ pk, uint64_t R, uint64_t &p, uint64_t &w) {
-  const uint32_t t = pk[p];
-  const uint32_t c1 = pk[min(p + 1, R - 1)], c9 = pk[min(p + 9, R - 1)];
+template <class Rd>
+__device__ __forceinline__ bool ss_step(const Rd &rd, uint64_t R, uint64_t &p, uint64_t &w) {
+  const uint32_t t = rd(p), c1 = rd(p + 1), c9 = rd(p + 9);
   uint64_t len = 1u + (uint32_t)__builtin_popcount(t), wd = 1;
   if (t == 0) {
     len = 2;
@@ -78,8 +94,9 @@ __device__ __forceinline__ bool ss_step(const uint8_t *__restrict__ pk, uint64_t
 __device__ __forceinline__ uint64_t ss_end(uint64_t b, uint64_t R) { return min(b * kSsBlock + kSsBlock, R); }
 
 // the block's exit and words for entry e (merged with its speculative walk)
-__device__ __forceinline__ void ss_from(const uint8_t *__restrict__ pk, uint64_t R, uint64_t b, uint64_t e,
-                                        uint64_t Xb, uint64_t Wb, uint64_t &exit, uint64_t &words) {
+template <class Rd>
+__device__ __forceinline__ void ss_from(const Rd &rd, uint64_t R, uint64_t b, uint64_t e, uint64_t Xb,
+                                        uint64_t Wb, uint64_t &exit, uint64_t &words) {
   const uint64_t end = ss_end(b, R);
   if (e >= end) {  // a record crosses the whole block (or the walk is dead)
     exit = e;
@@ -94,8 +111,8 @@ __device__ __forceinline__ void ss_from(const uint8_t *__restrict__ pk, uint64_t
       return;
     }
     if (s < t) {
-      if (!ss_step(pk, R, s, ws)) s = kSsInf;
-    } else if (!ss_step(pk, R, t, wt)) {
+      if (!ss_step(rd, R, s, ws)) s = kSsInf;
+    } else if (!ss_step(rd, R, t, wt)) {
       exit = kSsInf;
       words = wt;
       return;
@@ -111,63 +128,161 @@ __device__ __forceinline__ uint64_t ss_R(const uint64_t *swo, uint32_t n, uint64
   return min(avail, 10 * total + 16);
 }
 
-__global__ __launch_bounds__(256) void ss_spec_kernel(const uint8_t *__restrict__ pk, uint64_t avail,
-                                                      const uint64_t *__restrict__ swo, uint32_t n, uint64_t nbmax,
-                                                      SsBufs B) {
+// The walks on a group's staged bytes: positions relative to the staged
+// start (u32), the three bytes a record may need read together, no branches.
+struct SsLw {
+  const uint8_t *lds;
+  uint32_t last;  // staged bytes - 1
+  uint32_t rlim;  // R - s0 (clamped): a record may not end past it
+  __device__ __forceinline__ bool step(uint32_t &p, uint32_t &w) const {
+    const uint32_t t = lds[min(p, last)], c1 = lds[min(p + 1, last)], c9 = lds[min(p + 9, last)];
+    const uint32_t len = t == 0 ? 2u : (t == 0xffu ? 10u + 8u * c9 : 1u + (uint32_t)__builtin_popcount(t));
+    const uint32_t wd = t == 0 ? 1u + c1 : (t == 0xffu ? 1u + c9 : 1u);
+    if (p + len > rlim) return false;
+    p += len;
+    w += wd;
+    return true;
+  }
+  // ss_from on the staged bytes: block start bs, end be (relative)
+  __device__ __forceinline__ void from(uint32_t bs, uint32_t be, uint32_t e, uint32_t Xb, uint32_t Wb,
+                                       uint32_t &exit, uint32_t &words) const {
+    if (e >= be) {
+      exit = e;
+      words = 0;
+      return;
+    }
+    uint32_t t = e, wt = 0, s = bs, ws = 0;
+    while (t < be) {
+      if (s == t) {
+        exit = Xb;
+        words = wt + (Wb - ws);
+        return;
+      }
+      if (s < t) {
+        if (!step(s, ws)) s = ~0u;
+      } else if (!step(t, wt)) {
+        exit = ~0u;
+        words = wt;
+        return;
+      }
+    }
+    exit = t;
+    words = wt;
+  }
+};
+
+// A group's walks run on its bytes staged in LDS: its blocks, the block
+// before (whose speculative exit is block b0's first guess) and the 9 after
+// (a record is at most 2050 bytes, so a landing from the group's blocks ends
+// at most 9 blocks further on), plus the longest record past those.
+constexpr uint32_t kSsPre = 1, kSsPost = 9;
+constexpr uint32_t kSsLocal = kSsPre + kSsGroup + kSsPost;                      // blocks walked
+constexpr uint32_t kSsStage = ((kSsLocal * kSsBlock + 2064) + 15) & ~15u;      // bytes staged
+constexpr uint32_t kSsoX = kSsStage, kSsoW = kSsoX + 4 * kSsLocal, kSsoN = kSsoW + 4 * kSsLocal;
+constexpr uint32_t kSsoC = kSsoN + 4 * kSsLocal;
+constexpr uint32_t kSsLds = kSsoC + 4 * kSsCand * kSsLocal;  // 75,480 B: two groups per CU
+constexpr uint32_t kSsThreads = kSsGroup;  // a thread per block
+constexpr uint32_t kSsStageLoads = (kSsStage / 16 + kSsThreads - 1) / kSsThreads;
+
+// a workgroup per group: speculative walks, landing walks from the previous
+// block's speculative exit, and walks from the landings' exits (the second
+// guesses of the blocks they land in, published in global slots)
+__global__ __launch_bounds__(kSsThreads) void ss_scan_kernel(const uint8_t *__restrict__ pk, uint64_t avail,
+                                                     const uint64_t *__restrict__ swo, uint32_t n, uint64_t nbmax,
+                                                     SsBufs B) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint64_t R = ss_R(swo, n, avail);
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b == 0) {
+  const uint32_t t = threadIdx.x;
+  if (blockIdx.x == 0 && t == 0) {
     B.lim[0] = R;
     B.lim[1] = swo[n] - swo[0];
   }
-  if (b >= nbmax || b * kSsBlock >= R) return;
-  const uint64_t end = ss_end(b, R);
-  uint64_t p = b * kSsBlock, w = 0;
-  while (p < end)
-    if (!ss_step(pk, R, p, w)) {
-      p = kSsInf;
-      break;
+  const uint64_t nb = min(nbmax, (R + kSsBlock - 1) / kSsBlock);
+  const uint64_t b0 = (uint64_t)blockIdx.x * kSsGroup;
+  if (b0 >= nb) return;
+  const uint64_t lb0 = b0 ? b0 - kSsPre : 0, lb1 = min(nb, b0 + kSsGroup + kSsPost);
+  const uint32_t L = (uint32_t)(lb1 - lb0);
+  const uint64_t s0 = lb0 * kSsBlock, s1 = min(R, lb1 * kSsBlock + 2064);
+  uint32_t *lx = reinterpret_cast<uint32_t *>(smem + kSsoX);
+  uint32_t *lw = reinterpret_cast<uint32_t *>(smem + kSsoW);
+  uint32_t *lnc = reinterpret_cast<uint32_t *>(smem + kSsoN);
+  uint32_t *lc = reinterpret_cast<uint32_t *>(smem + kSsoC);
+  // stage [s0, s1) (16-byte loads: the stream is readable to a 16-byte
+  // bound), all of a thread's loads in flight before its LDS writes
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(pk + s0);
+    uint4 *dst = reinterpret_cast<uint4 *>(smem);
+    const uint32_t lines = (uint32_t)((s1 - s0 + 15) / 16);
+    uint4 v[kSsStageLoads];
+#pragma unroll
+    for (uint32_t k = 0; k < kSsStageLoads; ++k) v[k] = src[min(t + k * kSsThreads, lines - 1)];
+#pragma unroll
+    for (uint32_t k = 0; k < kSsStageLoads; ++k) {
+      const uint32_t i = t + k * kSsThreads;
+      if (i < lines) dst[i] = v[k];
     }
-  B.X[b] = p;
-  B.W[b] = w;
-}
-
-__device__ __forceinline__ void ss_push(SsBufs &B, uint64_t R, uint64_t c, uint64_t e) {
-  const uint32_t k = atomicAdd(&B.N2[c], 1u);
-  if (k < kSsCand) B.C2[c * kSsCand + k] = e;
-  (void)R;
-}
-
-__global__ __launch_bounds__(256) void ss_land_kernel(const uint8_t *__restrict__ pk, uint64_t nbmax, SsBufs B) {
-  const uint64_t R = B.lim[0];
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nb = (R + kSsBlock - 1) / kSsBlock;
-  if (b >= nbmax || b >= nb) return;
-  const uint64_t e = b ? B.X[b - 1] : 0;
-  uint64_t x, w;
-  ss_from(pk, R, b, e, B.X[b], B.W[b], x, w);
-  B.C1[b] = e;
-  B.L1[b] = x;
-  B.WL1[b] = w;
-  // where the true parse goes next if e was right: a guess for that block
-  if (x < R) {
-    const uint64_t c = x / kSsBlock;
-    if (x != B.X[c - 1]) ss_push(B, R, c, x);
+    for (uint32_t i = t; i < kSsLocal; i += kSsThreads) lnc[i] = 0;
   }
-}
-
-__global__ __launch_bounds__(256) void ss_land2_kernel(const uint8_t *__restrict__ pk, uint64_t nbmax, SsBufs B) {
-  const uint64_t R = B.lim[0];
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t nb = (R + kSsBlock - 1) / kSsBlock;
-  const uint64_t b = i / kSsCand;
-  const uint32_t k = (uint32_t)(i % kSsCand);
-  if (b >= nbmax || b >= nb || k >= min(B.N2[b], kSsCand)) return;
-  const uint64_t e = B.C2[i];
-  uint64_t x, w;
-  ss_from(pk, R, b, e, B.X[b], B.W[b], x, w);
-  B.L2[i] = x;
-  B.WL2[i] = w;
+  __syncthreads();
+  const SsLw wk{smem, (uint32_t)(s1 - s0 - 1), (uint32_t)min(R - s0, (uint64_t)0xffffffffu)};
+  const uint32_t rel_end = (uint32_t)(min(R, lb1 * kSsBlock) - s0);  // (relative end of the last local block)
+  auto rel = [&](uint32_t v) -> uint64_t { return v == ~0u ? kSsInf : s0 + v; };
+  // speculative walks of the local blocks (relative exits; ~0u: past R)
+  for (uint32_t j = t; j < L; j += kSsThreads) {
+    const uint32_t bs = j * kSsBlock, be = min(bs + kSsBlock, rel_end);
+    uint32_t p = bs, w = 0;
+    while (p < be)
+      if (!wk.step(p, w)) {
+        p = ~0u;
+        break;
+      }
+    lx[j] = p;
+    lw[j] = w;
+    const uint64_t b = lb0 + j;
+    if (b >= b0 && b < b0 + kSsGroup) {
+      B.X[b] = rel(p);
+      B.W[b] = w;
+    }
+  }
+  __syncthreads();
+  // landing walks of the group's blocks
+  const uint64_t b = b0 + t;
+  if (b < nb) {
+    const uint32_t j = (uint32_t)(b - lb0);
+    const uint32_t bs = j * kSsBlock, be = min(bs + kSsBlock, rel_end);
+    const uint32_t e = b ? lx[j - 1] : 0u;
+    uint32_t x, w;
+    wk.from(bs, be, e, lx[j], lw[j], x, w);
+    B.C1[b] = rel(e);
+    B.L1[b] = rel(x);
+    B.WL1[b] = w;
+    // where the true parse goes next if e was right: a guess for that block
+    if (x != ~0u && s0 + x < R) {
+      const uint32_t c = x / kSsBlock;  // (local; j < c <= j + kSsPost)
+      if (c < L && x != lx[c - 1]) {
+        const uint32_t k = atomicAdd(&lnc[c], 1u);
+        if (k < kSsCand) lc[c * kSsCand + k] = x;
+      }
+    }
+  }
+  __syncthreads();
+  // the second guesses: blocks b0 + 1 .. lb1 - 1
+  for (uint32_t j = (uint32_t)(b0 + 1 - lb0) + t; j < L; j += kSsThreads) {
+    const uint32_t cnt = min(lnc[j], kSsCand);
+    const uint64_t c = lb0 + j;
+    const uint32_t bs = j * kSsBlock, be = min(bs + kSsBlock, rel_end);
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const uint32_t e = lc[j * kSsCand + k];
+      uint32_t x, w;
+      wk.from(bs, be, e, lx[j], lw[j], x, w);
+      const uint32_t slot = atomicAdd(&B.N2[c], 1u);
+      if (slot < kSsCand) {
+        B.C2[c * kSsCand + slot] = rel(e);
+        B.L2[c * kSsCand + slot] = rel(x);
+        B.WL2[c * kSsCand + slot] = w;
+      }
+    }
+  }
 }
 
 __device__ __forceinline__ uint64_t ss_rl64(uint64_t v, int l) {
@@ -175,62 +290,13 @@ __device__ __forceinline__ uint64_t ss_rl64(uint64_t v, int l) {
          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
 }
 
-// The group's blocks resolved in order from entry e (wave-uniform loop; the
-// lanes hold the blocks' walk results).  Lane i receives block b0 + i's entry
-// and the words of the blocks before it in the group; returns the exit and
-// the group's words.
 struct SsLane {
   uint64_t c1, l1, w1, c2[kSsCand], l2[kSsCand], w2[kSsCand], X, W;
   uint32_t n2;
 };
-__device__ __forceinline__ void ss_chain(const uint8_t *__restrict__ pk, uint64_t R, uint64_t b0, uint32_t cnt,
-                                         const SsLane &L, uint64_t e, int lane, uint64_t &ve, uint32_t &vw,
-                                         uint64_t &exit, uint64_t &words) {
-  uint64_t acc = 0;
-  ve = 0;
-  vw = 0;
-  for (uint32_t i = 0; i < cnt; ++i) {
-    const uint64_t b = b0 + i;
-    if ((uint32_t)lane == i) {
-      ve = e;
-      vw = (uint32_t)acc;
-    }
-    uint64_t x, w;
-    if (e >= ss_end(b, R)) {
-      x = e;
-      w = 0;
-    } else if (e == ss_rl64(L.c1, (int)i)) {
-      x = ss_rl64(L.l1, (int)i);
-      w = ss_rl64(L.w1, (int)i);
-    } else {
-      const uint32_t n2 = (uint32_t)__builtin_amdgcn_readlane((int)L.n2, (int)i);
-      int hit = -1;
-#pragma unroll
-      for (int k = 0; k < (int)kSsCand; ++k)
-        if (hit < 0 && (uint32_t)k < n2 && e == ss_rl64(L.c2[k], (int)i)) hit = k;
-      if (hit >= 0) {
-        uint64_t xs = 0, ws = 0;
-#pragma unroll
-        for (int k = 0; k < (int)kSsCand; ++k)
-          if (k == hit) {
-            xs = ss_rl64(L.l2[k], (int)i);
-            ws = ss_rl64(L.w2[k], (int)i);
-          }
-        x = xs;
-        w = ws;
-      } else {
-        ss_from(pk, R, b, e, ss_rl64(L.X, (int)i), ss_rl64(L.W, (int)i), x, w);
-      }
-    }
-    acc += w;
-    e = x;
-  }
-  exit = e;
-  words = acc;
-}
 
 __device__ __forceinline__ void ss_load_lane(const SsBufs &B, uint64_t b, bool ok, SsLane &L) {
-  L.c1 = ok ? B.C1[b] : 0;
+  L.c1 = ok ? B.C1[b] : kSsInf - 1;
   L.l1 = ok ? B.L1[b] : 0;
   L.w1 = ok ? B.WL1[b] : 0;
   L.X = ok ? B.X[b] : 0;
@@ -245,6 +311,90 @@ __device__ __forceinline__ void ss_load_lane(const SsBufs &B, uint64_t b, bool o
   }
 }
 
+__device__ __forceinline__ uint64_t ss_scan_add(uint64_t w, int lane) {  // inclusive, over the wave
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(w, d, 64);
+    if (lane >= d) w += o;
+  }
+  return w;
+}
+
+// Resolves blocks [b0, b0 + cnt) in order from entry e (one wave, 64 blocks
+// at a time): a run of blocks each entered at its first guess is taken at
+// once (lane-parallel check); the block that breaks the run is crossed by a
+// record, matches a second guess, or is walked.  Row `row` of VE / VW gets
+// each block's entry and the words of the group's blocks before it.
+__device__ void ss_chain(const uint8_t *__restrict__ pk, uint64_t R, const SsBufs &B, uint64_t nbmax, uint64_t b0,
+                         uint32_t cnt, uint64_t e, uint32_t row, int lane, uint64_t &exit, uint64_t &words) {
+  uint64_t acc = 0;
+  for (uint32_t base = 0; base < cnt; base += 64) {
+    const uint32_t m = min(64u, cnt - base);
+    const bool ok = (uint32_t)lane < m;
+    const uint64_t b = b0 + base + (uint64_t)lane;
+    SsLane L;
+    ss_load_lane(B, b, ok, L);
+    const uint64_t px = __shfl_up(L.l1, 1, 64);
+    uint64_t ve = 0, vw = 0;
+    uint32_t k = 0;
+    while (k < m) {
+      // optimistic from lane k: lane k enters at e, a later lane at the
+      // first-guess exit of the lane before it
+      const uint64_t ent = (uint32_t)lane == k ? e : px;
+      const uint64_t bad = __ballot(ok && (uint32_t)lane >= k && ent != L.c1);
+      const uint32_t r = bad ? (uint32_t)__builtin_ctzll(bad) : m;
+      const bool in = (uint32_t)lane >= k && (uint32_t)lane < r;
+      const uint64_t w = ss_scan_add(in ? L.w1 : 0, lane);
+      if (in) {
+        ve = ent;
+        vw = acc + w - L.w1;
+      }
+      if (r > k) {
+        acc += ss_rl64(w, (int)r - 1);
+        e = ss_rl64(L.l1, (int)r - 1);
+      }
+      if (r >= m) break;
+      // lane r
+      uint64_t x, wr;
+      const uint64_t br = b0 + base + r;
+      if (e >= ss_end(br, R)) {  // a record crosses the whole block
+        x = e;
+        wr = 0;
+      } else {
+        const uint32_t n2 = (uint32_t)__builtin_amdgcn_readlane((int)L.n2, (int)r);
+        int hit = -1;
+#pragma unroll
+        for (int q = 0; q < (int)kSsCand; ++q)
+          if (hit < 0 && (uint32_t)q < n2 && e == ss_rl64(L.c2[q], (int)r)) hit = q;
+        if (hit >= 0) {
+          x = 0;
+          wr = 0;
+#pragma unroll
+          for (int q = 0; q < (int)kSsCand; ++q)
+            if (q == hit) {
+              x = ss_rl64(L.l2[q], (int)r);
+              wr = ss_rl64(L.w2[q], (int)r);
+            }
+        } else {
+          ss_from(SsGlobal{pk, R}, R, br, e, ss_rl64(L.X, (int)r), ss_rl64(L.W, (int)r), x, wr);
+        }
+      }
+      if ((uint32_t)lane == r) {
+        ve = e;
+        vw = acc;
+      }
+      acc += wr;
+      e = x;
+      k = r + 1;
+    }
+    if (ok) {
+      B.VE[row * nbmax + b] = ve;
+      B.VW[row * nbmax + b] = (uint32_t)vw;
+    }
+  }
+  exit = e;
+  words = acc;
+}
+
 // one wave per group, each guess of the group's entry
 __global__ __launch_bounds__(64) void ss_group_kernel(const uint8_t *__restrict__ pk, uint64_t nbmax, SsBufs B) {
   const uint64_t R = B.lim[0];
@@ -254,29 +404,12 @@ __global__ __launch_bounds__(64) void ss_group_kernel(const uint8_t *__restrict_
   if (b0 >= nb) return;
   const int lane = (int)threadIdx.x;
   const uint32_t cnt = (uint32_t)min((uint64_t)kSsGroup, nb - b0);
-  const uint64_t b = b0 + (uint64_t)lane;
-  SsLane L;
-  ss_load_lane(B, b, (uint32_t)lane < cnt, L);
-  const uint32_t n20 = (uint32_t)__builtin_amdgcn_readlane((int)L.n2, 0);
+  const uint32_t n20 = min(B.N2[b0], kSsCand);
   for (uint32_t v = 0; v < kSsVar; ++v) {
-    uint64_t e;
-    bool have = true;
-    if (v == 0) {
-      e = ss_rl64(L.c1, 0);
-    } else {
-      have = v - 1 < n20;
-      e = 0;
-#pragma unroll
-      for (int k = 0; k < (int)kSsCand; ++k)
-        if ((uint32_t)k == v - 1) e = ss_rl64(L.c2[k], 0);
-    }
-    uint64_t ve = 0, x = kSsInf, w = 0;
-    uint32_t vw = 0;
-    if (have) ss_chain(pk, R, b0, cnt, L, e, lane, ve, vw, x, w);
-    if ((uint32_t)lane < cnt) {
-      B.VE[v * nbmax + b] = ve;
-      B.VW[v * nbmax + b] = vw;
-    }
+    const bool have = v == 0 || v - 1 < n20;
+    const uint64_t e = v == 0 ? B.C1[b0] : (have ? B.C2[b0 * kSsCand + v - 1] : 0);
+    uint64_t x = kSsInf, w = 0;
+    if (have) ss_chain(pk, R, B, nbmax, b0, cnt, e, v, lane, x, w);
     if (lane == 0) {
       B.GE[g * kSsVar + v] = have ? e : kSsInf - 1;  // (no guess: never matches)
       B.GX[g * kSsVar + v] = x;
@@ -304,34 +437,24 @@ __global__ __launch_bounds__(64) void ss_top_kernel(const uint8_t *__restrict__ 
       gw[v] = ok ? B.GW[g * kSsVar + v] : 0;
     }
     const uint32_t cnt = (uint32_t)min((uint64_t)64, ng - g0);
+    const uint64_t px = __shfl_up(gx[0], 1, 64);
     uint32_t ch = 0;
     uint64_t gb = 0;
     uint32_t i = 0;
     while (i < cnt) {
       // optimistic: from lane i on, every group entered by its first guess
-      const uint64_t px = __shfl_up(gx[0], 1, 64);
-      const bool chain = (uint32_t)lane > i ? (px == ge[0]) : ((uint32_t)lane == i ? e == ge[0] : true);
-      const uint64_t bad = __ballot((uint32_t)lane >= i && (uint32_t)lane < cnt && !chain);
+      const uint64_t ent = (uint32_t)lane == i ? e : px;
+      const uint64_t bad = __ballot((uint32_t)lane >= i && (uint32_t)lane < cnt && ent != ge[0]);
       const uint32_t k = bad ? (uint32_t)__builtin_ctzll(bad) : cnt;  // first group off the guess
-      // lanes [i, k): variant 0, words scanned
-      {
-        const bool in = (uint32_t)lane >= i && (uint32_t)lane < k;
-        uint64_t w = in ? gw[0] : 0;
-        // inclusive scan (u64 via two 32-bit halves would overflow-carry;
-        // the group words fit 40 bits: scan with shuffles)
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint64_t o = __shfl_up(w, d, 64);
-          if (lane >= d) w += o;
-        }
-        const uint64_t own = in ? gw[0] : 0;
-        if (in) {
-          ch = 0;
-          gb = wsum + w - own;
-        }
-        if (k > i) {
-          wsum += ss_rl64(w, (int)k - 1);
-          e = ss_rl64(gx[0], (int)k - 1);
-        }
+      const bool in = (uint32_t)lane >= i && (uint32_t)lane < k;
+      const uint64_t w = ss_scan_add(in ? gw[0] : 0, lane);
+      if (in) {
+        ch = 0;
+        gb = wsum + w - gw[0];
+      }
+      if (k > i) {
+        wsum += ss_rl64(w, (int)k - 1);
+        e = ss_rl64(gx[0], (int)k - 1);
       }
       if (k >= cnt) break;
       // group k: another guess, or resolved again with the true entry
@@ -339,35 +462,24 @@ __global__ __launch_bounds__(64) void ss_top_kernel(const uint8_t *__restrict__ 
 #pragma unroll
       for (int v = 1; v < (int)kSsVar; ++v)
         if (hit < 0 && e == ss_rl64(ge[v], (int)k)) hit = v;
-      uint64_t x, w;
+      uint64_t x = 0, wk = 0;
       if (hit >= 0) {
-        x = 0;
-        w = 0;
 #pragma unroll
         for (int v = 1; v < (int)kSsVar; ++v)
           if (v == hit) {
             x = ss_rl64(gx[v], (int)k);
-            w = ss_rl64(gw[v], (int)k);
+            wk = ss_rl64(gw[v], (int)k);
           }
       } else {
-        const uint64_t gk = g0 + k, b0 = gk * kSsGroup;
-        const uint32_t bc = (uint32_t)min((uint64_t)kSsGroup, nb - b0);
-        SsLane L;
-        ss_load_lane(B, b0 + (uint64_t)lane, (uint32_t)lane < bc, L);
-        uint64_t ve;
-        uint32_t vw;
-        ss_chain(pk, R, b0, bc, L, e, lane, ve, vw, x, w);
-        if ((uint32_t)lane < bc) {
-          B.VE[kSsVar * nbmax + b0 + lane] = ve;
-          B.VW[kSsVar * nbmax + b0 + lane] = vw;
-        }
+        const uint64_t b0 = (g0 + k) * kSsGroup;
+        ss_chain(pk, R, B, nbmax, b0, (uint32_t)min((uint64_t)kSsGroup, nb - b0), e, kSsVar, lane, x, wk);
         hit = (int)kSsVar;
       }
       if ((uint32_t)lane == k) {
         ch = (uint32_t)hit;
         gb = wsum;
       }
-      wsum += w;
+      wsum += wk;
       e = x;
       i = k + 1;
     }
@@ -419,7 +531,7 @@ __global__ __launch_bounds__(64) void ss_bound_kernel(const uint8_t *__restrict_
   uint64_t p = B.E[lo], w = B.WO[lo];
   bool good = p < kSsInf;
   while (good && w < T) {
-    if (p >= R || !ss_step(pk, R, p, w)) good = false;
+    if (p >= R || !ss_step(SsGlobal{pk, R}, R, p, w)) good = false;
   }
   if (!good || w != T) {
     atomicOr(&B.flag[0], 1u);  // truncated / a run across the boundary
@@ -428,21 +540,38 @@ __global__ __launch_bounds__(64) void ss_bound_kernel(const uint8_t *__restrict_
   in_off[j] = p;
 }
 
-// the blocks as batch pieces, clamped to the last piece's end
+// the blocks, kSsSub at a time, as batch pieces, clamped to the last piece's
+// end (a few large pieces keep the batch decoder's waves busy; one per block
+// would spend them on per-piece setup)
+#ifndef CPK_SS_SUB
+#define CPK_SS_SUB 32
+#endif
+constexpr uint32_t kSsSub = CPK_SS_SUB;
 __global__ __launch_bounds__(256) void ss_sub_kernel(const uint64_t *__restrict__ swo, uint32_t n, uint64_t nbmax,
                                                      const uint64_t *__restrict__ in_off, SsBufs B) {
   const uint64_t R = B.lim[0];
   const uint64_t nb = min(nbmax, (R + kSsBlock - 1) / kSsBlock);
-  const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > nbmax) return;
-  const uint64_t T = B.lim[1], endp = in_off[n];
-  uint64_t e = endp, wo = T;
-  if (b <= nb && B.WO[b] < T) {
-    e = B.E[b];
-    wo = B.WO[b];
+  const uint64_t nsub = (nbmax + kSsSub - 1) / kSsSub;
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > nsub) return;
+  const uint64_t b = min(k * kSsSub, nb);
+  const uint64_t T = B.lim[1];
+  uint64_t e = 0, wo = 0;  // (a failed resolution: every piece empty)
+  if (B.flag[0] == 0) {
+    e = in_off[n];
+    wo = T;
+    if (B.WO[b] < T) {
+      e = B.E[b];
+      wo = B.WO[b];
+    }
   }
-  B.sin[b] = e;
-  B.sswo[b] = swo[0] + wo;
+  B.sin[k] = e;
+  B.sswo[k] = swo[0] + wo;
+}
+
+__global__ __launch_bounds__(256) void ss_check_kernel(uint64_t nsub, SsBufs B) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (__ballot(k < nsub && B.sst[k] != CPK_OK) && (threadIdx.x & 63) == 0) atomicOr(&B.flag[0], 2u);
 }
 
 // good path: statuses, and the fallback decoder's tickets taken away
@@ -450,15 +579,10 @@ __global__ __launch_bounds__(256) void ss_sub_kernel(const uint64_t *__restrict_
 // stream the parallel path gives up on is reported as CPK_EUNSUPPORTED
 // instead of being decoded by one wave -- tests use it to show that the
 // parallel path itself decoded a stream)
-__global__ __launch_bounds__(256) void ss_final_kernel(uint32_t n, uint64_t nbmax, int32_t *__restrict__ status,
-                                                       uint32_t *tickets, SsBufs B, int no_fallback) {
-  __shared__ int bad;
-  if (threadIdx.x == 0) bad = (int)B.flag[0];
-  __syncthreads();
-  for (uint64_t b = threadIdx.x; b < nbmax; b += blockDim.x)
-    if (B.sst[b] != CPK_OK) bad = 1;
-  __syncthreads();
-  if (!bad || no_fallback)
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) status[i] = bad ? CPK_EUNSUPPORTED : CPK_OK;
-  if (threadIdx.x < 8) tickets[threadIdx.x * kTkStride] = (bad && !no_fallback) ? 0u : 0x40000000u;
+__global__ __launch_bounds__(256) void ss_final_kernel(uint32_t n, int32_t *__restrict__ status, uint32_t *tickets,
+                                                       SsBufs B, int no_fallback) {
+  const bool bad = B.flag[0] != 0;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if ((!bad || no_fallback) && i < n) status[i] = bad ? CPK_EUNSUPPORTED : CPK_OK;
+  if (blockIdx.x == 0 && threadIdx.x < 8) tickets[threadIdx.x * kTkStride] = (bad && !no_fallback) ? 0u : 0x40000000u;
 }
