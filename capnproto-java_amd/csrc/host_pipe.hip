@@ -425,31 +425,48 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
 
 }  // extern "C"
 
-// ---- message batches from host memory (staged whole; SerializePacked.write /
-// read for many messages, the JNI facade's encodeMessages / decodeMessages) --
+// ---- message batches from host memory (SerializePacked.write / read for
+// many messages, the JNI facade's encodeMessages / decodeMessages): chunks of
+// whole messages through the same two pinned slots as the piece forms
 namespace {
-struct DevBufs {  // hipFree on scope exit
-  std::vector<void *> p;
-  void *get(uint64_t bytes) {
-    void *q = nullptr;
-    if (hipMalloc(&q, bytes ? bytes : 16) != hipSuccess) return nullptr;
-    p.push_back(q);
-    return q;
-  }
-  ~DevBufs() {
-    for (void *q : p) hipFree(q);
-  }
+
+struct MsgChunk {
+  uint32_t m0, m1;    // messages [m0, m1)
+  uint64_t s0, s1;    // their segments (encode) / none (decode)
+  uint64_t in0, in_len;  // input bytes: segment words (encode) / packed (decode)
+  uint64_t out_cap;   // encode: packed bytes the chunk may produce
+  uint64_t maxw;      // encode: largest segment, words
 };
-}  // namespace
 
-extern "C" {
+// encode: chunks of about `target` bytes of segment words
+std::vector<MsgChunk> enc_msg_chunks(const uint64_t *swo, const uint64_t *mso, uint32_t nm, uint64_t target) {
+  std::vector<MsgChunk> cs;
+  uint32_t m = 0;
+  while (m < nm) {
+    MsgChunk c{m, m, mso[m], mso[m], 0, 0, 16, 1};
+    while (c.m1 < nm) {
+      const uint64_t a = mso[c.m1], b = mso[c.m1 + 1];
+      const uint64_t bytes = 8 * (swo[b] - swo[a]);
+      if (c.m1 > c.m0 && c.in_len + bytes > target) break;
+      c.in_len += bytes;
+      for (uint64_t i = a; i < b; ++i) {
+        const uint64_t w = swo[i + 1] - swo[i];
+        c.out_cap += cpk_packed_bound(w);
+        c.maxw = w > c.maxw ? w : c.maxw;
+      }
+      c.out_cap += 10 * ((b - a + 2) / 2 + 1);
+      ++c.m1;
+    }
+    c.s1 = mso[c.m1];
+    c.in0 = 8 * (swo[c.s0] - swo[0]);
+    cs.push_back(c);
+    m = c.m1;
+  }
+  return cs;
+}
 
-}  // extern "C"
-
-namespace {
-
-// cpk_encode_messages_host(_gather): `fill(d_in, words)` puts the segments'
-// words, back to back, into device memory
+// cpk_encode_messages_host(_gather): `fill(pin, c)` puts chunk c's segment
+// words, back to back, into the pinned input slot
 template <class Fill>
 int encode_messages_host_impl(cpk_ctx ctx, Fill fill, const uint64_t *h_swo, uint32_t nseg,
                               const uint64_t *h_msg_seg_off, uint32_t nm, void *h_out,
@@ -458,39 +475,99 @@ int encode_messages_host_impl(cpk_ctx ctx, Fill fill, const uint64_t *h_swo, uin
   if (h_msg_seg_off[0] != 0 || h_msg_seg_off[nm] != nseg) return CPK_EINVAL;
   for (uint32_t m = 0; m < nm; ++m)
     if (h_msg_seg_off[m + 1] < h_msg_seg_off[m]) return CPK_EINVAL;
-  uint64_t maxw = 1, cap = 16;
-  for (uint32_t i = 0; i < nseg; ++i) {
+  for (uint32_t i = 0; i < nseg; ++i)
     if (h_swo[i + 1] < h_swo[i]) return CPK_EINVAL;
-    const uint64_t w = h_swo[i + 1] - h_swo[i];
-    maxw = w > maxw ? w : maxw;
-    cap += cpk_packed_bound(w);
-  }
-  for (uint32_t m = 0; m < nm; ++m) cap += 10 * ((h_msg_seg_off[m + 1] - h_msg_seg_off[m] + 2) / 2 + 1);
   if (nm == 0) {
     h_out_off[0] = 0;
     return CPK_OK;
   }
   DeviceGuard g(ctx->device);
-  const uint64_t words = h_swo[nseg] - h_swo[0];
-  std::vector<uint64_t> rel(nseg + 1);
-  for (uint32_t i = 0; i <= nseg; ++i) rel[i] = h_swo[i] - h_swo[0];
-  DevBufs b;
-  void *d_in = b.get(words * 8 + 8), *d_out = b.get((cap + 15) & ~15ull);
-  uint64_t *d_swo = (uint64_t *)b.get((nseg + 1) * 8ull), *d_ms = (uint64_t *)b.get((nm + 1) * 8ull);
-  uint64_t *d_off = (uint64_t *)b.get(((uint64_t)nm + nseg + 1) * 8);
-  if (!d_in || !d_out || !d_swo || !d_ms || !d_off) return CPK_ENOMEM;
-  if ((words && fill(d_in, words)) ||
-      hipMemcpy(d_swo, rel.data(), (nseg + 1) * 8ull, hipMemcpyHostToDevice) ||
-      hipMemcpy(d_ms, h_msg_seg_off, (nm + 1) * 8ull, hipMemcpyHostToDevice))
-    return CPK_EDEVICE;
-  int rc = cpk_encode_messages(ctx, d_in, d_swo, nseg, d_ms, nm, maxw, d_out, d_off, nullptr);
+  const std::vector<MsgChunk> cs = enc_msg_chunks(h_swo, h_msg_seg_off, nm, host_chunk_bytes());
+  uint64_t mi = 0, mo = 0, mm = 0;
+  for (const MsgChunk &c : cs) {
+    const uint64_t ns = c.s1 - c.s0, nmk = c.m1 - c.m0;
+    mi = c.in_len > mi ? c.in_len : mi;
+    mo = c.out_cap > mo ? c.out_cap : mo;
+    // meta: swo [ns + 1] | msg_seg_off [nm + 1] | out_off [nm + ns + 1]
+    const uint64_t need = (ns + 1) + (nmk + 1) + (nmk + ns + 1);
+    mm = need > mm ? need : mm;
+  }
+  HostPipe *p = nullptr;
+  int rc = pipe_get(ctx, mi, mo, mm, &p);
   if (rc) return rc;
-  if ((rc = cpk_ctx_take_error(ctx, nullptr))) return rc;
-  if (hipMemcpy(h_out_off, d_off, ((uint64_t)nm + nseg + 1) * 8, hipMemcpyDeviceToHost))
-    return CPK_EDEVICE;
-  const uint64_t P = h_out_off[(uint64_t)nm + nseg];
-  if (P > h_out_cap) return CPK_ENOMEM;
-  return hip_ok(hipMemcpy(h_out, d_out, P, hipMemcpyDeviceToHost));
+  uint8_t *dst = (uint8_t *)h_out;
+  uint64_t base = 0;
+  const size_t K = cs.size();
+  for (size_t k = 0; k <= K + 1 && rc == CPK_OK; ++k) {
+    if (k < K) {  // copy-in, H2D, kernels of chunk k
+      const MsgChunk &c = cs[k];
+      HostSlot &s = p->slot[k & 1];
+      const uint32_t ns = (uint32_t)(c.s1 - c.s0), nmk = c.m1 - c.m0;
+      fill((uint8_t *)s.pin_in, c);
+      uint64_t *m = s.pin_meta;
+      for (uint32_t j = 0; j <= ns; ++j) m[j] = h_swo[c.s0 + j] - h_swo[c.s0];
+      for (uint32_t j = 0; j <= nmk; ++j) m[ns + 1 + j] = h_msg_seg_off[c.m0 + j] - c.s0;
+      uint64_t *dm = s.d_meta, *doff = dm + (ns + 1) + (nmk + 1);
+      if ((c.in_len && hipMemcpyAsync(s.d_in, s.pin_in, c.in_len, hipMemcpyHostToDevice, p->sh)) ||
+          hipMemcpyAsync(dm, m, ((ns + 1) + (nmk + 1)) * 8ull, hipMemcpyHostToDevice, p->sh) ||
+          hipEventRecord(s.eh, p->sh) || hipStreamWaitEvent(p->sk, s.eh, 0) ||
+          (k >= 2 && hipStreamWaitEvent(p->sk, s.ed, 0))) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      rc = cpk_encode_messages(ctx, s.d_in, dm, ns, dm + ns + 1, nmk, c.maxw, s.d_out, doff, p->sk);
+      if (rc) break;
+      if (hipMemcpyAsync(m + (ns + 1) + (nmk + 1), doff, ((uint64_t)nmk + ns + 1) * 8, hipMemcpyDeviceToHost,
+                         p->sk) ||
+          hipEventRecord(s.ek, p->sk)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+    }
+    if (k >= 1 && k - 1 < K) {  // chunk k-1: offsets, then its D2H
+      const MsgChunk &c = cs[k - 1];
+      HostSlot &s = p->slot[(k - 1) & 1];
+      const uint32_t ns = (uint32_t)(c.s1 - c.s0), nmk = c.m1 - c.m0;
+      if (hipEventSynchronize(s.ek)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      const uint64_t *off = s.pin_meta + (ns + 1) + (nmk + 1);
+      const uint64_t np = (uint64_t)nmk + ns, P = off[np];
+      if (P > c.out_cap) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      if (base + P > h_out_cap) {
+        rc = CPK_ENOMEM;
+        break;
+      }
+      // pieces in message order: chunk k-1's start at piece c.m0 + c.s0
+      for (uint64_t j = 0; j <= np; ++j) h_out_off[c.m0 + c.s0 + j] = base + off[j];
+      if ((P && hipMemcpyAsync(s.pin_out, s.d_out, P, hipMemcpyDeviceToHost, p->sd)) ||
+          hipEventRecord(s.ed, p->sd)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      base += P;
+    }
+    if (k >= 2) {  // chunk k-2: copy-out
+      const MsgChunk &c = cs[k - 2];
+      HostSlot &s = p->slot[k & 1];
+      if (hipEventSynchronize(s.ed)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      const uint64_t np = (uint64_t)(c.m1 - c.m0) + (c.s1 - c.s0);
+      const uint64_t o0 = h_out_off[c.m0 + c.s0], o1 = h_out_off[c.m0 + c.s0 + np];
+      par_copy(dst + o0, s.pin_out, o1 - o0);
+    }
+  }
+  if (rc) {
+    pipe_drain(p);
+    return rc;
+  }
+  return cpk_ctx_take_error(ctx, p->sk);
 }
 
 }  // namespace
@@ -500,36 +577,32 @@ extern "C" {
 int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32_t nseg,
                              const uint64_t *h_msg_seg_off, uint32_t nm, void *h_out,
                              uint64_t h_out_cap, uint64_t *h_out_off) {
-  if (!h_swo) return CPK_EINVAL;
+  if (!h_swo || (nseg && h_swo[nseg] > h_swo[0] && !h_in) || (nm && !h_out)) return CPK_EINVAL;
   const uint8_t *src = (const uint8_t *)h_in + 8 * h_swo[0];
   return encode_messages_host_impl(
-      ctx,
-      [&](void *d_in, uint64_t words) {
-        return hipMemcpy(d_in, src, words * 8, hipMemcpyHostToDevice) != hipSuccess;
-      },
-      h_swo, nseg, h_msg_seg_off, nm, h_out, h_out_cap, h_out_off);
+      ctx, [&](uint8_t *pin, const MsgChunk &c) { par_copy(pin, src + c.in0, c.in_len); }, h_swo, nseg,
+      h_msg_seg_off, nm, h_out, h_out_cap, h_out_off);
 }
 
 int cpk_encode_messages_host_gather(cpk_ctx ctx, const void *const *h_segs, const uint64_t *h_swo,
                                     uint32_t nseg, const uint64_t *h_msg_seg_off, uint32_t nm,
                                     void *h_out, uint64_t h_out_cap, uint64_t *h_out_off) {
-  if (!h_swo || (nseg && !h_segs)) return CPK_EINVAL;
+  if (!h_swo || (nseg && !h_segs) || (nm && !h_out)) return CPK_EINVAL;
   for (uint32_t i = 0; i < nseg; ++i)
     if (h_swo[i + 1] > h_swo[i] && !h_segs[i]) return CPK_EINVAL;
   return encode_messages_host_impl(
       ctx,
-      [&](void *d_in, uint64_t words) {
-        // segments gathered by host threads into pinned memory, one DMA
-        void *pin = nullptr;
-        if (hipHostMalloc(&pin, words * 8, hipHostMallocDefault) != hipSuccess) return true;
-        gather_copy((uint8_t *)pin, h_segs, h_swo, 0, nseg);
-        const bool bad = hipMemcpy(d_in, pin, words * 8, hipMemcpyHostToDevice) != hipSuccess;
-        hipHostFree(pin);
-        return bad;
+      [&](uint8_t *pin, const MsgChunk &c) {
+        gather_copy(pin, h_segs, h_swo, (uint32_t)c.s0, (uint32_t)c.s1);
       },
       h_swo, nseg, h_msg_seg_off, nm, h_out, h_out_cap, h_out_off);
 }
 
+// Decode: chunks of whole messages by packed bytes.  A chunk's table pass
+// gives its words and segments; the chunk is then decoded straight into the
+// caller's arrays at the running totals.  When the caller's capacities are
+// too small (or zero: the sizing call) the remaining chunks only run their
+// table passes, and the totals are returned with CPK_ENOMEM.
 int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_msg_off, uint32_t nm,
                              uint64_t traversal_limit_words, void *h_out, uint64_t out_cap_words,
                              uint64_t *h_seg_word_off, uint32_t seg_cap, uint64_t *h_msg_seg_off,
@@ -542,41 +615,110 @@ int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *
   }
   for (uint32_t m = 0; m < nm; ++m)
     if (h_msg_off[m + 1] < h_msg_off[m]) return CPK_EINVAL;
+  if (!h_packed && h_msg_off[nm] > h_msg_off[0]) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
-  const uint64_t P = h_msg_off[nm] - h_msg_off[0];
-  std::vector<uint64_t> rel(nm + 1);
-  for (uint32_t m = 0; m <= nm; ++m) rel[m] = h_msg_off[m] - h_msg_off[0];
-  DevBufs b;
-  void *d_pk = b.get(P + 64);
-  uint64_t *d_mo = (uint64_t *)b.get((nm + 1) * 8ull), *d_ms = (uint64_t *)b.get((nm + 1) * 8ull);
-  int32_t *d_mst = (int32_t *)b.get(nm * 4ull);
-  if (!d_pk || !d_mo || !d_ms || !d_mst) return CPK_ENOMEM;
-  if (hipMemset(d_pk, 0, P + 64) ||
-      (P && hipMemcpy(d_pk, (const uint8_t *)h_packed + h_msg_off[0], P, hipMemcpyHostToDevice)) ||
-      hipMemcpy(d_mo, rel.data(), (nm + 1) * 8ull, hipMemcpyHostToDevice))
-    return CPK_EDEVICE;
-  // the totals first (the table pass), then the decode into buffers of that size
-  int rc = cpk_decode_messages(ctx, d_pk, d_mo, nm, traversal_limit_words, nullptr, 0, nullptr,
-                               nullptr, nullptr, 0, d_ms, d_mst, h_totals, nullptr);
-  if (rc != CPK_OK && rc != CPK_ENOMEM) return rc;
-  if (h_totals[0] > out_cap_words || h_totals[1] > seg_cap) return CPK_ENOMEM;
-  if (h_totals[1] && (!h_out || !h_seg_word_off)) return CPK_EINVAL;
-  const uint64_t W = h_totals[0], S = h_totals[1];
-  void *d_out = b.get(W * 8 + 8);
-  uint64_t *d_sw = (uint64_t *)b.get((S + 1) * 8), *d_si = (uint64_t *)b.get((S + 1) * 8);
-  int32_t *d_ss = (int32_t *)b.get(S * 4 + 4);
-  if (!d_out || !d_sw || !d_si || !d_ss) return CPK_ENOMEM;
-  rc = cpk_decode_messages(ctx, d_pk, d_mo, nm, traversal_limit_words, d_out, W, d_sw, d_si, d_ss,
-                           (uint32_t)S, d_ms, d_mst, h_totals, nullptr);
+  // chunks of whole messages, about `target` packed bytes each
+  const uint64_t target = host_chunk_bytes() / 2;
+  std::vector<MsgChunk> cs;
+  for (uint32_t m = 0; m < nm;) {
+    MsgChunk c{m, m, 0, 0, h_msg_off[m], 0, 0, 0};
+    while (c.m1 < nm && (c.m1 == c.m0 || h_msg_off[c.m1 + 1] - c.in0 <= target)) ++c.m1;
+    c.in_len = h_msg_off[c.m1] - c.in0;
+    cs.push_back(c);
+    m = c.m1;
+  }
+  uint64_t mi = 0, mmsg = 0;
+  for (const MsgChunk &c : cs) {
+    mi = c.in_len > mi ? c.in_len : mi;
+    mmsg = (uint64_t)(c.m1 - c.m0) > mmsg ? c.m1 - c.m0 : mmsg;
+  }
+  // meta: msg_off [n + 1] | msg_seg_off [n + 1] | msg_status [n] (as u32 pairs)
+  //       | seg_word_off [S + 1] | seg_in_off [S + 1] | seg_status [S]
+  auto meta_need = [](uint64_t nmk, uint64_t S) { return 2 * (nmk + 1) + (nmk + 1) / 2 + 2 * (S + 1) + S / 2 + 1; };
+  HostPipe *p = nullptr;
+  int rc = pipe_get(ctx, mi, 64, meta_need(mmsg, 0), &p);
   if (rc) return rc;
-  if (hipDeviceSynchronize() || hipMemcpy(h_msg_seg_off, d_ms, (nm + 1) * 8ull, hipMemcpyDeviceToHost) ||
-      hipMemcpy(h_msg_status, d_mst, nm * 4ull, hipMemcpyDeviceToHost) ||
-      (h_seg_word_off && hipMemcpy(h_seg_word_off, d_sw, (S + 1) * 8, hipMemcpyDeviceToHost)) ||
-      (W && hipMemcpy(h_out, d_out, W * 8, hipMemcpyDeviceToHost)))
-    return CPK_EDEVICE;
-  for (uint32_t m = 0; m < nm; ++m)
-    if (h_msg_status[m] != CPK_OK) return h_msg_status[m];
-  return CPK_OK;
+  const uint8_t *src = (const uint8_t *)h_packed;
+  uint64_t W = 0, S = 0;  // running totals
+  bool sizing = false;     // capacities exceeded: table passes only
+  int first_bad = CPK_OK;
+  for (size_t k = 0; k < cs.size() && rc == CPK_OK; ++k) {
+    const MsgChunk &c = cs[k];
+    const uint32_t nmk = c.m1 - c.m0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      HostSlot &s = p->slot[k & 1];
+      par_copy(s.pin_in, src + c.in0, c.in_len);
+      memset((uint8_t *)s.pin_in + c.in_len, 0, 64);  // (the decoder reads whole 16-byte lines)
+      uint64_t *m = s.pin_meta, *dm = s.d_meta;
+      for (uint32_t j = 0; j <= nmk; ++j) m[j] = h_msg_off[c.m0 + j] - c.in0;
+      uint64_t *d_ms = dm + (nmk + 1);
+      int32_t *d_mst = (int32_t *)(d_ms + (nmk + 1));
+      uint64_t *d_sw = dm + 2 * (nmk + 1) + (nmk + 1) / 2;
+      uint64_t tot[2] = {0, 0};
+      if (hipMemcpyAsync(s.d_in, s.pin_in, c.in_len + 64, hipMemcpyHostToDevice, p->sk) ||
+          hipMemcpyAsync(dm, m, (nmk + 1) * 8ull, hipMemcpyHostToDevice, p->sk)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      // the table pass (synchronises the stream for the chunk's totals)
+      rc = cpk_decode_messages(ctx, s.d_in, dm, nmk, traversal_limit_words, nullptr, 0, nullptr, nullptr, nullptr,
+                               0, d_ms, d_mst, tot, p->sk);
+      if (rc == CPK_ENOMEM) rc = CPK_OK;
+      if (rc) break;
+      if (!sizing && (W + tot[0] > out_cap_words || S + tot[1] > seg_cap || (tot[1] && (!h_out || !h_seg_word_off))))
+        sizing = true;
+      if (sizing) {
+        W += tot[0];
+        S += tot[1];
+        break;
+      }
+      // room in the slot for the chunk's words and segments?
+      if (tot[0] * 8 + 64 > p->cap_out || meta_need(nmk, tot[1]) > p->cap_meta) {
+        if (attempt) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+        pipe_drain(p);
+        rc = pipe_get(ctx, mi, tot[0] * 8, meta_need(mmsg, tot[1]), &p);
+        continue;  // (buffers replaced: stage the chunk again)
+      }
+      uint64_t *d_si = d_sw + (tot[1] + 1);
+      int32_t *d_ss = (int32_t *)(d_si + (tot[1] + 1));
+      rc = cpk_decode_messages(ctx, s.d_in, dm, nmk, traversal_limit_words, s.d_out, tot[0], d_sw, d_si, d_ss,
+                               (uint32_t)tot[1], d_ms, d_mst, tot, p->sk);
+      if (rc) break;
+      uint64_t *hm = m + (nmk + 1);  // msg_seg_off | msg_status | seg_word_off
+      if (hipMemcpyAsync(hm, d_ms, ((nmk + 1) + (nmk + 1) / 2 + (tot[1] + 1)) * 8ull, hipMemcpyDeviceToHost,
+                         p->sk) ||
+          (tot[0] && hipMemcpyAsync(s.pin_out, s.d_out, tot[0] * 8, hipMemcpyDeviceToHost, p->sk)) ||
+          hipStreamSynchronize(p->sk)) {
+        rc = CPK_EDEVICE;
+        break;
+      }
+      const uint64_t *ms = hm;
+      const int32_t *mst = (const int32_t *)(hm + (nmk + 1));
+      const uint64_t *sw = hm + (nmk + 1) + (nmk + 1) / 2;
+      for (uint32_t j = 0; j < nmk; ++j) {
+        h_msg_seg_off[c.m0 + j] = S + ms[j];
+        h_msg_status[c.m0 + j] = mst[j];
+        if (mst[j] != CPK_OK && first_bad == CPK_OK) first_bad = mst[j];
+      }
+      for (uint64_t j = 0; j <= tot[1]; ++j) h_seg_word_off[S + j] = W + sw[j];
+      if (tot[0]) par_copy((uint8_t *)h_out + 8 * W, s.pin_out, tot[0] * 8);
+      W += tot[0];
+      S += tot[1];
+      break;
+    }
+  }
+  if (rc) {
+    pipe_drain(p);
+    return rc;
+  }
+  h_msg_seg_off[nm] = S;
+  h_totals[0] = W;
+  h_totals[1] = S;
+  if (sizing) return CPK_ENOMEM;
+  return first_bad;
 }
 
 }  // extern "C"

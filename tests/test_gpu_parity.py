@@ -556,10 +556,14 @@ def test_encode_messages_matches_serialize_write(ctx, oracle):
     assert got == b"".join(s for m, g in zip(msgs, ok) if g for s in m)
 
 
-def test_message_host_forms(ctx, oracle):
+@pytest.mark.parametrize("chunk_kb", [None, "4", "64"])
+def test_message_host_forms(ctx, oracle, chunk_kb, monkeypatch):
     """cpk_encode_messages_host / cpk_decode_messages_host: the JNI facade's
-    SerializePacked batch path, against the oracle's Serialize.write/read."""
-    import capnp_packed as cp
+    SerializePacked batch path, against the oracle's Serialize.write/read;
+    whole messages flow through the pinned slots in chunks (small chunks:
+    many chunks, slot growth mid-batch)."""
+    if chunk_kb:
+        monkeypatch.setenv("CPK_HOST_CHUNK_KB", chunk_kb)
     rng = np.random.default_rng(43)
     msgs = [[_random_words(rng, int(rng.choice([0, 1, 9, 500, 4000])), [.4, .3, .2, .1]).tobytes()
              for _ in range(int(rng.integers(1, 6)))] for _ in range(60)]
