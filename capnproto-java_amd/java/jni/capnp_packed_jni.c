@@ -7,9 +7,12 @@
  *      -I../../../include capnp_packed_jni.c \
  *      -L../../lib -lcapnp_packed_hip -Wl,-rpath,'$ORIGIN' -o libcapnp_packed_jni.so
  *
- * Buffers: direct ByteBuffers are passed zero-copy (GetDirectBufferAddress;
- * DIRECT allocation exists in the reference, DefaultAllocator.java:56-62);
- * heap buffers are pinned with Get/ReleasePrimitiveArrayCritical.  Status
+ * Buffers: every ByteBuffer argument must be direct and is passed zero-copy
+ * (GetDirectBufferAddress; DIRECT allocation exists in the reference,
+ * DefaultAllocator.java:56-62); a heap buffer is rejected with CPK_EINVAL --
+ * PackedGpu.java copies heap buffers into direct ones before calling in.
+ * Array lengths, positions and buffer capacities are checked here before the
+ * library sees a pointer.  Status
  * codes become the reference's exceptions: decode errors ->
  * org.capnproto.DecodeException (DecodeException.java:24-27), device / memory
  * errors -> java.io.IOException.
@@ -28,6 +31,21 @@ static void throw_status(JNIEnv *env, int st) {
                         : "java/io/IOException";
   jclass c = (*env)->FindClass(env, cls);
   if (c) (*env)->ThrowNew(env, c, cpk_status_string(st));
+}
+
+/* an offset array of n + 1 entries needs length >= 1 */
+static int offsets_ok(JNIEnv *env, jlongArray a) { return a && (*env)->GetArrayLength(env, a) >= 1; }
+
+/* piece i of a gather: buffer b from pos for `bytes` bytes, inside its capacity */
+static const void *gather_ptr(JNIEnv *env, jobject b, jint pos, uint64_t bytes, int *st) {
+  uint8_t *a = b ? (uint8_t *)(*env)->GetDirectBufferAddress(env, b) : NULL;
+  jlong cap = b ? (*env)->GetDirectBufferCapacity(env, b) : -1;
+  if (bytes == 0) return a ? a + (pos > 0 ? pos : 0) : NULL;  /* (an empty piece needs no buffer) */
+  if (!a || pos < 0 || cap < 0 || (uint64_t)cap < (uint64_t)pos || (uint64_t)cap - (uint64_t)pos < bytes) {
+    *st = CPK_EINVAL;
+    return NULL;
+  }
+  return a + pos;
 }
 
 /* long PackedGpu.nativeCreate(int device) */
@@ -53,6 +71,10 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDestroy(JNIEnv *en
 JNIEXPORT jlong JNICALL Java_org_capnproto_gpu_PackedGpu_nativeCapacity(JNIEnv *env, jclass k,
                                                                         jlongArray segWordOff) {
   (void)k;
+  if (!offsets_ok(env, segWordOff)) {
+    throw_status(env, CPK_EINVAL);
+    return 0;
+  }
   jsize n1 = (*env)->GetArrayLength(env, segWordOff);
   jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
   uint64_t cap = cpk_batch_packed_capacity((const uint64_t *)swo, (uint32_t)(n1 - 1));
@@ -71,12 +93,18 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncode(
   void *pin = (*env)->GetDirectBufferAddress(env, in);
   void *pout = (*env)->GetDirectBufferAddress(env, out);
   jlong cap = (*env)->GetDirectBufferCapacity(env, out);
-  if (!pin || !pout) {
+  if (!pin || !pout || !offsets_ok(env, segWordOff) || !outOff ||
+      (*env)->GetArrayLength(env, outOff) < (*env)->GetArrayLength(env, segWordOff)) {
     throw_status(env, CPK_EINVAL);
     return;
   }
   jsize n1 = (*env)->GetArrayLength(env, segWordOff);
   jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
+  if ((uint64_t)(*env)->GetDirectBufferCapacity(env, in) < 8 * (uint64_t)swo[n1 - 1]) {
+    (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
+    throw_status(env, CPK_EINVAL);
+    return;
+  }
   jlong *off = (*env)->GetLongArrayElements(env, outOff, NULL);
   int st = cpk_encode_host((cpk_ctx)(intptr_t)h, pin, (const uint64_t *)swo, (uint32_t)(n1 - 1),
                            pout, (uint64_t)cap, (uint64_t *)off);
@@ -94,13 +122,21 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDecode(
   (void)k;
   void *ppk = (*env)->GetDirectBufferAddress(env, packed);
   void *pout = (*env)->GetDirectBufferAddress(env, out);
-  if (!ppk || !pout) {
+  if (!ppk || !pout || !offsets_ok(env, segWordOff) || !inOff ||
+      (*env)->GetArrayLength(env, inOff) != (*env)->GetArrayLength(env, segWordOff)) {
     throw_status(env, CPK_EINVAL);
     return;
   }
   jsize n1 = (*env)->GetArrayLength(env, segWordOff);
   jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
   jlong *io = (*env)->GetLongArrayElements(env, inOff, NULL);
+  if ((uint64_t)(*env)->GetDirectBufferCapacity(env, packed) < (uint64_t)io[n1 - 1] ||
+      (uint64_t)(*env)->GetDirectBufferCapacity(env, out) < 8 * (uint64_t)swo[n1 - 1]) {
+    (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
+    (*env)->ReleaseLongArrayElements(env, inOff, io, JNI_ABORT);
+    throw_status(env, CPK_EINVAL);
+    return;
+  }
   int32_t *status = (int32_t *)calloc((size_t)(n1 > 1 ? n1 - 1 : 1), sizeof(int32_t));
   int st = cpk_decode_host((cpk_ctx)(intptr_t)h, ppk, (const uint64_t *)io,
                            (const uint64_t *)swo, (uint32_t)(n1 - 1), pout, status);
@@ -121,7 +157,9 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeMessages(
   void *pin = (*env)->GetDirectBufferAddress(env, in);
   void *pout = (*env)->GetDirectBufferAddress(env, out);
   jlong cap = (*env)->GetDirectBufferCapacity(env, out);
-  if (!pin || !pout) {
+  if (!pin || !pout || !offsets_ok(env, segWordOff) || !offsets_ok(env, msgSegOff) || !outOff ||
+      (*env)->GetArrayLength(env, outOff) <
+          (*env)->GetArrayLength(env, segWordOff) + (*env)->GetArrayLength(env, msgSegOff) - 1) {
     throw_status(env, CPK_EINVAL);
     return;
   }
@@ -129,6 +167,12 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeMessages(
   jsize nm1 = (*env)->GetArrayLength(env, msgSegOff);
   jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
   jlong *mso = (*env)->GetLongArrayElements(env, msgSegOff, NULL);
+  if ((uint64_t)(*env)->GetDirectBufferCapacity(env, in) < 8 * (uint64_t)swo[ns1 - 1]) {
+    (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
+    (*env)->ReleaseLongArrayElements(env, msgSegOff, mso, JNI_ABORT);
+    throw_status(env, CPK_EINVAL);
+    return;
+  }
   jlong *off = (*env)->GetLongArrayElements(env, outOff, NULL);
   int st = cpk_encode_messages_host((cpk_ctx)(intptr_t)h, pin, (const uint64_t *)swo,
                                     (uint32_t)(ns1 - 1), (const uint64_t *)mso, (uint32_t)(nm1 - 1),
@@ -151,13 +195,20 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDecodeMessages(
   void *ppk = (*env)->GetDirectBufferAddress(env, packed);
   void *pout = out ? (*env)->GetDirectBufferAddress(env, out) : NULL;
   jlong ocap = out ? (*env)->GetDirectBufferCapacity(env, out) : 0;
-  if (!ppk || (out && !pout)) {
+  if (!ppk || (out && !pout) || !offsets_ok(env, msgOff) || !msgSegOff || !totals ||
+      (*env)->GetArrayLength(env, msgSegOff) < (*env)->GetArrayLength(env, msgOff) ||
+      (*env)->GetArrayLength(env, totals) < 2) {
     throw_status(env, CPK_EINVAL);
     return;
   }
   jsize nm1 = (*env)->GetArrayLength(env, msgOff);
   jsize sw1 = segWordOff ? (*env)->GetArrayLength(env, segWordOff) : 0;
   jlong *mo = (*env)->GetLongArrayElements(env, msgOff, NULL);
+  if ((uint64_t)(*env)->GetDirectBufferCapacity(env, packed) < (uint64_t)mo[nm1 - 1]) {
+    (*env)->ReleaseLongArrayElements(env, msgOff, mo, JNI_ABORT);
+    throw_status(env, CPK_EINVAL);
+    return;
+  }
   jlong *ms = (*env)->GetLongArrayElements(env, msgSegOff, NULL);
   jlong *sw = segWordOff ? (*env)->GetLongArrayElements(env, segWordOff, NULL) : NULL;
   jlong *tot = (*env)->GetLongArrayElements(env, totals, NULL);
@@ -188,13 +239,19 @@ JNIEXPORT jlong JNICALL Java_org_capnproto_gpu_PackedGpu_nativeDecodeStream(
   (void)k;
   uint8_t *ppk = (uint8_t *)(*env)->GetDirectBufferAddress(env, packed);
   void *pout = (*env)->GetDirectBufferAddress(env, out);
-  if (!ppk || !pout || position < 0 || limit < position) {
+  if (!ppk || !pout || position < 0 || limit < position || !offsets_ok(env, segWordOff) ||
+      (*env)->GetDirectBufferCapacity(env, packed) < limit) {
     throw_status(env, CPK_EINVAL);
     return 0;
   }
   jsize n1 = (*env)->GetArrayLength(env, segWordOff);
-  uint32_t n = (uint32_t)(n1 > 1 ? n1 - 1 : 0);
+  uint32_t n = (uint32_t)(n1 - 1);
   jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
+  if ((uint64_t)(*env)->GetDirectBufferCapacity(env, out) < 8 * (uint64_t)swo[n]) {
+    (*env)->ReleaseLongArrayElements(env, segWordOff, swo, JNI_ABORT);
+    throw_status(env, CPK_EINVAL);
+    return 0;
+  }
   uint64_t *in_off = (uint64_t *)calloc((size_t)n + 1, sizeof(uint64_t));
   int32_t *status = (int32_t *)calloc((size_t)(n ? n : 1), sizeof(int32_t));
   int st = (in_off && status)
@@ -222,8 +279,10 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeGather(
   (void)k;
   void *pout = (*env)->GetDirectBufferAddress(env, out);
   jlong cap = (*env)->GetDirectBufferCapacity(env, out);
-  jsize n = (*env)->GetArrayLength(env, pieces);
-  if (!pout || (*env)->GetArrayLength(env, segWordOff) != n + 1) {
+  jsize n = pieces ? (*env)->GetArrayLength(env, pieces) : -1;
+  if (!pout || n < 0 || !positions || (*env)->GetArrayLength(env, positions) != n || !segWordOff ||
+      (*env)->GetArrayLength(env, segWordOff) != n + 1 || !outOff ||
+      (*env)->GetArrayLength(env, outOff) < n + 1) {
     throw_status(env, CPK_EINVAL);
     return;
   }
@@ -232,17 +291,19 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeGather(
     throw_status(env, CPK_ENOMEM);
     return;
   }
+  jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
   jint *pos = (*env)->GetIntArrayElements(env, positions, NULL);
   int st = CPK_OK;
   for (jsize i = 0; i < n && st == CPK_OK; ++i) {
+    if (swo[i + 1] < swo[i]) {
+      st = CPK_EINVAL;
+      break;
+    }
     jobject b = (*env)->GetObjectArrayElement(env, pieces, i);
-    uint8_t *a = (uint8_t *)(*env)->GetDirectBufferAddress(env, b);
-    if (!a) st = CPK_EINVAL;
-    else ptrs[i] = a + pos[i];
-    (*env)->DeleteLocalRef(env, b);
+    ptrs[i] = gather_ptr(env, b, pos[i], 8 * (uint64_t)(swo[i + 1] - swo[i]), &st);
+    if (b) (*env)->DeleteLocalRef(env, b);
   }
   (*env)->ReleaseIntArrayElements(env, positions, pos, JNI_ABORT);
-  jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
   jlong *off = (*env)->GetLongArrayElements(env, outOff, NULL);
   if (st == CPK_OK)
     st = cpk_encode_host_gather((cpk_ctx)(intptr_t)h, ptrs, (const uint64_t *)swo, (uint32_t)n,
@@ -264,8 +325,10 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeMessagesGath
   (void)k;
   void *pout = (*env)->GetDirectBufferAddress(env, out);
   jlong cap = (*env)->GetDirectBufferCapacity(env, out);
-  jsize ns = (*env)->GetArrayLength(env, segs);
-  if (!pout || (*env)->GetArrayLength(env, segWordOff) != ns + 1) {
+  jsize ns = segs ? (*env)->GetArrayLength(env, segs) : -1;
+  if (!pout || ns < 0 || !positions || (*env)->GetArrayLength(env, positions) != ns || !segWordOff ||
+      (*env)->GetArrayLength(env, segWordOff) != ns + 1 || !offsets_ok(env, msgSegOff) || !outOff ||
+      (*env)->GetArrayLength(env, outOff) < ns + (*env)->GetArrayLength(env, msgSegOff)) {
     throw_status(env, CPK_EINVAL);
     return;
   }
@@ -274,18 +337,20 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeMessagesGath
     throw_status(env, CPK_ENOMEM);
     return;
   }
+  jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
   jint *pos = (*env)->GetIntArrayElements(env, positions, NULL);
   int st = CPK_OK;
   for (jsize i = 0; i < ns && st == CPK_OK; ++i) {
+    if (swo[i + 1] < swo[i]) {
+      st = CPK_EINVAL;
+      break;
+    }
     jobject b = (*env)->GetObjectArrayElement(env, segs, i);
-    uint8_t *a = (uint8_t *)(*env)->GetDirectBufferAddress(env, b);
-    if (!a) st = CPK_EINVAL;
-    else ptrs[i] = a + pos[i];
-    (*env)->DeleteLocalRef(env, b);
+    ptrs[i] = gather_ptr(env, b, pos[i], 8 * (uint64_t)(swo[i + 1] - swo[i]), &st);
+    if (b) (*env)->DeleteLocalRef(env, b);
   }
   (*env)->ReleaseIntArrayElements(env, positions, pos, JNI_ABORT);
   jsize nm1 = (*env)->GetArrayLength(env, msgSegOff);
-  jlong *swo = (*env)->GetLongArrayElements(env, segWordOff, NULL);
   jlong *mso = (*env)->GetLongArrayElements(env, msgSegOff, NULL);
   jlong *off = (*env)->GetLongArrayElements(env, outOff, NULL);
   if (st == CPK_OK)

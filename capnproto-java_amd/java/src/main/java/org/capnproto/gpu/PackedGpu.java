@@ -41,6 +41,23 @@ public final class PackedGpu implements AutoCloseable {
 
     private long handle;
 
+    /** A direct buffer of `bytes` bytes: ByteBuffer capacities are ints, so a
+     *  batch whose packed or unpacked size passes 2 GiB - 1 must be split by
+     *  the caller (an IOException here rather than a wrapped (int) cast). */
+    private static ByteBuffer direct(long bytes) throws IOException {
+        if (bytes < 0 || bytes > Integer.MAX_VALUE)
+            throw new IOException("batch of " + bytes + " bytes exceeds one ByteBuffer (2 GiB - 1): split it");
+        return ByteBuffer.allocateDirect((int) bytes).order(ByteOrder.LITTLE_ENDIAN);
+    }
+
+    /** `b`'s remaining bytes in a direct buffer (itself when already direct). */
+    private static ByteBuffer asDirect(ByteBuffer b) throws IOException {
+        if (b.isDirect()) return b;
+        ByteBuffer d = direct(b.remaining());
+        d.put(b.duplicate()).flip();
+        return d;
+    }
+
     public PackedGpu(int device) {
         this.handle = nativeCreate(device);
     }
@@ -74,7 +91,7 @@ public final class PackedGpu implements AutoCloseable {
             words += len / 8;
         }
         swo[n] = words;
-        ByteBuffer out = ByteBuffer.allocateDirect((int) nativeCapacity(swo));
+        ByteBuffer out = direct(nativeCapacity(swo));
         long[] off = new long[n + 1];
         boolean direct = true;
         for (ByteBuffer p : pieces) direct &= p.isDirect();
@@ -83,7 +100,7 @@ public final class PackedGpu implements AutoCloseable {
             for (int i = 0; i < n; ++i) pos[i] = pieces[i].position();
             nativeEncodeGather(handle, pieces, pos, swo, out, off);
         } else {
-            ByteBuffer in = ByteBuffer.allocateDirect((int) (words * 8)).order(ByteOrder.LITTLE_ENDIAN);
+            ByteBuffer in = direct(words * 8);
             for (ByteBuffer p : pieces) in.put(p.duplicate());
             nativeEncode(handle, in, swo, out, off);
         }
@@ -115,7 +132,7 @@ public final class PackedGpu implements AutoCloseable {
         }
         mso[nm] = s;
         swo[nseg] = words;
-        ByteBuffer out = ByteBuffer.allocateDirect((int) (nativeCapacity(swo) + tableCap));
+        ByteBuffer out = direct(nativeCapacity(swo) + tableCap);
         long[] off = new long[nm + nseg + 1];
         ByteBuffer[] flat = new ByteBuffer[nseg];
         boolean direct = true;
@@ -127,7 +144,7 @@ public final class PackedGpu implements AutoCloseable {
             for (int i = 0; i < nseg; ++i) pos[i] = flat[i].position();
             nativeEncodeMessagesGather(handle, flat, pos, swo, mso, out, off);
         } else {
-            ByteBuffer in = ByteBuffer.allocateDirect((int) (words * 8 + 8)).order(ByteOrder.LITTLE_ENDIAN);
+            ByteBuffer in = direct(words * 8 + 8);
             for (ByteBuffer b : flat) in.put(b.duplicate());
             nativeEncodeMessages(handle, in, swo, mso, out, off);
         }
@@ -146,7 +163,7 @@ public final class PackedGpu implements AutoCloseable {
         long[] mso = new long[nm + 1];
         long[] tot = new long[2];
         nativeDecodeMessages(handle, packed, msgOff, traversalLimitInWords, null, null, mso, tot);
-        ByteBuffer out = ByteBuffer.allocateDirect((int) (tot[0] * 8 + 8)).order(ByteOrder.LITTLE_ENDIAN);
+        ByteBuffer out = direct(tot[0] * 8 + 8);
         long[] swo = new long[(int) tot[1] + 1];
         nativeDecodeMessages(handle, packed, msgOff, traversalLimitInWords, out, swo, mso, tot);
         ByteBuffer[][] res = new ByteBuffer[nm][];
@@ -177,9 +194,8 @@ public final class PackedGpu implements AutoCloseable {
             words += len / 8;
         }
         swo[n] = words;
-        ByteBuffer pk = packed.isDirect() ? packed
-                : (ByteBuffer) ByteBuffer.allocateDirect(packed.remaining()).put(packed.duplicate()).flip();
-        ByteBuffer out = ByteBuffer.allocateDirect((int) (words * 8));
+        ByteBuffer pk = asDirect(packed);
+        ByteBuffer out = direct(words * 8);
         nativeDecode(handle, pk, inOff, swo, out);
         for (int i = 0; i < n; ++i) {
             ByteBuffer slice = out.duplicate();
@@ -195,6 +211,14 @@ public final class PackedGpu implements AutoCloseable {
      *  BufferedInputStream does).
      *  @throws org.capnproto.DecodeException on malformed input */
     public void decodeStream(ByteBuffer packed, ByteBuffer[] outs) throws IOException {
+        ByteBuffer pk = asDirect(packed);
+        long used = decodeStreamDirect(pk, pk.position(), outs);
+        packed.position(packed.position() + (int) used);
+    }
+
+    /** decodeStream on a direct buffer from byte `at`; returns the bytes
+     *  consumed (the buffer's position is left alone). */
+    private long decodeStreamDirect(ByteBuffer pk, int at, ByteBuffer[] outs) throws IOException {
         int n = outs.length;
         long[] swo = new long[n + 1];
         long words = 0;
@@ -206,16 +230,14 @@ public final class PackedGpu implements AutoCloseable {
             words += len / 8;
         }
         swo[n] = words;
-        ByteBuffer pk = packed.isDirect() ? packed
-                : (ByteBuffer) ByteBuffer.allocateDirect(packed.remaining()).put(packed.duplicate()).flip();
-        ByteBuffer out = ByteBuffer.allocateDirect((int) (words * 8 + 8));
-        long used = nativeDecodeStream(handle, pk, pk.position(), pk.limit(), swo, out);
-        packed.position(packed.position() + (int) used);
+        ByteBuffer out = direct(words * 8 + 8);
+        long used = nativeDecodeStream(handle, pk, at, pk.limit(), swo, out);
         for (int i = 0; i < n; ++i) {
             ByteBuffer slice = out.duplicate();
             slice.position((int) (swo[i] * 8)).limit((int) (swo[i + 1] * 8));
             outs[i].put(slice);
         }
+        return used;
     }
 
     /** SerializePacked.read of one message from the front of `packed`
@@ -224,8 +246,11 @@ public final class PackedGpu implements AutoCloseable {
      *  decode; the same checks and messages as doRead.  packed.position
      *  advances past the message.  Returns the segments (little-endian). */
     public ByteBuffer[] readMessage(ByteBuffer packed, long traversalLimitInWords) throws IOException {
+        // a heap buffer is copied to direct memory once for the three reads
+        ByteBuffer pk = asDirect(packed);
+        int at = pk.position();
         ByteBuffer first = ByteBuffer.allocate(8).order(ByteOrder.LITTLE_ENDIAN);
-        decodeStream(packed, new ByteBuffer[] {first});
+        at += (int) decodeStreamDirect(pk, at, new ByteBuffer[] {first});
         int rawCount = first.getInt(0);
         if (rawCount < 0 || rawCount > 511)
             throw new org.capnproto.DecodeException("segment count must be between 0 and 512");
@@ -237,7 +262,7 @@ public final class PackedGpu implements AutoCloseable {
         long total = sizes[0];
         if (count > 1) {
             ByteBuffer more = ByteBuffer.allocate(4 * (count & ~1)).order(ByteOrder.LITTLE_ENDIAN);
-            decodeStream(packed, new ByteBuffer[] {more});
+            at += (int) decodeStreamDirect(pk, at, new ByteBuffer[] {more});
             for (int i = 0; i < count - 1; ++i) {
                 sizes[i + 1] = more.getInt(i * 4);
                 if (sizes[i + 1] < 0)
@@ -256,11 +281,9 @@ public final class PackedGpu implements AutoCloseable {
                 throw new org.capnproto.DecodeException("segment has too many words (" + sizes[i] + ")");
             swo[i + 1] = swo[i] + sizes[i];
         }
-        ByteBuffer out = ByteBuffer.allocateDirect((int) (swo[count] * 8 + 8)).order(ByteOrder.LITTLE_ENDIAN);
-        ByteBuffer pk = packed.isDirect() ? packed
-                : (ByteBuffer) ByteBuffer.allocateDirect(packed.remaining()).put(packed.duplicate()).flip();
-        long used = nativeDecodeStream(handle, pk, pk.position(), pk.limit(), swo, out);
-        packed.position(packed.position() + (int) used);
+        ByteBuffer out = direct(swo[count] * 8 + 8);
+        at += (int) nativeDecodeStream(handle, pk, at, pk.limit(), swo, out);
+        packed.position(packed.position() + (at - pk.position()));
         ByteBuffer[] segs = new ByteBuffer[count];
         for (int i = 0; i < count; ++i) {
             ByteBuffer seg = out.duplicate();

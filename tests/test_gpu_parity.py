@@ -413,6 +413,26 @@ def test_encode_host_gather_matches_contiguous(ctx, oracle, chunk_kb, monkeypatc
         assert got[int(goff[i]):int(goff[i + 1])].tobytes() == oracle.pack(parts[i].tobytes())
 
 
+def test_gather_threaded_split_large(ctx, oracle):
+    """Over 8 MiB of ragged pieces (empty ones passed as NULL) under the
+    default chunk size, so the host threads' byte-balanced gather split runs:
+    cpk_encode_host_gather and cpk_encode_messages_host_gather against the
+    oracle byte for byte."""
+    rng = np.random.default_rng(808)
+    sizes = [int(s) for s in rng.integers(0, 30000, size=90)]
+    sizes[::9] = [0] * len(sizes[::9])
+    parts = [oracle.generate(oracle.preset(int(rng.integers(2, 5))), _swo([s])) for s in sizes]
+    assert sum(p.size for p in parts) >= 8 << 20
+    got, goff = ctx.encode_host_gather([p.view(np.uint64) for p in parts])
+    opk, ooff = oracle.pack_batch(np.concatenate(parts), _swo(sizes), threads=8)
+    assert np.array_equal(goff, ooff)
+    assert got.tobytes() == opk.tobytes()
+    # the same segments as 30 messages of 3
+    msgs = [[parts[3 * m + j].tobytes() for j in range(3)] for m in range(30)]
+    pkg, _ = ctx.encode_messages_host_gather(msgs)
+    assert pkg == b"".join(oracle.write_message(m) for m in msgs)
+
+
 def _message_cases(oracle, rng, limit):
     """Packed messages (SerializePacked.write) and broken ones: truncated,
     trailing bytes, flipped table bytes, segment count over 512, negative
