@@ -7,15 +7,25 @@
 //   PackedOutputStream  PackedOutputStream.java:28-213 (write = one piece)
 //   PackedInputStream   PackedInputStream.java:28-148  (read fills the buffer)
 //   SerializePacked     SerializePacked.java:35-134 (write / read a message
-//                       of segments: table piece + one piece per segment)
+//                       of segments: table piece + one piece per segment;
+//                       writeToUnbuffered / readFromUnbuffered over a channel)
+//   FdChannel           java.nio.channels.{Readable,Writable}ByteChannel over a
+//                       file descriptor (socket, pipe, file)
+//   ChannelReader       BufferedInputStreamWrapper.java:28-108's role for the
+//                       GPU path (bytes read ahead of the decoder)
 // Every byte is produced by the GPU kernels; there is no CPU codec here.
 #pragma once
 
+#include <cerrno>
 #include <cstdint>
 #include <cstring>
+#include <optional>
 #include <stdexcept>
 #include <string>
 #include <vector>
+
+#include <poll.h>
+#include <unistd.h>
 
 #include "../../../include/capnp_packed.h"
 
@@ -80,6 +90,111 @@ class ArrayInputStream {
   const uint8_t *buf_;
   size_t len_, pos_ = 0;
 };
+
+// ---- unbuffered channels --------------------------------------------------
+class FdChannel {  // ReadableByteChannel / WritableByteChannel over a descriptor
+ public:
+  explicit FdChannel(int fd) : fd_(fd) {}
+  int fd() const { return fd_; }
+  // WritableByteChannel.write until every byte is out
+  void writeAll(const uint8_t *p, size_t n) {
+    while (n) {
+      const ssize_t k = ::write(fd_, p, n);
+      if (k < 0 && errno == EINTR) continue;
+      if (k <= 0) throw IOException(std::string("channel write: ") + std::strerror(errno));
+      p += k;
+      n -= (size_t)k;
+    }
+  }
+  // one ReadableByteChannel.read: blocks for >= 1 byte; 0 at end of stream
+  size_t readSome(uint8_t *p, size_t cap) {
+    for (;;) {
+      const ssize_t k = ::read(fd_, p, cap);
+      if (k < 0 && errno == EINTR) continue;
+      if (k < 0) throw IOException(std::string("channel read: ") + std::strerror(errno));
+      return (size_t)k;
+    }
+  }
+  // bytes (or the end of the stream) ready within timeout_ms
+  bool ready(int timeout_ms) {
+    pollfd q{fd_, POLLIN, 0};
+    for (;;) {
+      const int r = ::poll(&q, 1, timeout_ms);
+      if (r < 0 && errno == EINTR) continue;
+      return r > 0;
+    }
+  }
+
+ private:
+  int fd_;
+};
+
+// The bytes read from a channel and not yet decoded (the role of
+// BufferedInputStreamWrapper.java:28-108 for the GPU path).  A message's
+// packed length is known only once it is decoded, so reads may run ahead of
+// the message; what they bring in stays here for the next one (the
+// reference's wrapper, made per call, would drop it).
+class ChannelReader {
+ public:
+  explicit ChannelReader(FdChannel ch) : ch_(ch), buf_(1 << 16) {}
+  const uint8_t *data() const { return buf_.data() + pos_; }
+  size_t available() const { return len_ - pos_; }
+  void consume(size_t n) { pos_ += n; }
+  FdChannel &channel() { return ch_; }
+  // one read of what the channel has (blocking for >= 1 byte); false at EOF
+  bool fill() {
+    if (pos_ == len_) pos_ = len_ = 0;
+    if (len_ + 4096 > buf_.size()) {
+      if (pos_ >= buf_.size() / 2) {  // compact
+        std::memmove(buf_.data(), buf_.data() + pos_, len_ - pos_);
+        len_ -= pos_;
+        pos_ = 0;
+      } else {
+        buf_.resize(2 * buf_.size());
+      }
+    }
+    const size_t k = ch_.readSome(buf_.data() + len_, buf_.size() - len_ - 16);
+    len_ += k;
+    std::memset(buf_.data() + len_, 0, 16);
+    return k > 0;
+  }
+
+ private:
+  FdChannel ch_;
+  std::vector<uint8_t> buf_;
+  size_t pos_ = 0, len_ = 0;
+};
+
+// Pieces of `swo` (word offsets) decoded back to back from the channel, as
+// PackedInputStream.read over BufferedInputStreamWrapper would
+// (PackedInputStream.java:35-140): a try on the bytes buffered so far; if
+// they end inside the pieces (CPK_ETRUNC), more are read -- everything the
+// channel has, then, until twice as many as at the last try are buffered,
+// more as they arrive, unless the channel stays idle for a millisecond.  The
+// channel's end inside the pieces is the reference's "premature EOF".
+inline void decodeFromChannel(Gpu &gpu, ChannelReader &in, const std::vector<uint64_t> &swo, uint8_t *out) {
+  const uint32_t n = (uint32_t)swo.size() - 1;
+  std::vector<uint64_t> bounds(n + 1);
+  std::vector<int32_t> st(n ? n : 1);
+  size_t tried = 0;
+  bool first = true;
+  for (;;) {
+    if (in.available() > tried || (first && swo[n] == swo[0])) {
+      const int rc = cpk_decode_stream_host(gpu.get(), in.data(), in.available(), swo.data(), n, out,
+                                            bounds.data(), st.data());
+      if (rc == CPK_OK) {
+        in.consume(bounds[n]);
+        return;
+      }
+      if (rc != CPK_ETRUNC) check(rc, "readFromUnbuffered");
+      tried = in.available();
+    }
+    first = false;
+    if (!in.fill()) throw DecodeException("premature EOF");  // BufferedInputStreamWrapper.java:98-108
+    while (in.available() < 2 * tried && in.channel().ready(1))
+      if (!in.fill()) break;
+  }
+}
 
 // ---- PackedOutputStream: write(piece) == one PackedOutputStream.write ----
 class PackedOutputStream {
@@ -203,7 +318,66 @@ struct SerializePacked {
     return segs;
   }
 
+  // SerializePacked.writeToUnbuffered (SerializePacked.java:119-134): the
+  // message packed on the GPU, then every byte written to the channel.
+  static void writeToUnbuffered(Gpu &gpu, FdChannel &out, const std::vector<std::vector<uint8_t>> &segs) {
+    const std::vector<uint8_t> b = write(gpu, segs);
+    out.writeAll(b.data(), b.size());
+  }
+
+  // SerializePacked.readFromUnbuffered (SerializePacked.java:84-96): as read()
+  // above, over a channel (Serialize.read's checks, Serialize.java:119-178).
+  static std::vector<std::vector<uint8_t>> readFromUnbuffered(Gpu &gpu, ChannelReader &in,
+                                                              uint64_t traversal_limit_words = 8ull << 20) {
+    uint8_t first[8];
+    decodeFromChannel(gpu, in, {0, 1}, first);
+    int32_t raw, s0;
+    std::memcpy(&raw, first, 4);
+    std::memcpy(&s0, first + 4, 4);
+    if (raw < 0 || raw > 511) throw DecodeException("segment count must be between 0 and 512");
+    if (s0 < 0) throw DecodeException("segment 0 has more than 2^31 words, which is unsupported");
+    const uint32_t count = (uint32_t)raw + 1;
+    std::vector<uint64_t> sizes = {(uint64_t)s0};
+    uint64_t total = (uint64_t)s0;
+    if (count > 1) {
+      std::vector<uint8_t> rest(4 * (count & ~1u));
+      decodeFromChannel(gpu, in, {0, rest.size() / 8}, rest.data());
+      for (uint32_t i = 0; i + 1 < count; ++i) {
+        int32_t sz;
+        std::memcpy(&sz, rest.data() + 4 * i, 4);
+        if (sz < 0) throw DecodeException("segment has more than 2^31 words");
+        sizes.push_back((uint64_t)sz);
+        total += (uint64_t)sz;
+      }
+    }
+    if (total > traversal_limit_words) throw DecodeException("Message size exceeds traversal limit.");
+    for (auto sz : sizes)
+      if (sz > (1u << 28) - 1) throw DecodeException("segment has too many words");
+    std::vector<uint64_t> swo = {0};
+    for (auto sz : sizes) swo.push_back(swo.back() + sz);
+    std::vector<uint8_t> out(8 * total + 8);
+    if (total) decodeFromChannel(gpu, in, swo, out.data());
+    std::vector<std::vector<uint8_t>> segs;
+    for (uint32_t i = 0; i < count; ++i)
+      segs.emplace_back(out.begin() + 8 * swo[i], out.begin() + 8 * swo[i + 1]);
+    return segs;
+  }
+
+  // SerializePacked.tryReadFromUnbuffered (SerializePacked.java:67-79):
+  // nothing when the channel ends before a message starts.
+  static std::optional<std::vector<std::vector<uint8_t>>> tryReadFromUnbuffered(
+      Gpu &gpu, ChannelReader &in, uint64_t traversal_limit_words = 8ull << 20) {
+    if (in.available() == 0 && !in.fill()) return std::nullopt;
+    return readFromUnbuffered(gpu, in, traversal_limit_words);
+  }
+
   using Message = std::vector<std::vector<uint8_t>>;  // its segments
+
+  // writeToUnbuffered for many messages, packed in one GPU call
+  static void writeMessagesToUnbuffered(Gpu &gpu, FdChannel &out, const std::vector<Message> &msgs) {
+    const std::vector<uint8_t> b = writeMessages(gpu, msgs);
+    out.writeAll(b.data(), b.size());
+  }
 
   // write() for each message, ONE GPU call: the segment tables are built and
   // packed on the device (cpk_encode_messages_host).  Returns the packed

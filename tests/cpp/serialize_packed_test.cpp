@@ -1,8 +1,12 @@
 // SerializePackedTest (runtime/src/test/java/org/capnproto/SerializePackedTest.java)
 // written against the C++ mirror of the reference API (capnproto-java_amd/
 // csrc/host/packed_stream.hpp), every byte through the MI355X kernels.
+#include <unistd.h>
+
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "../../capnproto-java_amd/csrc/host/packed_stream.hpp"
@@ -181,6 +185,89 @@ int main() {
     ArrayInputStream in(scratch.data(), scratch.size());
     for (auto &segs : msgs) EXPECT(SerializePacked::read(gpu, in) == segs, "message from scratch");
     EXPECT(in.remaining() == scratch.size() - used, "stale bytes left unread");
+  }
+  // writeToUnbuffered / readFromUnbuffered through a pipe
+  // (SerializePacked.java:84-96, :119-134): 1000 messages of 1-5 segments,
+  // 0-64 KiB each, written by one thread (its own context) while another
+  // reads them back; then tryReadFromUnbuffered sees the end of the stream.
+  {
+    std::vector<SerializePacked::Message> msgs;
+    uint64_t words = 0;
+    uint32_t rs = 12345;
+    auto rnd = [&]() { return rs = rs * 1103515245u + 12345u, rs >> 8; };
+    for (int m = 0; m < 1000; ++m) {
+      SerializePacked::Message msg;
+      const int nseg = 1 + (int)(rnd() % 5);
+      for (int i = 0; i < nseg; ++i) {
+        const uint32_t w = (m % 97 == 0) ? 8192 : rnd() % 1200;
+        Bytes sg(8 * w, 0);
+        for (uint32_t j = 0; j < 8 * w; ++j)
+          if (rnd() % 3 == 0) sg[j] = (uint8_t)rnd();
+        words += w;
+        msg.push_back(sg);
+      }
+      msgs.push_back(msg);
+    }
+    int fds[2];
+    EXPECT(pipe(fds) == 0, "pipe");
+    const auto t0 = std::chrono::steady_clock::now();
+    std::thread writer([&]() {
+      Gpu wg(0);
+      FdChannel out(fds[1]);
+      for (auto &m : msgs) SerializePacked::writeToUnbuffered(wg, out, m);
+      close(fds[1]);
+    });
+    ChannelReader in{FdChannel(fds[0])};
+    int same = 0;
+    for (auto &m : msgs) {
+      try {
+        same += SerializePacked::readFromUnbuffered(gpu, in) == m;
+      } catch (const std::exception &e) {
+        EXPECT(false, e.what());
+        break;
+      }
+    }
+    writer.join();
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    EXPECT(same == (int)msgs.size(), "messages through the pipe");
+    EXPECT(!SerializePacked::tryReadFromUnbuffered(gpu, in).has_value(), "end of stream");
+    close(fds[0]);
+    std::printf("pipe: %zu messages, %.1f MiB of words, %.3f s: %.3f GiB/s, %.0f messages/s\n", msgs.size(),
+                words * 8 / 1048576.0, dt, words * 8 / dt / (1 << 30), msgs.size() / dt);
+    // the same messages packed in one GPU call, then read one by one
+    EXPECT(pipe(fds) == 0, "pipe");
+    const auto t1 = std::chrono::steady_clock::now();
+    std::thread writer2([&]() {
+      Gpu wg(0);
+      FdChannel out(fds[1]);
+      SerializePacked::writeMessagesToUnbuffered(wg, out, msgs);
+      close(fds[1]);
+    });
+    ChannelReader in2{FdChannel(fds[0])};
+    same = 0;
+    while (auto m = SerializePacked::tryReadFromUnbuffered(gpu, in2)) same += (size_t)same < msgs.size() && *m == msgs[same];
+    writer2.join();
+    const double dt2 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+    EXPECT(same == (int)msgs.size(), "batch-written messages through the pipe");
+    close(fds[0]);
+    std::printf("pipe (writeMessagesToUnbuffered): %.3f s: %.3f GiB/s\n", dt2, words * 8 / dt2 / (1 << 30));
+    // a message cut short by the end of the channel: premature EOF
+    EXPECT(pipe(fds) == 0, "pipe");
+    {
+      Bytes b = SerializePacked::write(gpu, msgs[5]);
+      FdChannel out(fds[1]);
+      out.writeAll(b.data(), b.size() - 3);
+      close(fds[1]);
+    }
+    ChannelReader in3{FdChannel(fds[0])};
+    bool threw = false;
+    try {
+      SerializePacked::readFromUnbuffered(gpu, in3);
+    } catch (const DecodeException &) {
+      threw = true;
+    }
+    EXPECT(threw, "truncated channel must throw DecodeException");
+    close(fds[0]);
   }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);

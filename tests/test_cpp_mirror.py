@@ -11,7 +11,7 @@ LIB = REPO / "capnproto-java_amd" / "lib"
 
 def _build(tmp_path):
     exe = tmp_path / "serialize_packed_test"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-o", str(exe),
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-pthread", "-o", str(exe),
                     str(REPO / "tests" / "cpp" / "serialize_packed_test.cpp"),
                     f"-L{LIB}", "-lcapnp_packed_hip", f"-Wl,-rpath,{LIB}",
                     "-Wl,-rpath,/opt/rocm/lib"], check=True)
@@ -29,3 +29,4 @@ def test_cpp_serialize_packed_test(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
     assert "all passed" in r.stdout
+    print(r.stdout)
