@@ -29,6 +29,8 @@ static void throw_status(JNIEnv *env, int st) {
                      st == CPK_EINVAL || st == CPK_EFRAME)
                         ? "org/capnproto/DecodeException"
                         : "java/io/IOException";
+  /* (the message is cpk_status_string's: PackedGpu.TRUNCATED tells a
+     truncation apart, DecodeException being final) */
   jclass c = (*env)->FindClass(env, cls);
   if (c) (*env)->ThrowNew(env, c, cpk_status_string(st));
 }

@@ -41,6 +41,17 @@ public final class PackedGpu implements AutoCloseable {
 
     private long handle;
 
+    /** The message of the DecodeException thrown when the packed bytes end
+     *  inside what a read must fill (CPK_ETRUNC, cpk_status_string; the
+     *  reference's "Premature EOF", ArrayInputStream.java:53-58).
+     *  DecodeException is final, so GpuDispatch tells truncation apart by it
+     *  and takes more bytes from a channel. */
+    public static final String TRUNCATED = "premature end of packed input";
+
+    public static boolean isTruncation(org.capnproto.DecodeException e) {
+        return TRUNCATED.equals(e.getMessage());
+    }
+
     /** A direct buffer of `bytes` bytes: ByteBuffer capacities are ints, so a
      *  batch whose packed or unpacked size passes 2 GiB - 1 must be split by
      *  the caller (an IOException here rather than a wrapped (int) cast). */

@@ -1,0 +1,102 @@
+"""Regenerates integration/capnproto-java.patch: the reference-side changes a
+capnproto-java maintainer applies (patch -p1 at the repository root) to
+select the MI355X codec.
+
+  runtime/.../SerializePacked.java  read / write dispatch to GpuDispatch when
+                                    enabled (SerializePacked.java:58-61, :101-114)
+  benchmark/.../Compression.java    Compression.GPU_PACKED (Compression.java:33-34)
+  benchmark/.../TestCase.java       the "gpu-packed" argument (TestCase.java:188-195)
+  do_benchmarks.bash                gpu-packed runs beside each packed run
+  + the new files: runtime/.../gpu/{PackedGpu,GpuDispatch}.java and
+    benchmark/.../GpuPacked.java, copied from capnproto-java_amd/java/.
+
+Run in the build container (reads the reference checkout):
+  python integration/make_patch.py [/root/reference]
+"""
+import shutil
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+JAVA = REPO / "capnproto-java_amd" / "java"
+EDITED = ["runtime/src/main/java/org/capnproto/SerializePacked.java",
+          "benchmark/src/main/java/org/capnproto/benchmark/Compression.java",
+          "benchmark/src/main/java/org/capnproto/benchmark/TestCase.java",
+          "do_benchmarks.bash"]
+NEW = {"runtime/src/main/java/org/capnproto/gpu/PackedGpu.java":
+       JAVA / "src/main/java/org/capnproto/gpu/PackedGpu.java",
+       "runtime/src/main/java/org/capnproto/gpu/GpuDispatch.java":
+       JAVA / "src/main/java/org/capnproto/gpu/GpuDispatch.java",
+       "benchmark/src/main/java/org/capnproto/benchmark/GpuPacked.java":
+       JAVA / "benchmark/src/main/java/org/capnproto/benchmark/GpuPacked.java"}
+
+
+def edit(path: Path, old: str, new: str):
+    s = path.read_text()
+    assert old in s, (path, old)
+    path.write_text(s.replace(old, new, 1))
+
+
+def main():
+    ref = Path(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")
+    with tempfile.TemporaryDirectory(dir=REPO / "build") as td:
+        a, b = Path(td) / "a", Path(td) / "b"
+        for f in EDITED:
+            for d in (a, b):
+                (d / f).parent.mkdir(parents=True, exist_ok=True)
+                shutil.copy(ref / f, d / f)
+        sp = b / EDITED[0]
+        edit(sp, "    public static MessageReader read(BufferedInputStream input, ReaderOptions options) "
+                 "throws java.io.IOException {\n",
+             "    public static MessageReader read(BufferedInputStream input, ReaderOptions options) "
+             "throws java.io.IOException {\n"
+             "        if (org.capnproto.gpu.GpuDispatch.enabled()) {\n"
+             "            return org.capnproto.gpu.GpuDispatch.read(input, options);\n"
+             "        }\n")
+        edit(sp, "    public static void write(BufferedOutputStream output,\n"
+                 "                             MessageBuilder message) throws java.io.IOException {\n",
+             "    public static void write(BufferedOutputStream output,\n"
+             "                             MessageBuilder message) throws java.io.IOException {\n"
+             "        if (org.capnproto.gpu.GpuDispatch.enabled()) {\n"
+             "            org.capnproto.gpu.GpuDispatch.write(output, message);\n"
+             "            return;\n"
+             "        }\n")
+        edit(b / EDITED[1], "    public final Compression UNCOMPRESSED = new Uncompressed();",
+             "    public final Compression UNCOMPRESSED = new Uncompressed();\n"
+             "    public final Compression GPU_PACKED = new GpuPacked();")
+        edit(b / EDITED[2], '        } else if (args[2].equals("none")) {\n'
+                            '            compression = Compression.UNCOMPRESSED;\n',
+             '        } else if (args[2].equals("none")) {\n'
+             '            compression = Compression.UNCOMPRESSED;\n'
+             '        } else if (args[2].equals("gpu-packed")) {\n'
+             '            compression = Compression.GPU_PACKED;\n')
+        db = b / EDITED[3]
+        edit(db, 'alias run_java="java -cp runtime/target/classes:benchmark/target/classes"',
+             'alias run_java="java -cp runtime/target/classes:benchmark/target/classes"\n'
+             '# gpu-packed: the MI355X codec (libcapnp_packed_jni.so + libcapnp_packed_hip.so '
+             'on java.library.path)\n'
+             'alias run_java_gpu="java -Djava.library.path=${CAPNP_GPU_LIB:-lib} '
+             '-cp runtime/target/classes:benchmark/target/classes"')
+        for t in ("CarSales", "CatRank", "Eval"):
+            line = f"time run_java org.capnproto.benchmark.{t} bytes no-reuse packed $ITERS\n"
+            edit(db, line, line + f"time run_java_gpu org.capnproto.benchmark.{t} bytes no-reuse gpu-packed $ITERS\n")
+            line = (f"time run_java org.capnproto.benchmark.{t} client no-reuse packed $ITERS < fifo | "
+                    f"run_java org.capnproto.benchmark.{t} server no-reuse packed $ITERS > fifo\n")
+            edit(db, line, line + f"time run_java_gpu org.capnproto.benchmark.{t} client no-reuse gpu-packed "
+                                  f"$ITERS < fifo | run_java_gpu org.capnproto.benchmark.{t} server no-reuse "
+                                  f"gpu-packed $ITERS > fifo\n")
+        for f, src in NEW.items():
+            (b / f).parent.mkdir(parents=True, exist_ok=True)
+            shutil.copy(src, b / f)
+        r = subprocess.run(["diff", "-ruN", "a", "b"], cwd=td, capture_output=True, text=True)
+        assert r.returncode in (0, 1), r.stderr
+        # (no timestamps: the patch is stable under regeneration)
+        lines = [ln.split("\t")[0] if ln.startswith(("--- ", "+++ ")) else ln
+                 for ln in r.stdout.splitlines()]
+        (REPO / "integration" / "capnproto-java.patch").write_text("\n".join(lines) + "\n")
+
+
+if __name__ == "__main__":
+    main()
