@@ -289,11 +289,13 @@ def run_rank(args, rank, world, local):
     pmc = REPO / "profiles" / "pmc_traffic.json"
     workload_key = f"config{args.config}:{n}x{args.seg_words if mso is None else 'mixed'}"
     if pmc.exists():
+        # PMC-measured HBM bytes per launch (tools/pmc_summary.py --json),
+        # keyed by the workload they were measured on
         try:
-            t = json.loads(pmc.read_text())
-            if t.get("workload") == workload_key and "decode" in t:
+            t = json.loads(pmc.read_text()).get(workload_key)
+            if t and "decode" in t:
                 traffic = int(t["decode"]["hbm_bytes"])
-        except (ValueError, KeyError, TypeError):
+        except (ValueError, KeyError, TypeError, AttributeError):
             traffic = None
 
     cpu = None

@@ -2,7 +2,7 @@
 mean counter value per dispatch of encode_kernel / decode_kernel, plus the
 HBM-traffic fields bench.py reads (FETCH_SIZE doubled on gfx950 and
 WRITE_SIZE, both in KB per rocprofv3 -> bytes).
-usage: python tools/pmc_summary.py gpurun_out/<tag> [--json out.json WORKLOAD]
+usage: python tools/pmc_summary.py gpurun_out/<tag> [--json out.json WORKLOAD] (merged by WORKLOAD)
 (WORKLOAD: the bench config string the passes ran, stored with the numbers so
 bench.py only reports traffic measured on its own workload)"""
 import csv
@@ -57,7 +57,16 @@ if len(sys.argv) > 3 and sys.argv[2] == "--json":
             # wide streaming reads (MI355X_MICROARCH.md HBM section)
             traffic[key] = {"fetch_bytes": 2 * 1024 * d["FETCH_SIZE"], "write_bytes": 1024 * d["WRITE_SIZE"],
                             "hbm_bytes": 2 * 1024 * d["FETCH_SIZE"] + 1024 * d["WRITE_SIZE"]}
-    traffic["workload"] = sys.argv[4] if len(sys.argv) > 4 else None
     traffic["source"] = str(root)
-    Path(sys.argv[3]).write_text(json.dumps(traffic, indent=1))
+    # one entry per workload in the file (merged with what it holds)
+    key = sys.argv[4] if len(sys.argv) > 4 else "unknown"
+    dst = Path(sys.argv[3])
+    try:
+        allw = json.loads(dst.read_text()) if dst.exists() else {}
+        if "workload" in allw:  # (the single-workload form of round 1)
+            allw = {}
+    except ValueError:
+        allw = {}
+    allw[key] = traffic
+    dst.write_text(json.dumps(allw, indent=1, sort_keys=True))
     print(json.dumps(traffic))
