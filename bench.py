@@ -280,23 +280,28 @@ def run_rank(args, rank, world, local):
     ms_per_step = 1e3 * wall / args.steps
     value = U_total / GIB / (wall / args.steps)
     r = P / U
-    # Roofline of the dominant kernel: the decode stage is one launch of
-    # decode_kernel (U+P algorithmic bytes); the encode stage's kernels are
+    # Roofline of the dominant kernel: the longer stage, each one launch of
+    # its main kernel (the single-pass encoder, sp_encode_kernel, or
+    # decode_kernel; U+P algorithmic bytes either way); the other stage is
     # reported beside it.  HIP events on the launch stream, median of K.
-    dom_ms = dec_ms
+    enc_kernel = "e4_size_kernel+e4_emit_kernel" if os.environ.get("CPK_ENCODER", "0")[:1] == "4" \
+        else "sp_encode_kernel"
+    dom_enc = enc_ms > dec_ms
+    dom_ms = enc_ms if dom_enc else dec_ms
     achieved = (U + P) / (dom_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = {"encode": None, "decode": None}
     pmc = REPO / "profiles" / "pmc_traffic.json"
     workload_key = f"config{args.config}:{n}x{args.seg_words if mso is None else 'mixed'}"
     if pmc.exists():
         # PMC-measured HBM bytes per launch (tools/pmc_summary.py --json),
         # keyed by the workload they were measured on
         try:
-            t = json.loads(pmc.read_text()).get(workload_key)
-            if t and "decode" in t:
-                traffic = int(t["decode"]["hbm_bytes"])
+            t = json.loads(pmc.read_text()).get(workload_key) or {}
+            for k in traffic:
+                if k in t:
+                    traffic[k] = int(t[k]["hbm_bytes"])
         except (ValueError, KeyError, TypeError, AttributeError):
-            traffic = None
+            pass
 
     cpu = None
     if not args.no_cpu:
@@ -333,19 +338,22 @@ def run_rank(args, rank, world, local):
         "encode_GiBps": round(U / GIB / (enc_ms * 1e-3), 2),
         "decode_GiBps": round(U / GIB / (dec_ms * 1e-3), 2),
         "roofline": {
-            "kernel": "decode_kernel",
+            "kernel": enc_kernel if dom_enc else "decode_kernel",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": PEAK_HBM_GBS,
             "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 4),
-            "traffic": traffic,
+            "traffic": traffic["encode" if dom_enc else "decode"],
             "algorithmic_bytes_per_launch": U + P,
         },
-        "encode_stage_roofline": {
-            "achieved": round((U + P) / (enc_ms * 1e-3) / 1e9, 1),
-            "frac": round((U + P) / (enc_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-            "note": "algorithmic U+P over the encode stage's event time",
+        ("decode_stage_roofline" if dom_enc else "encode_stage_roofline"): {
+            "kernel": "decode_kernel" if dom_enc else enc_kernel,
+            "ms": round(dec_ms if dom_enc else enc_ms, 3),
+            "achieved": round((U + P) / ((dec_ms if dom_enc else enc_ms) * 1e-3) / 1e9, 1),
+            "frac": round((U + P) / ((dec_ms if dom_enc else enc_ms) * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            "traffic": traffic["decode" if dom_enc else "encode"],
+            "note": "algorithmic U+P over the other stage's event time",
         },
         "roundtrip_roofline_frac": round(2 * (U + P) / ((enc_ms + dec_ms) * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
         "parity": {"mismatched_words_plus_bad_status": errors, "oracle_sample_equal": sample_ok},

@@ -516,10 +516,18 @@ __device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t 
 #define CPK_SP_DEFER 12  // steps laid out before the offset is needed (12 x 640 B < kSpRing)
 #endif
 constexpr int kSpDefer = CPK_SP_DEFER;
+// which waves may lay out all their steps before fetching the offset when
+// their output fits the ring (0: none; 1: waves 1-3; 2: all -- measured
+// best: the look-back then runs last, when the pieces before have published)
+#ifndef CPK_SP_FITS
+#define CPK_SP_FITS 2
+#endif
+#define CPK_SP_FITS_WAVES(w) (CPK_SP_FITS == 2 || (CPK_SP_FITS == 1 && (w) != 0))
 static_assert(kSpDefer * 640 + 16 <= (int)kSpRing, "deferred steps must fit the ring");
 template <class GetBase>
 __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, uint32_t *ring, uint8_t *out,
-                                     bool known, uint64_t g0, int lane, uint64_t ocap, GetBase getbase) {
+                                     bool known, bool fits, uint64_t g0, int lane, uint64_t ocap,
+                                     GetBase getbase) {
   uint32_t rel = 0, ft = 0;
   const uint32_t l64 = 64u - (uint32_t)lane;
   auto step = [&](const int j) __attribute__((always_inline)) {
@@ -592,7 +600,7 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
 #pragma unroll
   for (int j = 0; j < kSpDefer; ++j)
     if (j < cnt) step(j);
-  if (!known && cnt > kSpDefer) {
+  if (!known && !fits && cnt > kSpDefer) {
     g0 = getbase();
     known = true;
   }
@@ -644,11 +652,11 @@ __device__ __forceinline__ void sp_lookahead(const uint64_t *__restrict__ src, u
   ladl = rd;
 }
 
-// the decoupled look-back (wave 0, all lanes): publishes the aggregate,
-// returns the exclusive prefix, publishes the inclusive one
+// the decoupled look-back (wave 0, all lanes; the piece's aggregate was
+// published as soon as its size was known): returns the exclusive prefix,
+// publishes the inclusive one
 __device__ uint64_t sp_lookback(uint64_t *status, uint32_t p, uint64_t agg, uint32_t ep, uint32_t *err,
                                 int lane) {
-  if (lane == 0) st_status(&status[p], sp_word(ep, p == 0 ? 2u : 1u, agg));
   if (p == 0) return 0;
   uint64_t excl = 0;
   int64_t top = (int64_t)p - 1;
@@ -711,7 +719,7 @@ __device__ __forceinline__ SpSt sp_get_state(const uint64_t *scr, int par) {
 __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restrict__ pw, uint32_t W,
                                              uint32_t c, uint64_t *msk, uint64_t *scr, SpSt &cst,
                                              int w, int lane, bool kEmit, int &cnt, uint32_t &Xlast,
-                                             uint64_t &wbefore) {
+                                             uint64_t &wbefore, uint64_t &wmine) {
   const uint32_t ns = (W + 63) >> 6;
   const uint32_t cs0 = c * kSpCS;
   const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
@@ -767,10 +775,12 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   __syncthreads();  // wave bytes and the exit state in LDS
   uint64_t tot = 0;
   wbefore = 0;
+  wmine = 0;
 #pragma unroll
   for (int q = 0; q < kSpWaves; ++q) {
     const uint64_t b = sp_ld(&scr[16 + q]);
     if (q < w) wbefore += b;
+    if (q == w) wmine = b;
     tot += b;
   }
   cst = sp_get_state(scr, c & 1);
@@ -837,7 +847,7 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
       const uint32_t nch = (((W + 63) >> 6) + kSpCS - 1) / kSpCS;
       int cnt = 0;
       uint32_t Xlast = 0;
-      uint64_t wbefore = 0, total = 0, cbase = 0;
+      uint64_t wbefore = 0, wmine = 0, total = 0, cbase = 0;
       SpSt cst = {0u, 0u, 0u};
       // one chunk: A1, A2, offset, B.  More: every chunk sized (pass 0),
       // the offset, every chunk read again and emitted (pass 1).  One copy
@@ -847,18 +857,24 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
         const bool emit = nch <= 1 || it >= nch;
         const uint32_t c = nch > 1 ? (emit ? it - nch : it) : 0;
         if (emit && c == 0) cst = SpSt{0u, 0u, 0u};
-        const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, cst, w, lane, emit, cnt, Xlast, wbefore);
+        const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, cst, w, lane, emit, cnt, Xlast, wbefore, wmine);
         WPH(1)
         if (!emit) {
           total += ct;
           continue;
         }
         if (c == 0 && nch <= 1) total = ct;
+        if (c == 0 && w == 0 && lane == 0) {
+          // the piece's size, published before its strings are laid out: the
+          // pieces after it find it there when they look back
+          st_status(&status[p], sp_word(ep, p == 0 ? 2u : 1u, total));
+        }
         WPH(2)
         if (cnt) {
           // the offset: known past chunk 0; for chunk 0 the look-back (wave 0)
           // runs once the waves have laid out kSpDefer steps
           auto getbase = [&]() -> uint64_t {
+            WPH(4)
             if (w == 0) {
               const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
               if (lane == 0) {
@@ -868,12 +884,15 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
                 __builtin_amdgcn_s_waitcnt(0xc07f);  // (the offset before the flag)
                 scr[11] = (uint64_t)p + 1;
               }
+              WPH(5)
               return excl + wbefore;
             }
             while ((uint32_t)sp_ld(&scr[11]) != p + 1) __builtin_amdgcn_s_sleep(1);
+            WPH(6)
             return sp_ld(&scr[5]) + wbefore;
           };
-          sp_b(R, cnt, lut, ring, out, c != 0, cbase + wbefore, lane, ocap, getbase);
+          sp_b(R, cnt, lut, ring, out, c != 0, CPK_SP_FITS_WAVES(w) && wmine + 16 <= kSpRing, cbase + wbefore,
+               lane, ocap, getbase);
         } else if (c == 0 && w == 0) {
           // wave 0 runs the look-back even without steps (an empty piece)
           const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
