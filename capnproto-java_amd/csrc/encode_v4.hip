@@ -209,7 +209,8 @@ __device__ __forceinline__ uint32_t e4_next_piece(uint32_t *ticket, int &xq, int
 __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     uint64_t *__restrict__ sizes, uint32_t *ticket, uint64_t hint, uint32_t *err,
-    uint64_t *__restrict__ bvbuf, uint64_t stride) {
+    uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip) {
+  if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;  // (the single pass took the batch)
   const int lane = lane_id();
   const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
   int xq = xcc_id(), dry = 0;
@@ -439,7 +440,8 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
 __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint32_t *ticket,
-    const uint64_t *__restrict__ bvbuf, uint64_t stride) {
+    const uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip) {
+  if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint64_t *lut = reinterpret_cast<const uint64_t *>(smem + kE4oLut);
   const int lane = lane_id();
@@ -495,3 +497,40 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     }
   }
 }
+
+// ---- encoder choice on the device (cpk_encode_batch, no host sync) --------
+// min / max piece words of the batch (mm[0] preset to ~0, mm[1] to 0)
+__global__ __launch_bounds__(256) void e4_minmax_kernel(const uint64_t *__restrict__ swo, uint32_t n,
+                                                        uint32_t *mm) {
+  uint32_t lo = 0xffffffffu, hi = 0;
+  const uint32_t i0 = blockIdx.x * 1024 + threadIdx.x;
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t i = i0 + 256 * k;
+    if (i < n) {
+      const uint64_t w = swo[i + 1] - swo[i];
+      const uint32_t w32 = w > 0xffffffffull ? 0xffffffffu : (uint32_t)w;
+      lo = min(lo, w32);
+      hi = max(hi, w32);
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    lo = min(lo, (uint32_t)__shfl_xor((int)lo, d, 64));
+    hi = max(hi, (uint32_t)__shfl_xor((int)hi, d, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+// like-sized pieces of 1024-8192 words: the single pass (its ticket left at
+// 0, the two-pass kernels told to skip, tickets[kTkGate + 2]); else the
+// reverse (the single pass's ordered ticket exhausted)
+__global__ void e4_gate_kernel(uint32_t *tickets) {
+  const uint32_t lo = tickets[kTkGate], hi = tickets[kTkGate + 1];
+  const bool sp = lo >= 1024u && hi <= 8192u && 2u * lo >= hi;
+  if (threadIdx.x == 0) {
+    tickets[kTkGate + 2] = sp ? 1u : 0u;
+    tickets[kTkPlan] = sp ? 0u : 0x7fffffffu;
+  }
+}
+

@@ -44,6 +44,7 @@ constexpr int kTkEnc = 0;              // encoder counters [8]
 constexpr int kTkDec = 8 * kTkStride;  // decoder counters [8]
 constexpr int kTkPlan = 16 * kTkStride;
 constexpr int kTkErr = 17 * kTkStride;
+constexpr int kTkGate = 17 * kTkStride + 8;  // [2]: min, max piece words (encoder choice)
 constexpr int kTkWords = 18 * kTkStride;
 __device__ __forceinline__ int xcc_id() {
   int x;
@@ -1005,7 +1006,7 @@ struct cpk_ctx_s {
   uint64_t *status;       // look-back words
   uint64_t status_cap;    // entries
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
-  int encoder;            // 0: single pass (encode_sp.hip); 4: size + emit passes
+  int encoder;            // 0: single pass (encode_sp.hip); 4: size + emit passes; 5: by piece size
   int decoder;            // 2: record index (decode_v2.hip); 1: block map (decode_kernel)
   uint64_t *sp_status;    // single pass: look-back word per piece
   uint64_t sp_cap;        //   entries
@@ -1098,11 +1099,12 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
   if (!c) return CPK_ENOMEM;
   c->device = device;
   {
-    // CPK_ENCODER=0 selects the single-pass encoder (encode_sp.hip), 4 the
-    // two-pass one (encode_v4.hip); the default is whichever measured faster
-    // (single pass: 4.35 against 5.05 ms per 131,072 config-2 pieces)
+    // Encoders: the single pass (encode_sp.hip) for batches of pieces up to
+    // 8192 words (4.35 against 5.05 ms per 131,072 config-2 pieces), the two
+    // passes (encode_v4.hip) for larger ones (sp_takes).  CPK_ENCODER=0 / 4
+    // force one of them for every batch.
     const char *e = getenv("CPK_ENCODER");
-    c->encoder = (e && e[0] == '4') ? 4 : 0;
+    c->encoder = (e && e[0] == '4') ? 4 : (e && e[0] == '0') ? 0 : 5;
     // CPK_DECODER=1 selects the block-map decoder, 2 the record-index one
     const char *d = getenv("CPK_DECODER");
     c->decoder = (d && d[0] == '2') ? 2 : 1;
@@ -1141,9 +1143,21 @@ int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
 
 // Single-pass encoder (encode_sp.hip): one launch, the look-back words
 // epoch-tagged (cleared only when the epoch wraps or the array grows).
+// The single-pass encoder takes batches of like-sized pieces of 1024-8192
+// words: its ordered look-back makes every piece wait for the size of the
+// pieces before it, which a larger piece publishes late (sized chunk by
+// chunk) and tiny pieces each cost a workgroup round -- mixed 4-256 KiB
+// segments measured 2.4x slower than the two-pass encoder, mixed 4-64 KiB
+// 2.2x, uniform 64 KiB 14 % faster.  sp_takes screens the bound; the
+// device then checks the sizes themselves (e4_gate_kernel).
+static bool sp_takes(cpk_ctx ctx, uint64_t max_seg_words) {
+  if (ctx->encoder == 0) return true;  // (CPK_ENCODER=0: single pass for every batch)
+  return ctx->encoder != 4 && max_seg_words != 0 && max_seg_words <= 64ull * cpk::kSpCS;
+}
+
 int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64_t *pdesc,
               const uint64_t *tin, uint32_t n, uint64_t hint, void *d_out, uint64_t *d_out_off,
-              hipStream_t s) {
+              hipStream_t s, bool gated = false) {
   bool fresh = false;
   if (n > ctx->sp_cap) {
     if (ctx->sp_status) hipFree(ctx->sp_status);
@@ -1159,7 +1173,9 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
     fresh = true;
   }
   if (fresh && hipMemsetAsync(ctx->sp_status, 0, ctx->sp_cap * 8, s) != hipSuccess) return CPK_EDEVICE;
-  if (hipMemsetAsync(ctx->tickets + cpk::kTkEnc, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
+  // (gated: the ticket was set by e4_gate_kernel -- exhausted unless the
+  // batch is the single pass's)
+  if (!gated && hipMemsetAsync(ctx->tickets + cpk::kTkPlan, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
   // one piece per ticket: a workgroup holding two pieces would publish the
   // second's size only after emitting the first, and the pieces after it
   // would wait on that (a serial chain through the tickets)
@@ -1180,12 +1196,12 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
   if (pdesc)
     hipLaunchKernelGGL(cpk::sp_encode_kernel<true>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
-                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkEnc, ppt, hint,
+                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, ppt, hint,
                        ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr);
   else
     hipLaunchKernelGGL(cpk::sp_encode_kernel<false>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
-                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkEnc, ppt, hint,
+                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, ppt, hint,
                        ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr);
   return hip_ok(hipGetLastError());
 }
@@ -1196,7 +1212,7 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
 // per piece from the hint, or packed by word offset when there is no hint (the
 // batch's word count is then read back, synchronising the stream).
 int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, uint64_t hint,
-              void *d_out, uint64_t *d_out_off, hipStream_t s) {
+              void *d_out, uint64_t *d_out_off, hipStream_t s, bool gate = false) {
   const uint32_t nb = (uint32_t)((n + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
   int rc = ensure_status(ctx, (uint64_t)n + nb + 1);
   if (rc) return rc;
@@ -1222,11 +1238,23 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
   }
   uint64_t *sizes = ctx->status, *bsum = ctx->status + n;
   if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
+  if (gate) {
+    // which encoder takes the batch, decided on the device from the piece
+    // sizes (no host sync): the other's tickets are exhausted, so its
+    // kernels return at once (the scans then write offsets the single pass
+    // overwrites)
+    uint32_t *mm = ctx->tickets + cpk::kTkGate;
+    if (hipMemsetAsync(mm, 0xff, 4, s) != hipSuccess || hipMemsetAsync(mm + 1, 0, 4, s) != hipSuccess)
+      return CPK_EDEVICE;
+    hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3((n + 1023) / 1024), dim3(256), 0, s, d_swo, n, mm);
+    hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets);
+  }
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (n + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (n + cpk::kE4Waves - 1) / cpk::kE4Waves;
   hipLaunchKernelGGL(cpk::e4_size_kernel, dim3(grid), dim3(cpk::kE4Threads), 0, s,
                      (const uint64_t *)d_in, d_swo, n, sizes, ctx->tickets + cpk::kTkEnc, hint,
-                     ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride);
+                     ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride,
+                     gate ? (const uint32_t *)(ctx->tickets + cpk::kTkGate + 2) : (const uint32_t *)nullptr);
   hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
                      (const uint64_t *)sizes, n, bsum);
   hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bsum, nb);
@@ -1235,7 +1263,7 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
   hipLaunchKernelGGL(cpk::e4_emit_kernel, dim3(grid), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
                      (const uint64_t *)d_in, d_swo, n, (const uint64_t *)d_out_off,
                      (uint8_t *)d_out, ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv,
-                     stride);
+                     stride, gate ? (const uint32_t *)(ctx->tickets + cpk::kTkGate + 2) : (const uint32_t *)nullptr);
   return hip_ok(hipGetLastError());
 }
 
@@ -1250,8 +1278,10 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
   if (nm == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
   const uint64_t np = (uint64_t)nm + nseg;  // pieces: a table per message + the segments
   if (np > 0xffffffffull) return CPK_EINVAL;
-  if (ctx->encoder != 4) {
-    // single pass: piece descriptors in message order + the tables' words
+  if (ctx->encoder == 0) {
+    // single pass (forced; the segment tables make a message batch one of
+    // mixed sizes, which the two passes handle faster): piece descriptors in
+    // message order + the tables' words
     const uint64_t need = 2 * np + (uint64_t)nseg / 2 + nm + 2;
     if (need > ctx->sp_desc_cap) {
       if (ctx->sp_desc) hipFree(ctx->sp_desc);
@@ -1292,7 +1322,7 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
   if (nseg)
     hipLaunchKernelGGL(cpk::e4_size_kernel, dim3(grid), dim3(cpk::kE4Threads), 0, s,
                        (const uint64_t *)d_in, d_swo, nseg, ssize, ctx->tickets + cpk::kTkEnc,
-                       max_seg_words, ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride);
+                       max_seg_words, ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride, (const uint32_t *)nullptr);
   hipLaunchKernelGGL(cpk::msg_table_size_kernel, dim3(tg), dim3(tb), 0, s, d_swo, d_msg_seg_off, nm,
                      tsize);
   hipLaunchKernelGGL(cpk::msg_interleave_kernel, dim3(tg), dim3(tb), 0, s, d_msg_seg_off, nm,
@@ -1307,7 +1337,7 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
   if (nseg)
     hipLaunchKernelGGL(cpk::e4_emit_kernel, dim3(grid), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
                        (const uint64_t *)d_in, d_swo, nseg, (const uint64_t *)soff, (uint8_t *)d_out,
-                       ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv, stride);
+                       ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv, stride, (const uint32_t *)nullptr);
   return hip_ok(hipGetLastError());
 }
 
@@ -1318,8 +1348,12 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
-  if (ctx->encoder == 4) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
-  return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s);
+  if (!sp_takes(ctx, max_seg_words)) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
+  if (ctx->encoder == 0) return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s);
+  // by piece size: both enqueued, the device picks one (e4_gate_kernel)
+  int rc = e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s, true);
+  if (rc) return rc;
+  return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s, true);
 }
 
 int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {

@@ -17,7 +17,10 @@ import capnp_packed as cp  # noqa: E402
 
 nm = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 rng = np.random.default_rng(3)
-seg = rng.choice([512, 1024, 2048, 4096, 8192, 16384, 32768], size=(nm, 4)).astype(np.uint64)
+import os  # noqa: E402
+maxw = int(os.environ.get("MB_MAXW", "32768"))  # (largest segment size drawn)
+seg = rng.choice([w for w in (512, 1024, 2048, 4096, 8192, 16384, 32768) if w <= maxw],
+                 size=(nm, 4)).astype(np.uint64)
 sizes = np.concatenate([np.full((nm, 1), 3, np.uint64), seg], axis=1).reshape(-1)
 swo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
 n = len(sizes)
@@ -36,7 +39,7 @@ d_in[idx] = tw
 cap = (cp.batch_capacity(swo) + 63) // 16 * 16
 d_pk = torch.zeros(cap, dtype=torch.uint8, device="cuda")
 d_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
-ctx.encode_batch(d_in, d_swo, 32768, d_pk, d_off)
+ctx.encode_batch(d_in, d_swo, maxw, d_pk, d_off)
 assert ctx.take_error() == 0
 torch.cuda.synchronize()
 d_moff = d_off[::5].contiguous()  # message m starts at its table piece; [nm] = total
@@ -102,11 +105,11 @@ d_sswo = torch.from_numpy(sswo).cuda()
 d_msegs = torch.arange(0, 4 * nm + 1, 4, dtype=torch.int64, device="cuda")
 d_pk2 = torch.zeros_like(d_pk)
 d_off2 = torch.empty(n + 1, dtype=torch.int64, device="cuda")
-ctx.encode_messages(d_seg, d_sswo, d_msegs, 32768, d_pk2, d_off2)
+ctx.encode_messages(d_seg, d_sswo, d_msegs, maxw, d_pk2, d_off2)
 assert ctx.take_error() == 0
 assert torch.equal(d_off2, d_off) and torch.equal(d_pk2[:P], d_pk[:P])
-t_em = timed(lambda: ctx.encode_messages(d_seg, d_sswo, d_msegs, 32768, d_pk2, d_off2))
-t_eb = timed(lambda: ctx.encode_batch(d_in, d_swo, 32768, d_pk2, d_off2))
+t_em = timed(lambda: ctx.encode_messages(d_seg, d_sswo, d_msegs, maxw, d_pk2, d_off2))
+t_eb = timed(lambda: ctx.encode_batch(d_in, d_swo, maxw, d_pk2, d_off2))
 
 t_m = timed(run_msgs)
 t_b = timed(lambda: ctx.decode_batch(d_pk, d_off, d_swo, d_bout, d_bst))

@@ -10,10 +10,11 @@ import capnp_packed as cp
 n = int(__import__("os").environ.get("QB_N", "131072"))
 cfgs = [int(c) for c in __import__("os").environ.get("QB_CFG", "2").split(",")]
 libs = sys.argv[1:]
-hint = int(__import__("os").environ.get("QB_HINT", "8192"))  # 0: tiled encoder path
-swo = np.arange(0, (n + 1) * 8192, 8192, dtype=np.uint64)
+hint = int(__import__("os").environ.get("QB_HINT", __import__("os").environ.get("QB_W", "8192")))  # 0: tiled encoder path
+W = int(__import__("os").environ.get("QB_W", "8192"))  # words per piece
+swo = np.arange(0, (n + 1) * W, W, dtype=np.uint64)
 d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
-d_in = torch.empty(n * 8192, dtype=torch.int64, device="cuda")
+d_in = torch.empty(n * W, dtype=torch.int64, device="cuda")
 cap = cp.batch_capacity(swo)
 d_pk = torch.empty((cap + 255) // 256 * 256, dtype=torch.uint8, device="cuda")
 d_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
@@ -40,7 +41,7 @@ for cfg in cfgs:
     cp._lib = handles[0][1]
     handles[0][2].generate(cp.preset(cfg), d_swo, d_in)
     torch.cuda.synchronize()
-    U = n * 65536
+    U = n * W * 8
     print(f"config {cfg}: n={n}", flush=True)
     for name, L, ctx in handles:
         cp._lib = L
@@ -54,7 +55,7 @@ for cfg in cfgs:
             if rnd:
                 te.append(e[0].elapsed_time(e[1])); td.append(e[1].elapsed_time(e[2]))
         err = ctx.take_error() if hasattr(L, "cpk_ctx_take_error") else 0
-        cnt.zero_(); ctx.count_mismatch(d_in, d_out, n * 8192, cnt)
+        cnt.zero_(); ctx.count_mismatch(d_in, d_out, n * W, cnt)
         P = int(d_off[-1].item())
         me, md = np.median(te), np.median(td)
         print(f"  {name:44s} enc {me:8.3f} ms ({U / me / 1e6:7.1f} GB/s)  dec {md:8.3f} ms ({U / md / 1e6:7.1f} GB/s)"
