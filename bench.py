@@ -284,7 +284,10 @@ def run_rank(args, rank, world, local):
     # its main kernel (the single-pass encoder, sp_encode_kernel, or
     # decode_kernel; U+P algorithmic bytes either way); the other stage is
     # reported beside it.  HIP events on the launch stream, median of K.
-    enc_kernel = "e4_size_kernel+e4_emit_kernel" if os.environ.get("CPK_ENCODER", "0")[:1] == "4" \
+    # (the library's choice: the single pass for like-sized 64 KiB pieces,
+    # the two passes for message batches; CPK_ENCODER forces one)
+    forced = os.environ.get("CPK_ENCODER", "")[:1]
+    enc_kernel = "e4_size_kernel+e4_emit_kernel" if forced == "4" or (mso is not None and forced != "0") \
         else "sp_encode_kernel"
     dom_enc = enc_ms > dec_ms
     dom_ms = enc_ms if dom_enc else dec_ms
