@@ -523,67 +523,81 @@ constexpr int kSpDefer = CPK_SP_DEFER;
 #define CPK_SP_FITS 2
 #endif
 #define CPK_SP_FITS_WAVES(w) (CPK_SP_FITS == 2 || (CPK_SP_FITS == 1 && (w) != 0))
-static_assert(kSpDefer * 640 + 16 <= (int)kSpRing, "deferred steps must fit the ring");
+static_assert(kSpDefer * 640 + 16 <= (int)kSpRing && kSpDefer % 2 == 0, "deferred steps must fit the ring");
 template <class GetBase>
 __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, uint32_t *ring, uint8_t *out,
                                      bool known, bool fits, uint64_t g0, int lane, uint64_t ocap,
                                      GetBase getbase) {
   uint32_t rel = 0, ft = 0;
   const uint32_t l64 = 64u - (uint32_t)lane;
+  // step j's string per lane (s0..s2, nb bytes)
+  auto strings = [&](const int j, uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &nb)
+      __attribute__((always_inline)) {
+    const uint64_t ZO = sp_rl(R.ozl, R.ozh, j), Mem = sp_rl(R.oml, R.omh, j);
+    const uint64_t HC = sp_rl(R.ohl, R.ohh, j);
+    const uint32_t m = (R.mp[j >> 2] >> (8 * (j & 3))) & 0xffu;
+    const uint32_t lo = (uint32_t)R.v[j], hi = (uint32_t)(R.v[j] >> 32);
+    const uint64_t sel = lut[m];
+    const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
+    const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+    uint32_t cz = 0, cd = 0;
+    if (HC) {
+      // a head's count: words to its run's end, at most 255 (:119-131, :143-164)
+      const uint32_t X = (uint32_t)__builtin_amdgcn_readlane((int)R.ox, j);
+      const uint64_t E = sp_rl(R.oel, R.oeh, j);
+      const uint64_t e = E >> lane;
+      // ctz of e, 0xffffffff when e == 0 (the next run end is past the step)
+      const uint32_t z_lo = (uint32_t)e ? (uint32_t)__builtin_ctz((uint32_t)e) : 0xffffffffu;
+      const uint32_t z_hi = (uint32_t)(e >> 32) ? (uint32_t)__builtin_ctz((uint32_t)(e >> 32)) + 32u
+                                                : 0xffffffffu;
+      uint32_t tt = min(min(z_lo, z_hi), l64 + X);
+      tt = min(tt, 255u);
+      const uint32_t cn = sp_sel(0u, tt, HC);
+      cz = m == 0 ? cn : 0u;
+      cd = cn - cz;
+    }
+    // the string: tag, the nonzero bytes, the count after a 0x00 / 0xFF tag
+    // (c0 is zero for a zero word); a literal-run member is its 8 bytes
+    const uint32_t c0p = c0 | cz;
+    s0 = m | (c0p << 8);
+    s1 = __builtin_amdgcn_alignbyte(c1, c0p, 3);
+    s2 = __builtin_amdgcn_alignbyte(cd, c1, 3);
+    s0 = sp_sel(s0, lo, Mem);
+    s1 = sp_sel(s1, hi, Mem);
+    s2 = sp_sel(s2, 0u, Mem);
+    nb = (uint32_t)__builtin_popcount(m) + sp_sel(1u, 2u, HC);
+    nb = sp_sel(nb, 8u, Mem);
+    nb = sp_sel(nb, 0u, ZO);
+  };
+  // a string OR-ed into the ring at relative byte p
+  auto put = [&](uint32_t p, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t nb) __attribute__((always_inline)) {
+    const uint32_t sh = (p & 3) * 8;
+    const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
+    const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
+    const uint32_t d3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
+    uint32_t *rp = ring + ((p >> 2) & (kSpRing / 4 - 1));
+    if (nb) {  // (zero-length strings would all hit one address)
+      atomicOr(rp, (uint32_t)a01);
+      atomicOr(rp + 1, (uint32_t)(a01 >> 32));
+      atomicOr(rp + 2, (uint32_t)(a12 >> 32));
+      atomicOr(rp + 3, d3);
+    }
+  };
+  // steps j and j + 1 (when j + 1 < cnt): both byte counts in one wave scan
+  // (16-bit halves: a step's strings total at most 640 bytes)
   auto step = [&](const int j) __attribute__((always_inline)) {
     {
-      const uint64_t ZO = sp_rl(R.ozl, R.ozh, j), Mem = sp_rl(R.oml, R.omh, j);
-      const uint64_t HC = sp_rl(R.ohl, R.ohh, j);
-      const uint32_t m = (R.mp[j >> 2] >> (8 * (j & 3))) & 0xffu;
-      const uint32_t lo = (uint32_t)R.v[j], hi = (uint32_t)(R.v[j] >> 32);
-      const uint64_t sel = lut[m];
-      const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
-      const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
-      uint32_t cz = 0, cd = 0;
-      if (HC) {
-        // a head's count: words to its run's end, at most 255 (:119-131, :143-164)
-        const uint32_t X = (uint32_t)__builtin_amdgcn_readlane((int)R.ox, j);
-        const uint64_t E = sp_rl(R.oel, R.oeh, j);
-        const uint64_t e = E >> lane;
-        // ctz of e, 0xffffffff when e == 0 (the next run end is past the step)
-        const uint32_t z_lo = (uint32_t)e ? (uint32_t)__builtin_ctz((uint32_t)e) : 0xffffffffu;
-        const uint32_t z_hi = (uint32_t)(e >> 32) ? (uint32_t)__builtin_ctz((uint32_t)(e >> 32)) + 32u
-                                                  : 0xffffffffu;
-        uint32_t tt = min(min(z_lo, z_hi), l64 + X);
-        tt = min(tt, 255u);
-        const uint32_t cn = sp_sel(0u, tt, HC);
-        cz = m == 0 ? cn : 0u;
-        cd = cn - cz;
-      }
-      // the string: tag, the nonzero bytes, the count after a 0x00 / 0xFF tag
-      // (c0 is zero for a zero word); a literal-run member is its 8 bytes
-      const uint32_t c0p = c0 | cz;
-      uint32_t s0 = m | (c0p << 8);
-      uint32_t s1 = __builtin_amdgcn_alignbyte(c1, c0p, 3);
-      uint32_t s2 = __builtin_amdgcn_alignbyte(cd, c1, 3);
-      s0 = sp_sel(s0, lo, Mem);
-      s1 = sp_sel(s1, hi, Mem);
-      s2 = sp_sel(s2, 0u, Mem);
-      uint32_t nb = (uint32_t)__builtin_popcount(m) + sp_sel(1u, 2u, HC);
-      nb = sp_sel(nb, 8u, Mem);
-      nb = sp_sel(nb, 0u, ZO);
-      const int incl = wave_incl_add((int)nb);
-      const uint32_t o = (uint32_t)incl - nb;
-      const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+      uint32_t a0, a1, a2, na, b0 = 0, b1 = 0, b2 = 0, nb2 = 0;
+      strings(j, a0, a1, a2, na);
+      if (j + 1 < cnt) strings(j + 1, b0, b1, b2, nb2);
+      const uint32_t pk = na | (nb2 << 16);
+      const uint32_t incl = (uint32_t)wave_incl_add((int)pk);
+      const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       if (stot) {
-        const uint32_t p = rel + o;
-        const uint32_t sh = (p & 3) * 8;
-        const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
-        const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
-        const uint32_t d3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
-        uint32_t *rp = ring + ((p >> 2) & (kSpRing / 4 - 1));
-        if (nb) {  // (zero-length strings would all hit one address)
-          atomicOr(rp, (uint32_t)a01);
-          atomicOr(rp + 1, (uint32_t)(a01 >> 32));
-          atomicOr(rp + 2, (uint32_t)(a12 >> 32));
-          atomicOr(rp + 3, d3);
-        }
-        rel += stot;
+        const uint32_t ta = stot & 0xffffu;
+        put(rel + (incl & 0xffffu) - na, a0, a1, a2, na);
+        put(rel + ta + (incl >> 16) - nb2, b0, b1, b2, nb2);
+        rel += ta + (stot >> 16);
         // complete lines leave 64 at a time (one full-wave store)
         if (known) {
           const uint32_t done = ((uint32_t)(g0 & 15) + rel) >> 4;
@@ -598,14 +612,14 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
   };
   // (two fully unrolled loops around the one place the offset may be fetched)
 #pragma unroll
-  for (int j = 0; j < kSpDefer; ++j)
+  for (int j = 0; j < kSpDefer; j += 2)
     if (j < cnt) step(j);
   if (!known && !fits && cnt > kSpDefer) {
     g0 = getbase();
     known = true;
   }
 #pragma unroll
-  for (int j = kSpDefer; j < kSpWS; ++j)
+  for (int j = kSpDefer; j < kSpWS; j += 2)
     if (j < cnt) step(j);
   if (!known) g0 = getbase();
   wave_lds_order();
