@@ -44,7 +44,7 @@ constexpr int kTkEnc = 0;              // encoder counters [8]
 constexpr int kTkDec = 8 * kTkStride;  // decoder counters [8]
 constexpr int kTkPlan = 16 * kTkStride;
 constexpr int kTkErr = 17 * kTkStride;
-constexpr int kTkGate = 17 * kTkStride + 8;  // [2]: min, max piece words (encoder choice)
+constexpr int kTkGate = 17 * kTkStride + 8;  // [0..1] min, max piece words, [2] encoder choice, [4..5] decoder choice
 constexpr int kTkWords = 18 * kTkStride;
 __device__ __forceinline__ int xcc_id() {
   int x;
@@ -373,6 +373,7 @@ struct DecStreams {
   const uint64_t *sbeg, *send, *spc;
   uint32_t ns;
   uint64_t *send_out;
+  const uint32_t *skip;  // (batch form: nonzero = the other decoder took the batch)
 };
 template <bool kStream>
 __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
@@ -386,6 +387,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
   uint8_t *wbuf = wl;                                            // window bytes
   uint32_t *blk = reinterpret_cast<uint32_t *>(wl + kWinBuf);    // [256]
   VisMask *visa = reinterpret_cast<VisMask *>(blk);  // [64], over the block map
+  if (sd.skip && __builtin_amdgcn_readfirstlane(*sd.skip)) return;
   fill_luts(lut, true);
   __syncthreads();  // the only block-wide barrier: LUT ready
   int xq = xcc_id(), dry = 0;
@@ -1007,7 +1009,7 @@ struct cpk_ctx_s {
   uint64_t status_cap;    // entries
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
   int encoder;            // 0: single pass (encode_sp.hip); 4: size + emit passes; 5: by piece size
-  int decoder;            // 2: record index (decode_v2.hip); 1: block map (decode_kernel)
+  int decoder;            // 2: record index (decode_v2.hip); 1: block map (decode_kernel); 3: by density
   uint64_t *sp_status;    // single pass: look-back word per piece
   uint64_t sp_cap;        //   entries
   uint32_t sp_epoch;      //   launch epoch tagging the look-back words, 1..65535
@@ -1107,7 +1109,7 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     c->encoder = (e && e[0] == '4') ? 4 : (e && e[0] == '0') ? 0 : 5;
     // CPK_DECODER=1 selects the block-map decoder, 2 the record-index one
     const char *d = getenv("CPK_DECODER");
-    c->decoder = (d && d[0] == '2') ? 2 : 1;
+    c->decoder = (d && d[0] == '2') ? 2 : (d && d[0] == '1') ? 1 : 3;
   }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
@@ -1373,10 +1375,14 @@ int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
 // one launch of the configured decoder (grid: as many workgroups per CU as
 // its LDS allows, at most 8; never more than the work needs)
 namespace {
+// which decoder a single-decoder call uses (the record-index one only when
+// forced: the by-density choice is made for batches, cpk_decode_batch)
+bool dec_v2(cpk_ctx ctx) { return ctx->decoder == 2; }
+
 void dec_launch(cpk_ctx ctx, bool stream, unsigned want, const uint8_t *packed, uint64_t *in_off,
                 const uint64_t *swo, uint32_t n, uint64_t *out, int32_t *status, uint64_t avail,
-                cpk::DecStreams sd, hipStream_t s) {
-  const bool v2 = ctx->decoder == 2;
+                cpk::DecStreams sd, hipStream_t s, int which = 0) {
+  const bool v2 = which ? which == 2 : dec_v2(ctx);
   const uint32_t lds = v2 ? cpk::kD2Lds : cpk::kDecLds;
   const unsigned per_cu = (unsigned)min(8u, 160u * 1024u / lds);
   unsigned grid = per_cu * (unsigned)ctx->cus;
@@ -1409,8 +1415,20 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
     return CPK_EDEVICE;
   // persistent: blocks of 4 independent waves, as many per CU as the LDS holds
-  dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, const_cast<uint64_t *>(d_in_off), d_swo, n,
-             (uint64_t *)d_out, d_status, 0, cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr}, s);
+  uint64_t *in_off = const_cast<uint64_t *>(d_in_off);
+  if (ctx->decoder != 3) {
+    dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, in_off, d_swo, n, (uint64_t *)d_out,
+               d_status, 0, cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr, nullptr}, s);
+    return hip_ok(hipGetLastError());
+  }
+  // by density, decided on the device (dec_gate_kernel): both enqueued, the
+  // one not chosen returns at its first instruction
+  uint32_t *skip = ctx->tickets + cpk::kTkGate + 4;
+  hipLaunchKernelGGL(cpk::dec_gate_kernel, dim3(1), dim3(64), 0, s, (const uint64_t *)d_in_off, d_swo, n, skip);
+  dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, in_off, d_swo, n, (uint64_t *)d_out, d_status, 0,
+             cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr, skip}, s, 1);
+  dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, in_off, d_swo, n, (uint64_t *)d_out, d_status, 0,
+             cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr, skip + 1}, s, 2);
   return hip_ok(hipGetLastError());
 }
 
