@@ -289,6 +289,11 @@ def run_rank(args, rank, world, local):
     forced = os.environ.get("CPK_ENCODER", "")[:1]
     enc_kernel = "e4_size_kernel+e4_emit_kernel" if forced == "4" or (mso is not None and forced != "0") \
         else "sp_encode_kernel"
+    # (the batch decoder: the record-index one for sparse batches, packed
+    # under 15 % of the words' bytes, else the block map; messages: block map)
+    forced_d = os.environ.get("CPK_DECODER", "")[:1]
+    dec_kernel = "decode2_kernel" if forced_d == "2" or (forced_d != "1" and mso is None and 100 * P < 15 * U) \
+        else "decode_kernel"
     dom_enc = enc_ms > dec_ms
     dom_ms = enc_ms if dom_enc else dec_ms
     achieved = (U + P) / (dom_ms * 1e-3) / 1e9
@@ -341,7 +346,7 @@ def run_rank(args, rank, world, local):
         "encode_GiBps": round(U / GIB / (enc_ms * 1e-3), 2),
         "decode_GiBps": round(U / GIB / (dec_ms * 1e-3), 2),
         "roofline": {
-            "kernel": enc_kernel if dom_enc else "decode_kernel",
+            "kernel": enc_kernel if dom_enc else dec_kernel,
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": PEAK_HBM_GBS,
@@ -351,7 +356,7 @@ def run_rank(args, rank, world, local):
             "algorithmic_bytes_per_launch": U + P,
         },
         ("decode_stage_roofline" if dom_enc else "encode_stage_roofline"): {
-            "kernel": "decode_kernel" if dom_enc else enc_kernel,
+            "kernel": dec_kernel if dom_enc else enc_kernel,
             "ms": round(dec_ms if dom_enc else enc_ms, 3),
             "achieved": round((U + P) / ((dec_ms if dom_enc else enc_ms) * 1e-3) / 1e9, 1),
             "frac": round((U + P) / ((dec_ms if dom_enc else enc_ms) * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),

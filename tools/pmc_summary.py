@@ -42,14 +42,22 @@ for kern in ("sp_encode_kernel", "e4_size_kernel", "e4_emit_kernel", "decode_ker
                 print(f"  {c:22s} {100 * d[c] / wc:6.1f} % of wave cycles")
 if len(sys.argv) > 3 and sys.argv[2] == "--json":
     traffic = {}
-    # the v4 encode stage = size pass + emit pass: their traffic adds up
+    # The library enqueues both encoders (and both batch decoders) and the
+    # one not chosen returns at once: the stage's traffic is the working
+    # one's -- the larger (the v4 encode stage = size pass + emit pass)
+    def traffic_of(d):
+        return d.get("FETCH_SIZE", 0) + d.get("WRITE_SIZE", 0)
+    enc = []
     if "sp_encode_kernel" in out:
-        out["encode_kernel"] = out["sp_encode_kernel"]
-    elif "e4_size_kernel" in out and "e4_emit_kernel" in out:
-        out["encode_kernel"] = {c: out["e4_size_kernel"].get(c, 0) + out["e4_emit_kernel"].get(c, 0)
-                                for c in ("FETCH_SIZE", "WRITE_SIZE")}
-    if "decode2_kernel" in out:
-        out["decode_kernel"] = out["decode2_kernel"]
+        enc.append(out["sp_encode_kernel"])
+    if "e4_size_kernel" in out and "e4_emit_kernel" in out:
+        enc.append({c: out["e4_size_kernel"].get(c, 0) + out["e4_emit_kernel"].get(c, 0)
+                    for c in ("FETCH_SIZE", "WRITE_SIZE")})
+    if enc:
+        out["encode_kernel"] = max(enc, key=traffic_of)
+    dec = [out[k] for k in ("decode_kernel", "decode2_kernel") if k in out]
+    if dec:
+        out["decode_kernel"] = max(dec, key=traffic_of)
     for kern, key in (("encode_kernel", "encode"), ("decode_kernel", "decode")):
         d = out.get(kern, {})
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
