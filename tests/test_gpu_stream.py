@@ -189,3 +189,25 @@ def test_device_stream_decode(ctx, oracle):
     assert np.array_equal(d_io.cpu().numpy().astype(np.uint64), off)
     got = d_out.cpu().numpy().view(np.uint8)[: data.size]
     assert np.array_equal(got, data)
+
+
+def test_parallel_stream_garbage_matches_one_wave(ctx, oracle):
+    """Random bytes as a packed stream (mostly malformed: truncations, runs
+    across piece ends) and valid streams with random byte flips, at sizes
+    that take the parallel path: every status, boundary and decoded word
+    equals the one-wave decoder's and the oracle's."""
+    rng = np.random.default_rng(77)
+    for trial in range(6):
+        n = int(rng.integers(1, 40))
+        sizes = [int(x) for x in rng.integers(0, 30000, size=n)]
+        swo = _swo(sizes)
+        if trial % 2 == 0:
+            stream = bytes(rng.integers(0, 256, size=400_000, dtype=np.uint8))
+        else:
+            data = oracle.generate(oracle.preset(int(rng.integers(2, 5))), swo)
+            b = bytearray(_stream_of(oracle, data, swo)[0])
+            for i in rng.integers(0, len(b), size=int(rng.integers(1, 5))):
+                b[int(i)] = int(rng.integers(0, 256))
+            stream = bytes(b) + bytes(rng.integers(0, 256, size=300_000, dtype=np.uint8))
+        _check(ctx, oracle, stream, swo)
+
