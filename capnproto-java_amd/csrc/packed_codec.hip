@@ -299,6 +299,16 @@ static_assert(kDecChunk <= 64, "visited mask bits");
 constexpr uint32_t kDecWaveLds = kWinBuf + (4 * (kRound / kBlk) > 64 * sizeof(VisMask)
                                                 ? 4 * (kRound / kBlk)
                                                 : 64 * sizeof(VisMask));
+#ifndef CPK_DEC_MAXMAP
+#define CPK_DEC_MAXMAP 1
+#endif
+// CPK_DEC_MAXMAP: a record marks only the block whose span ends at or after
+// its first word (ds_max of an entry ordered by output position), and a
+// prefix max over the blocks hands every block the last record starting at
+// or before its first word: one LDS op per record, no per-block loop
+constexpr int kMapPer = kRound / kBlk / 64;  // map entries per lane in the fill
+static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 && kRound + 256 < (1 << 19)),
+              "max-map entry: 12-bit window position, 19-bit output position");
 constexpr int kWinLinesPerLane = (int)((kWin + 47 + 15) / 16 + 63) / 64;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;                // 15,616
 
@@ -574,6 +584,12 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
       const bool chk = (ow + T >= W) || (P - e < 3 * kWin);
       for (int rb = 0; rb < T; rb += kRound) {
         int err = 0x7fffffff;
+#if CPK_DEC_MAXMAP
+        wave_lds_order();  // (the visited masks / last round's map reads are done)
+#pragma unroll
+        for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = 0u;
+        wave_lds_order();
+#endif
         // after the first round only the lanes whose output meets this round
         if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
           int o = o0;
@@ -599,11 +615,20 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
               if (code) err = (int)(((q - e) << 3) | (uint32_t)code);  // window-relative
               if (oo + nw == W) fin = q + adv;
             }
+#if CPK_DEC_MAXMAP
+            {
+              const int rel = o - rb;  // round-relative output of the record (> -256 when live)
+              const int idx = (max(rel, 0) + kBlk - 1) / kBlk;
+              if (rel + nw > 0 && idx < kRound / kBlk)
+                atomicMax(&blk[idx], ((uint32_t)(rel + 256) << 12) | (q - e));
+            }
+#else
             // blocks of this round whose first word this record covers
             const int lo = max(o, rb), hi = min(o + nw, rb + kRound);
             // window-relative record position (< 2 KiB) | offset in the run
             for (int bb = (lo + kBlk - 1) & ~(kBlk - 1); bb < hi; bb += kBlk)
               blk[(bb - rb) / kBlk] = (q - e) | ((uint32_t)(bb - o) << 16);
+#endif
             o += nw;
             q += adv;
           }
@@ -618,12 +643,33 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
           fin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u(fin));
         }
         wave_lds_order();
+#if CPK_DEC_MAXMAP
+        {
+          // prefix max: lane l holds blocks [kMapPer * l, kMapPer * (l + 1))
+          uint32_t m[kMapPer];
+          int run = 0;
+#pragma unroll
+          for (int i = 0; i < kMapPer; ++i) {
+            run = max(run, (int)blk[lane * kMapPer + i]);
+            m[i] = (uint32_t)run;
+          }
+          const uint32_t pre = (uint32_t)wave_shr1(wave_incl_max(run), 0);
+#pragma unroll
+          for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = max(m[i], pre);
+        }
+        wave_lds_order();
+#endif
         WPH(5)
         const int nb = (min(min(kRound, T - rb), W - ow - rb) + kBlk - 1) / kBlk;
         for (int b = lane; b < nb; b += 64) {
           const uint32_t v = blk[b];
+#if CPK_DEC_MAXMAP
+          uint32_t q = e + (v & 0xfffu);
+          int ofs = kBlk * b + 256 - (int)(v >> 12);
+#else
           uint32_t q = e + (v & 0xffffu);
           int ofs = (int)(v >> 16);
+#endif
           const int wbase = ow + rb + kBlk * b;  // piece word of the block's first word
           uint64_t words[kBlk];
 #pragma unroll
