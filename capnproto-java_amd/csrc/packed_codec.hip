@@ -267,20 +267,22 @@ __device__ uint64_t lb_resolve_wide(uint64_t *status, uint32_t tile, uint64_t ag
 //      under "lane -> owner of its landing point" hold every true record
 //      (pointer doubling);
 //   4. on-path lanes' word counts -> wave scan; they re-walk their true
-//      records to check the reference's error conditions and write, for
-//      every 4-word output block, the record covering it; all 64 lanes then
+//      records to check the reference's error conditions and mark, per
+//      record, the 4-word output block its first word falls in (ds_max);
+//      a prefix max hands every block its covering record; all 64 lanes then
 //      gather-expand the blocks (PackedInputStream.java:82-134 per word).
-// No barriers: up to 32 pieces in flight per CU.
+// No barriers: up to 28 pieces in flight per CU.
 constexpr int kDecThreads = 256;               // 4 independent waves
 #ifndef CPK_DEC_WPE
 #define CPK_DEC_WPE 8  // workgroups per CU the register budget is sized for
 #endif
 #ifndef CPK_DEC_CHUNK
-#define CPK_DEC_CHUNK 48
+#define CPK_DEC_CHUNK 56
 #endif
-// Lane chunks C of 48 bytes (3 KiB windows, 6 workgroups per CU by LDS):
-// measured against 28 / 32 / 64 at 131,072 pieces, 48 is fastest on configs
-// 2 and 3 (config 2 decode 5.07 -> 4.82 ms), 6 % slower on the sparse config 4
+// Lane chunks C of 56 bytes (3.5 KiB windows, 7 workgroups per CU by LDS):
+// measured against 40 / 48 / 60 / 64 at 131,072 pieces with the max-map
+// block map, 56 is fastest on configs 2-4 (against 48: 4.29 -> 4.13 ms,
+// 6.80 -> 6.51, 2.84 -> 2.80)
 constexpr uint32_t kDecChunk = CPK_DEC_CHUNK;
 constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per window
 constexpr uint32_t kWinBuf = (kWin + 15 + 32 + 16 + 15) & ~15u;  // + pad, look-ahead, slack
@@ -310,7 +312,7 @@ constexpr int kMapPer = kRound / kBlk / 64;  // map entries per lane in the fill
 static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 && kRound + 256 < (1 << 19)),
               "max-map entry: 12-bit window position, 19-bit output position");
 constexpr int kWinLinesPerLane = (int)((kWin + 47 + 15) / 16 + 63) / 64;
-constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;                // 15,616
+constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;  // 21,760 at 56-byte chunks
 
 __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
 #pragma unroll
