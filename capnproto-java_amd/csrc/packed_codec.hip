@@ -274,7 +274,8 @@ __device__ uint64_t lb_resolve_wide(uint64_t *status, uint32_t tile, uint64_t ag
 // No barriers: up to 28 pieces in flight per CU.
 constexpr int kDecThreads = 256;               // 4 independent waves
 #ifndef CPK_DEC_WPE
-#define CPK_DEC_WPE 8  // workgroups per CU the register budget is sized for
+#define CPK_DEC_WPE 7  // workgroups per CU the register budget is sized for (= the LDS limit:
+                       // 72 VGPRs; at 8 the stream form spilled, messages decode +10 %)
 #endif
 #ifndef CPK_DEC_CHUNK
 #define CPK_DEC_CHUNK 56

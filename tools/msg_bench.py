@@ -24,6 +24,8 @@ seg = rng.choice([w for w in (512, 1024, 2048, 4096, 8192, 16384, 32768) if w <=
 sizes = np.concatenate([np.full((nm, 1), 3, np.uint64), seg], axis=1).reshape(-1)
 swo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
 n = len(sizes)
+if os.environ.get("MB_LIB"):  # (A/B: a variant build of the library)
+    cp.load(Path(os.environ["MB_LIB"]), strict=False)
 ctx = cp.Context(0)
 d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
 d_in = torch.empty(int(swo[-1]) + 1, dtype=torch.int64, device="cuda")
