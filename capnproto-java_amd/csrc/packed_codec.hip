@@ -305,6 +305,10 @@ constexpr uint32_t kDecWaveLds = kWinBuf + (4 * (kRound / kBlk) > 64 * sizeof(Vi
 #ifndef CPK_DEC_MAXMAP
 #define CPK_DEC_MAXMAP 1
 #endif
+#ifndef CPK_DEC_LEANMAP
+#define CPK_DEC_LEANMAP 1  // a check-free block-map walk for windows no record of which can fail
+#endif
+static_assert(!CPK_DEC_LEANMAP || CPK_DEC_MAXMAP, "CPK_DEC_LEANMAP needs CPK_DEC_MAXMAP");
 // CPK_DEC_MAXMAP: a record marks only the block whose span ends at or after
 // its first word (ds_max of an entry ordered by output position), and a
 // prefix max over the blocks hands every block the last record starting at
@@ -594,6 +598,25 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
         wave_lds_order();
 #endif
         // after the first round only the lanes whose output meets this round
+#if CPK_DEC_LEANMAP
+        if (!(chk && rb == 0)) {
+          // no record here can fail or fill the piece: the map alone
+          if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
+            int rel = o0 - rb;  // round-relative output of the record (> -256 when live)
+            // (records past the round's last block start mark nothing, nor
+            // do the ones after them)
+            for (uint32_t q = entry; q < S && rel <= kRound - kBlk;) {
+              const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+              const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+              const int nw = 1 + (int)((zm & c1) + (fm & c9));
+              if (rel + nw > 0)
+                atomicMax(&blk[(max(rel, 0) + kBlk - 1) / kBlk], ((uint32_t)(rel + 256) << 12) | (q - e));
+              rel += nw;
+              q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
+            }
+          }
+        } else
+#endif
         if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
           int o = o0;
           for (uint32_t q = entry; q < S;) {

@@ -21,18 +21,18 @@ def oracle():
     return o
 
 
-@pytest.fixture(scope="module", params=[("5", "3"), ("0", "2")],
-                ids=["enc-auto+dec-auto", "enc-single-pass+dec-index"])
+@pytest.fixture(scope="module", params=[("5", "3"), ("0", "2"), ("4", "1")],
+                ids=["enc-auto+dec-auto", "enc-single-pass+dec-index", "enc-two-pass+dec-block-map"])
 def ctx(request):
     """A context per encoder / decoder pair (CPK_ENCODER, CPK_DECODER are read
     at context creation): every parity case runs through the default choice
     (the single pass for like-sized pieces of 1-8 Ki words, the two-pass
     encoder, encode_v4.hip, otherwise; the record-index decoder,
     decode_v2.hip, for sparse batches, the block-map decoder, decode_kernel,
-    otherwise), and through the single-pass encoder (encode_sp.hip) forced
-    for every batch with the record-index decoder forced.
-    tests/test_gpu_parity.py::test_every_encoder_matches_oracle forces the
-    two-pass encoder too."""
+    otherwise), through the single-pass encoder (encode_sp.hip) forced
+    for every batch with the record-index decoder forced, and through the
+    two-pass encoder with the block-map decoder forced (so sparse batches,
+    whose windows expand in several rounds, reach the block map too)."""
     import os
     import torch
     if not torch.cuda.is_available():
