@@ -88,3 +88,53 @@ def test_bench_messages_shape(ctx, oracle):
     assert int((d_mst != 0).sum().item()) == 0
     assert np.array_equal(d_sw.cpu().numpy().astype(np.uint64), swo)
     assert np.array_equal(d_out[:words].cpu().numpy().view(np.uint8), host)
+
+
+def test_sparse_messages_multi_round(ctx, oracle):
+    """Messages of sparse segments (config-4 data, ~90 % zero words, 4-256
+    KiB) through encode_messages / decode_messages: the stream-form decoder's
+    windows then hold more words than one expansion round (zero runs of up
+    to 256 words per 2-byte record), so later rounds and their block maps
+    are exercised; the packed bytes equal the oracle's Serialize.write and
+    the words come back."""
+    import torch
+    import capnp_packed as cp
+    rng = np.random.default_rng(44)
+    nm = 96
+    seg = rng.choice([512, 2048, 8192, 32768], size=(nm, 4)).astype(np.uint64)
+    swo = np.concatenate([[0], np.cumsum(seg.reshape(-1))]).astype(np.uint64)
+    mso = np.arange(0, 4 * nm + 1, 4, dtype=np.uint64)
+    nseg, words = 4 * nm, int(swo[-1])
+    d_swo, d_mso = _dev(swo), _dev(mso)
+    d_in = torch.empty(words + 1, dtype=torch.int64, device="cuda")
+    ctx.generate(cp.preset(4), d_swo, d_in)
+    cap = cp.batch_capacity(swo) + nm * 10 * 4
+    d_pk = torch.zeros((cap + 255) // 256 * 256, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(nm + nseg + 1, dtype=torch.int64, device="cuda")
+    ctx.encode_messages(d_in, d_swo, d_mso, 32768, d_pk, d_off)
+    torch.cuda.synchronize()
+    assert ctx.take_error() == 0
+    off = d_off.cpu().numpy().astype(np.uint64)
+    pk = d_pk[: int(off[-1])].cpu().numpy()
+    host = oracle.generate(oracle.preset(4), swo)
+    assert np.array_equal(d_in[:words].cpu().numpy().view(np.uint8), host)
+    expect = []
+    for m in range(nm):
+        segs = [host[8 * int(swo[s]): 8 * int(swo[s + 1])].tobytes() for s in range(4 * m, 4 * m + 4)]
+        expect.append(oracle.write_message(segs))
+    assert b"".join(expect) == pk.tobytes()
+    starts = np.concatenate([[0], np.cumsum([len(e) for e in expect])]).astype(np.uint64)
+    assert len(pk) < 0.2 * 8 * words  # sparse: windows of many words
+    d_moff = _dev(starts)
+    d_out = torch.empty(words + 1, dtype=torch.int64, device="cuda")
+    d_sw = torch.empty(nseg + 1, dtype=torch.int64, device="cuda")
+    d_si = torch.empty(nseg + 1, dtype=torch.int64, device="cuda")
+    d_ss = torch.empty(nseg, dtype=torch.int32, device="cuda")
+    d_ms = torch.empty(nm + 1, dtype=torch.int64, device="cuda")
+    d_mst = torch.empty(nm, dtype=torch.int32, device="cuda")
+    rc, tw, ts = ctx.decode_messages(d_pk, d_moff, d_out, d_sw, d_si, d_ss, d_ms, d_mst)
+    torch.cuda.synchronize()
+    assert rc == cp.OK and tw == words and ts == nseg
+    assert int((d_mst != 0).sum().item()) == 0 and int((d_ss != 0).sum().item()) == 0
+    assert np.array_equal(d_sw.cpu().numpy().astype(np.uint64), swo)
+    assert np.array_equal(d_out[:words].cpu().numpy().view(np.uint8), host)
