@@ -727,13 +727,23 @@ __device__ __forceinline__ SpSt sp_get_state(const uint64_t *scr, int par) {
   return s;
 }
 
+// (stats build: A1 alone into phase slot 7)
+#ifdef CPK_PHASE_STATS
+#define SP_A1_PARAMS , unsigned long long &wph_last, unsigned long long *wph_acc
+#define SP_A1_ARGS , wph_last, wph_acc
+#define SP_A1_STAMP WPH(7)
+#else
+#define SP_A1_PARAMS
+#define SP_A1_ARGS
+#define SP_A1_STAMP
+#endif
 // One chunk's A1 + A2 for this wave (all waves call it; two barriers).
 // Returns the chunk's packed bytes (all waves); wbefore: bytes of the waves
 // before this one.  cst: the state entering the chunk -> leaving it.
 __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restrict__ pw, uint32_t W,
                                              uint32_t c, uint64_t *msk, uint64_t *scr, SpSt &cst,
                                              int w, int lane, bool kEmit, int &cnt, uint32_t &Xlast,
-                                             uint64_t &wbefore, uint64_t &wmine) {
+                                             uint64_t &wbefore, uint64_t &wmine SP_A1_PARAMS) {
   const uint32_t ns = (W + 63) >> 6;
   const uint32_t cs0 = c * kSpCS;
   const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
@@ -746,6 +756,7 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
     acc = sp_a1(R, pw + wfirst, wrem, cnt, lane);
     sp_put_masks(R, msk, sa, cnt, lane);
   }
+  SP_A1_STAMP
   __syncthreads();  // the chunk's masks in LDS
   SpSt st = cst;
   uint32_t bytes = 0;
@@ -871,7 +882,7 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
         const bool emit = nch <= 1 || it >= nch;
         const uint32_t c = nch > 1 ? (emit ? it - nch : it) : 0;
         if (emit && c == 0) cst = SpSt{0u, 0u, 0u};
-        const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, cst, w, lane, emit, cnt, Xlast, wbefore, wmine);
+        const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, cst, w, lane, emit, cnt, Xlast, wbefore, wmine SP_A1_ARGS);
         WPH(1)
         if (!emit) {
           total += ct;

@@ -33,9 +33,9 @@ L.cpk_debug_phase_stats(buf.ctypes.data)
 ctx.encode_batch(d_in, d_swo, 8192, d_pk, d_off)
 torch.cuda.synchronize()
 L.cpk_debug_phase_stats(buf.ctypes.data)
-names = ["ticket + barriers", "A1 + A2 (+2 barriers)", "look-back + barrier", "loop top", "B emit",
-         "B: look-back (wave 0)", "B: wait for offset (waves 1-3)"]
-v = buf[32:39].astype(float)
+names = ["ticket + barriers", "barrier + A2 + barrier", "look-back + barrier", "loop top", "B emit",
+         "B: look-back (wave 0)", "B: wait for offset (waves 1-3)", "A1 (loads, tags, ballots)"]
+v = buf[32:40].astype(float)
 tot = v.sum()
 print(f"sp_encode config {cfg}: {tot / 1e6:.1f} Mcycles over all waves; per piece per wave {tot / n / 4:.0f} cyc")
 for nm, x in zip(names, v):
