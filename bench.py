@@ -311,8 +311,10 @@ def run_rank(args, rank, world, local):
         except (ValueError, KeyError, TypeError, AttributeError):
             pass
 
+    # (rank 0 at N = 1 only: at N > 1 the other ranks would wait on it and
+    # the host cores are shared by all ranks)
     cpu = None
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:
         cpu = cpu_baseline(args, params)
 
     if mso is None:

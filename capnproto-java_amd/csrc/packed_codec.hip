@@ -316,6 +316,14 @@ static_assert(!CPK_DEC_LEANMAP || CPK_DEC_MAXMAP, "CPK_DEC_LEANMAP needs CPK_DEC
 constexpr int kMapPer = kRound / kBlk / 64;  // map entries per lane in the fill
 static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 && kRound + 256 < (1 << 19)),
               "max-map entry: 12-bit window position, 19-bit output position");
+#ifndef CPK_DEC_HOIST_CNT
+#define CPK_DEC_HOIST_CNT 0
+#endif
+#ifndef CPK_DEC_CHK_REACH
+#define CPK_DEC_CHK_REACH (kWin + 2064)
+#endif
+constexpr uint32_t kDecChkReach = CPK_DEC_CHK_REACH;
+static_assert(kDecChkReach >= kWin + 2050, "a window's last record must fall inside the checked reach");
 constexpr int kWinLinesPerLane = (int)((kWin + 47 + 15) / 16 + 63) / 64;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;  // 21,760 at 56-byte chunks
 
@@ -588,7 +596,9 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
       // errors and the filling record can only occur in a window reaching the
       // piece's last word or within one window plus one record of its end
-      const bool chk = (ow + T >= W) || (P - e < 3 * kWin);
+      // (the window's records start before e + kWin; the longest record, a
+      // 0xFF tag with its word, count and 255 words, is 2,050 bytes)
+      const bool chk = (ow + T >= W) || (P - e < kDecChkReach);
       for (int rb = 0; rb < T; rb += kRound) {
         int err = 0x7fffffff;
 #if CPK_DEC_MAXMAP
@@ -703,7 +713,12 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
             // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
             // run (tag word, then the counted words), or a tagged word
             // (the count bytes are read with the tag: one LDS round trip)
-            const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+            uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+#if CPK_DEC_HOIST_CNT
+            // the count bytes with the tag (one LDS round trip), not sunk
+            // into the zero / 0xFF branches
+            asm volatile("" : "+v"(tag), "+v"(c1), "+v"(c9));
+#endif
             uint64_t x;
             int nw;
             uint32_t adv;
