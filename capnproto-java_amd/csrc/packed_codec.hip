@@ -309,6 +309,10 @@ constexpr uint32_t kDecWaveLds = kWinBuf + (4 * (kRound / kBlk) > 64 * sizeof(Vi
 #define CPK_DEC_LEANMAP 1  // a check-free block-map walk for windows no record of which can fail
 #endif
 static_assert(!CPK_DEC_LEANMAP || CPK_DEC_MAXMAP, "CPK_DEC_LEANMAP needs CPK_DEC_MAXMAP");
+#ifndef CPK_DEC_TRACKCHK
+#define CPK_DEC_TRACKCHK 1  // windows near the piece's end check only the two records that can fail
+#endif
+static_assert(!CPK_DEC_TRACKCHK || CPK_DEC_LEANMAP, "CPK_DEC_TRACKCHK needs CPK_DEC_LEANMAP");
 // CPK_DEC_MAXMAP: a record marks only the block whose span ends at or after
 // its first word (ds_max of an entry ordered by output position), and a
 // prefix max over the blocks hands every block the last record starting at
@@ -626,6 +630,65 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
             }
           }
         } else
+#endif
+#if CPK_DEC_TRACKCHK
+        {
+          // round 0 of a window near the piece's end.  Only two records can
+          // fail or fill the piece: the one whose words reach word W (when the
+          // window gets there; the reference stops reading after it), else the
+          // window's last record (the only one whose bytes can pass P: every
+          // other record ends where the next begins, before wend <= P).  The
+          // map walk notes them; one lane then runs the reference's checks
+          // on its record (PackedInputStream.java:53-138).
+          uint32_t qc = 0xffffffffu;
+          int oc = 0;
+          if (on) {
+            const int wr = W - ow;  // words left in the piece (> 0)
+            uint32_t ql = entry;
+            int o = o0, ol = o0;
+            for (uint32_t q = entry; q < S;) {
+              const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+              const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+              const int nw = 1 + (int)((zm & c1) + (fm & c9));
+              const int idx = (o + kBlk - 1) / kBlk;  // (round 0: o >= 0)
+              if (idx < kRound / kBlk) atomicMax(&blk[idx], ((uint32_t)(o + 256) << 12) | (q - e));
+              if (o < wr && o + nw >= wr) {
+                qc = q;
+                oc = o;
+              }
+              ql = q;
+              ol = o;
+              o += nw;
+              q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
+            }
+            if (ow + T < W && lane == 63 - __builtin_clzll(onmask)) {
+              qc = ql;
+              oc = ol;
+            }
+          }
+          if (qc != 0xffffffffu) {
+            const uint32_t q = qc;
+            const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+            const uint32_t ntag = 1 + __builtin_popcount(tag);
+            const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+            const int nw = 1 + (int)((zm & c1) + (fm & c9));
+            const uint32_t adv = ntag + (zm & 1u) + (fm & (8u * c9 + 1u));
+            const int oo = ow + oc;
+            // truncated tag bytes / count / literal run -> EOF DecodeException;
+            // run past the piece -> DecodeException / BufferOverflowException
+            int code = 0;
+            if (q + ntag > P) code = 2;
+            else if (tag == 0 || tag == 0xffu) {
+              if (q + (tag ? 10u : 2u) > P) code = 2;
+              else if (oo + nw > W) code = 3;
+              else if (q + adv > P) code = 2;
+            }
+            if (!kStream && !code && oo + nw == W && q + adv < P) code = 4;
+            if (code) err = (int)(((q - e) << 3) | (uint32_t)code);
+            if (oo + nw == W) fin = q + adv;
+          }
+        }
+        if (false)
 #endif
         if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
           int o = o0;

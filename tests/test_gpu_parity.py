@@ -178,6 +178,53 @@ def test_malformed_streams_match_reference_errors(ctx, oracle):
             assert dec[8 * int(swo[i]): 8 * int(swo[i + 1])].tobytes() == out
 
 
+def test_malformed_long_pieces_match_reference_errors(ctx, oracle):
+    """Multi-window pieces (up to 8192 words, up to ~80 KB packed) corrupted
+    anywhere, and pieces ending in a 255-word literal run (a 2,050-byte
+    record) cut short by every distance up to and past that record: the
+    decoder checks errors only in windows within one window plus one record
+    of the piece's end or reaching its last word, so the statuses must still
+    equal the oracle's wherever the damage lies."""
+    rng = np.random.default_rng(23)
+    cases = []
+    for k in range(120):
+        n = int(rng.integers(600, 8193))
+        probs = [[.3, .3, .2, .2], [.02, .6, .37, .01], [.05, .0, .0, .95]][k % 3]
+        u = _random_words(rng, n, probs).tobytes()
+        p = bytearray(oracle.pack(u))
+        r = k % 4
+        if r == 0:
+            p = p[: int(rng.integers(max(0, len(p) - 6000), len(p)))]          # truncate near the end
+        elif r == 1:
+            p += bytes(rng.integers(0, 256, size=int(rng.integers(1, 40)), dtype=np.uint8))
+        elif r == 2:
+            for _ in range(int(rng.integers(1, 4))):
+                i = int(rng.integers(0, len(p)))
+                p[i] = int(rng.integers(0, 256))                               # flip anywhere
+        else:
+            n = max(1, n + int(rng.integers(-300, 301)))                       # wrong piece size
+        cases.append((bytes(p), n))
+    # a tail of 255 all-nonzero words after mixed words: its 0xFF record is
+    # the piece's last, 2,050 bytes long; cut it by 1 .. 2,100 bytes
+    for cut in (1, 2, 7, 8, 9, 10, 11, 100, 1000, 2040, 2049, 2050, 2051, 2100):
+        head = _random_words(rng, 3000, [.3, .3, .2, .2]).tobytes()
+        tail = rng.integers(1, 256, size=8 * 256, dtype=np.uint8).tobytes()
+        p = oracle.pack(head + tail)
+        cases.append((p[: len(p) - cut], 3256))
+        cases.append((p, 3256 - int(rng.integers(1, 300))))                   # run past the piece
+    packed = b"".join(p for p, _ in cases)
+    in_off = _swo([len(p) for p, _ in cases])
+    swo = _swo([n for _, n in cases])
+    dec, st = ctx.decode_host(np.frombuffer(packed, np.uint8), in_off, swo)
+    for i, (p, n) in enumerate(cases):
+        ost, out, used = oracle.unpack(p, 8 * n)
+        if ost == oracle.OK and used != len(p):
+            ost = oracle.ETRAILING
+        assert st[i] == ost, (i, len(p), n, st[i], ost)
+        if ost == oracle.OK:
+            assert dec[8 * int(swo[i]): 8 * int(swo[i + 1])].tobytes() == out
+
+
 def test_serialize_packed_message(ctx, oracle):
     """SerializePacked.write = pack(table) || pack(seg0) || ... (Serialize.java
     :256-288): the table is one more piece of the batch."""
