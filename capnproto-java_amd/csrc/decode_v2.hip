@@ -265,7 +265,9 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
       // ---- 5: the index: each true record's window position and first word ----
       // (the reference's error checks run in a window that may reach the
       // piece's end: PackedInputStream.java:53-138)
-      const bool chk = (ow + T >= W) || (P - e < 3 * kD2Win);
+      // (within one window plus the longest record, 2,050 bytes, of the end:
+      // the window's records start before e + kD2Win)
+      const bool chk = (ow + T >= W) || (P - e < kD2Win + 2064);
       // a window with more true records than the index holds ends at its
       // kD2NI-th record (scr: that record's position and first word)
       const bool cut = NR > (int)kD2NI;
@@ -327,6 +329,10 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
       const uint32_t Tlim = min(Teff, (uint32_t)(W - ow));
       uint64_t *dst_w = dst + ow;
       uint32_t ia = 0;  // the record covering the round's first word
+      // two copies of the expansion: one for windows whose records all lie in
+      // the loaded bytes (eff_next + 12 <= lend), with unchecked reads
+      auto expand = [&](auto allin) __attribute__((always_inline)) {
+      constexpr bool kAllIn = decltype(allin)::value;
       for (uint32_t rb = 0; rb < Tlim; rb += kD2Round) {
         const uint32_t re = min(rb + kD2Round, Tlim);
         // the round's record starts after its first word
@@ -378,7 +384,7 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
             const uint32_t tag = pkw[q];
             // the word's bytes: after the tag, or the literal run's ofs-th word
             const uint32_t src = q + 1 + ((tag == 0xffu && ofs) ? 1u + 8u * ofs : 0u);
-            const uint64_t raw = read8(pkw, src, lend, gp, glim, ph, e);
+            const uint64_t raw = read8<kAllIn>(pkw, src, lend, gp, glim, ph, e);
             const uint64_t sel = lut[tag];
             const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
             const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
@@ -391,6 +397,12 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
         ia = ob == rb + kD2Round ? ib : ib - 1;
         wave_lds_order();  // bits / info reused
       }
+      };
+#if CPK_DEC_ALLIN
+      if (eff_next + 12 <= lend) expand(std::true_type{});
+      else
+#endif
+        expand(std::false_type{});
       WPH(6)
       if (ow + (int)Teff >= W && fin) {  // the piece is full: next piece starts at fin
         ow = W;

@@ -320,6 +320,9 @@ static_assert(!CPK_DEC_TRACKCHK || CPK_DEC_LEANMAP, "CPK_DEC_TRACKCHK needs CPK_
 constexpr int kMapPer = kRound / kBlk / 64;  // map entries per lane in the fill
 static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 && kRound + 256 < (1 << 19)),
               "max-map entry: 12-bit window position, 19-bit output position");
+#ifndef CPK_DEC_ALLIN
+#define CPK_DEC_ALLIN 1  // an expansion without bound checks for windows whose records are all loaded
+#endif
 #ifndef CPK_DEC_HOIST_CNT
 #define CPK_DEC_HOIST_CNT 0
 #endif
@@ -360,6 +363,9 @@ __device__ __forceinline__ DecRec rec_at(const uint8_t *pkw, uint32_t q) {
 
 // 8 bytes at piece position x: from the LDS window when loaded, otherwise
 // (tail of a literal run reaching past the window) straight from memory
+// (kAllIn: the caller knows x + 12 <= lend -- every record of the window
+// lies in the loaded bytes -- so no check and no memory path)
+template <bool kAllIn = false>
 __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32_t lend,
                                          const uint8_t *gpiece, uint32_t glim, uint32_t ph,
                                          uint32_t e) {
@@ -368,12 +374,12 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
   // both reads under one branch hipcc merged them into flat loads.
   // LDS-aligned dwords: piece position x sits at byte phase (x + ph) & 3 of
   // the 16-byte aligned window buffer.
-  const bool inw = x + 12 <= lend;
+  const bool inw = kAllIn || x + 12 <= lend;
   const uint32_t xl = inw ? x : e;
   uint32_t sh = (xl + ph) & 3;
   const uint32_t *pl = reinterpret_cast<const uint32_t *>(pkw + ((int64_t)xl - sh));  // (signed: xl < sh)
   uint32_t d0 = pl[0], d1 = pl[1], d2 = pl[2];
-  if (!inw) {
+  if (!kAllIn && !inw) {
     // address-aligned dwords of the packed buffer, none at or past the
     // readable limit glim (piece-relative: the piece's end rounded up to a
     // 16-byte line; bytes there are never part of a valid record)
@@ -760,6 +766,11 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
 #endif
         WPH(5)
         const int nb = (min(min(kRound, T - rb), W - ow - rb) + kBlk - 1) / kBlk;
+        // two copies of the expansion: one for windows whose records all lie
+        // in the loaded bytes (enext + 12 <= lend: the usual case), whose
+        // reads need no bound check and no memory path
+        auto expand = [&](auto allin) __attribute__((always_inline)) {
+        constexpr bool kAllIn = decltype(allin)::value;
         for (int b = lane; b < nb; b += 64) {
           const uint32_t v = blk[b];
 #if CPK_DEC_MAXMAP
@@ -793,9 +804,9 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
               const uint32_t rn = c9;
               nw = 1 + (int)rn;
               adv = 10 + 8 * rn;
-              x = read8(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
+              x = read8<kAllIn>(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
             } else {
-              const uint64_t raw = read8(pkw, q + 1, lend, gp, glim, ph, e);
+              const uint64_t raw = read8<kAllIn>(pkw, q + 1, lend, gp, glim, ph, e);
               const uint64_t sel = lut[tag];
               const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
               const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
@@ -829,6 +840,12 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
               if (i < kw) d[i] = words[i];
           }
         }
+        };
+#if CPK_DEC_ALLIN
+        if (enext + 12 <= lend) expand(std::true_type{});
+        else
+#endif
+          expand(std::false_type{});
         wave_lds_order();  // blk reused by the next round
         WPH(6)
       }
