@@ -57,6 +57,9 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #else
 #define CPK_SP_STEP_FENCE()
 #endif
+#ifndef CPK_SP_A1FULL
+#define CPK_SP_A1FULL 1
+#endif
 #ifndef CPK_SP_WPE
 #define CPK_SP_WPE 3  // waves per SIMD the registers must allow (3 workgroups per CU)
 #endif
@@ -244,19 +247,25 @@ struct SpRegs {
 
 // A1: the wave's cnt steps at src (wrem piece words from src on); returns
 // this lane's nonzero-byte count
+// kFull: the wave holds kSpWS whole steps -- straight-line code, so each
+// step waits only for its own load (vmcnt(kSpWS - 1 - j)); with the per-step
+// branches of the general form the compiler waits for all of them at the
+// first step
+template <bool kFull>
 __device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict__ src, uint32_t wrem,
                                           int cnt, int lane) {
   // loads clamped to the piece, not predicated: step j's lanes read
   // min(lane, last valid lane of the step) (one lane register for all steps)
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j)
-    if (j < cnt) R.v[j] = (src + j * 64)[min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))];
+    if (kFull || j < cnt)
+      R.v[j] = (src + j * 64)[kFull ? (uint32_t)lane : min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))];
   uint32_t acc = 0;
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j) {
-    if (j < cnt) {
+    if (kFull || j < cnt) {
       // (lane vs a scalar bound: no per-step lane constants kept in registers)
-      const bool valid = (uint32_t)lane < wrem - 64u * j;
+      const bool valid = kFull || (uint32_t)lane < wrem - 64u * j;
       const uint32_t m = valid ? e4_tag(R.v[j]) : 0u;
       if (j & 3) R.mp[j >> 2] |= m << (8 * (j & 3));
       else R.mp[j >> 2] = m;
@@ -753,7 +762,11 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   const uint32_t wrem = cnt ? W - wfirst : 0;
   uint32_t acc = 0;
   if (cnt) {
-    acc = sp_a1(R, pw + wfirst, wrem, cnt, lane);
+#if CPK_SP_A1FULL
+    if (cnt == kSpWS && wrem >= 64u * kSpWS) acc = sp_a1<true>(R, pw + wfirst, wrem, cnt, lane);
+    else
+#endif
+      acc = sp_a1<false>(R, pw + wfirst, wrem, cnt, lane);
     sp_put_masks(R, msk, sa, cnt, lane);
   }
   SP_A1_STAMP
