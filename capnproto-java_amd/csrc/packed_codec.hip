@@ -286,7 +286,12 @@ constexpr int kDecThreads = 256;               // 4 independent waves
 // 6.80 -> 6.51, 2.84 -> 2.80)
 constexpr uint32_t kDecChunk = CPK_DEC_CHUNK;
 constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per window
-constexpr uint32_t kWinBuf = (kWin + 15 + 32 + 16 + 15) & ~15u;  // + pad, look-ahead, slack
+#ifndef CPK_DEC_LOOK
+#define CPK_DEC_LOOK 240  // bytes loaded past the window (a literal run reaching past them is read from memory;
+                         // 240: config 3 decode -4.5 % against 32, config 2 neutral; 368 costs occupancy)
+#endif
+constexpr uint32_t kDecLook = CPK_DEC_LOOK;
+constexpr uint32_t kWinBuf = (kWin + 15 + kDecLook + 16 + 15) & ~15u;  // + pad, look-ahead, slack
 #ifndef CPK_DEC_ROUND
 #define CPK_DEC_ROUND 1280  // (8 workgroups per CU with 48-byte chunks; larger rounds cost occupancy)
 #endif
@@ -331,7 +336,7 @@ static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 
 #endif
 constexpr uint32_t kDecChkReach = CPK_DEC_CHK_REACH;
 static_assert(kDecChkReach >= kWin + 2050, "a window's last record must fall inside the checked reach");
-constexpr int kWinLinesPerLane = (int)((kWin + 47 + 15) / 16 + 63) / 64;
+constexpr int kWinLinesPerLane = (int)((kWin + 15 + kDecLook + 15) / 16 + 63) / 64;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;  // 21,760 at 56-byte chunks
 
 __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
@@ -499,7 +504,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
       // ---- window load: LDS byte x <-> packed[(a + e) & ~15 + x] ----------
       const uint32_t padw = (uint32_t)((a + e) & 15);
       const uint32_t ebase = e - padw;  // piece position of wbuf[0]
-      const uint32_t need = min(e + kWin + 32, P) - ebase;  // <= kWin + 47 bytes
+      const uint32_t need = min(e + kWin + kDecLook, P) - ebase;  // <= kWin + kDecLook + 15 bytes
       const uint32_t lines = (need + 15) >> 4;
       const uint4 *gsrc = reinterpret_cast<const uint4 *>(gp - padw + e);
       // all of a lane's lines (<= 3) in flight at once, then the LDS writes:
