@@ -57,6 +57,9 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #else
 #define CPK_SP_STEP_FENCE()
 #endif
+#ifndef CPK_SP_FLUSH_UNCOND
+#define CPK_SP_FLUSH_UNCOND 1
+#endif
 #ifndef CPK_SP_A1FULL
 #define CPK_SP_A1FULL 1
 #endif
@@ -505,8 +508,15 @@ __device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t 
   }
   for (uint32_t t0 = ft; t0 < upto; t0 += 64) {
     const uint32_t t = t0 + (uint32_t)lane;
+#if CPK_SP_FLUSH_UNCOND
+    // every lane builds a line (ring indices wrap: lanes past upto read
+    // harmless lines): the shift's switch on the uniform k stays a scalar
+    // branch instead of an exec-masked one inside the lane condition
+    const uint4 v = sp_gline(ring, t, k);
+#else
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (t < upto) v = sp_gline(ring, t, k);
+#endif
     wave_lds_order();
     if (t < upto) {
       if ((L0 + t) * 16 + 16 <= ocap) *reinterpret_cast<uint4 *>(out + (L0 + t) * 16) = v;
@@ -861,6 +871,7 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     const uint64_t pfirst = (uint64_t)t * ppt;
     WPH(0)
     if (pfirst >= n) break;
+
     const uint32_t plast = (uint32_t)min(pfirst + ppt, (uint64_t)n);
     for (uint32_t p = (uint32_t)pfirst; p < plast; ++p) {
       // an opaque copy of the lane id: nothing lane-dependent is hoisted out
