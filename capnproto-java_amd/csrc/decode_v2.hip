@@ -141,6 +141,10 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
     int ow = 0;      // output words produced
     if (W == 0) st = (P == 0 || kStream) ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
     while (W != 0) {
+#if CPK_DEC_UNI
+      e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);  // (wave-uniform: SGPRs, scalar branches)
+      ow = __builtin_amdgcn_readfirstlane(ow);
+#endif
       if (e >= P) {
         if (ow < W) st = CPK_ETRUNC;  // ArrayInputStream EOF -> DecodeException
         break;

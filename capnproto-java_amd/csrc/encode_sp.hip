@@ -57,6 +57,9 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #else
 #define CPK_SP_STEP_FENCE()
 #endif
+#ifndef CPK_SP_UNI_BASE
+#define CPK_SP_UNI_BASE 1
+#endif
 #ifndef CPK_SP_FLUSH_UNCOND
 #define CPK_SP_FLUSH_UNCOND 1
 #endif
@@ -548,6 +551,12 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
                                      bool known, bool fits, uint64_t g0, int lane, uint64_t ocap,
                                      GetBase getbase) {
   uint32_t rel = 0, ft = 0;
+#if CPK_SP_UNI_BASE
+  // the output offset is wave-uniform: say so (readfirstlane), or the flush
+  // condition and the line shift's switch on g0 & 15 compile to exec-masked
+  // branches
+  g0 = sp_uni(g0);
+#endif
   const uint32_t l64 = 64u - (uint32_t)lane;
   // step j's string per lane (s0..s2, nb bytes)
   auto strings = [&](const int j, uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &nb)
@@ -635,12 +644,18 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     if (j < cnt) step(j);
   if (!known && !fits && cnt > kSpDefer) {
     g0 = getbase();
+#if CPK_SP_UNI_BASE
+    g0 = sp_uni(g0);
+#endif
     known = true;
   }
 #pragma unroll
   for (int j = kSpDefer; j < kSpWS; j += 2)
     if (j < cnt) step(j);
   if (!known) g0 = getbase();
+#if CPK_SP_UNI_BASE
+  g0 = sp_uni(g0);
+#endif
   wave_lds_order();
   const uint32_t k = (uint32_t)(g0 & 15);
   const uint32_t done = (k + rel) >> 4;

@@ -325,6 +325,9 @@ static_assert(!CPK_DEC_TRACKCHK || CPK_DEC_LEANMAP, "CPK_DEC_TRACKCHK needs CPK_
 constexpr int kMapPer = kRound / kBlk / 64;  // map entries per lane in the fill
 static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 && kRound + 256 < (1 << 19)),
               "max-map entry: 12-bit window position, 19-bit output position");
+#ifndef CPK_DEC_UNI
+#define CPK_DEC_UNI 1
+#endif
 #ifndef CPK_DEC_ALLIN
 #define CPK_DEC_ALLIN 1  // an expansion without bound checks for windows whose records are all loaded
 #endif
@@ -494,6 +497,13 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
     int ow = 0;      // output words produced
     if (W == 0) st = (P == 0 || kStream) ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
     while (W != 0) {
+#if CPK_DEC_UNI
+      // the window's start and the words so far are wave-uniform: say so
+      // (the loop's exits made the compiler keep them in VGPRs and run the
+      // window's uniform branches under exec masks)
+      e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
+      ow = __builtin_amdgcn_readfirstlane(ow);
+#endif
       if (e >= P) {
         if (ow < W) st = CPK_ETRUNC;  // ArrayInputStream EOF -> DecodeException
         break;
