@@ -141,6 +141,16 @@ __device__ unsigned long long g_phase[64];
 #define WPH_FLUSH(base)
 #endif
 
+// floor(r / C) for window positions (r < 2^13) by a full-rate 24-bit
+// multiply and a shift (the compiler's division by a constant is a
+// quarter-rate v_mul_hi_u32 + v_mad_u64_u32 pair, in the landing walk's loop)
+template <uint32_t C>
+__device__ __forceinline__ uint32_t chunk_div(uint32_t r) {
+  constexpr uint32_t kM = ((1u << 20) + C - 1) / C;
+  static_assert((kM * C - (1u << 20)) * (1u << 13) < (1u << 20), "exact for r < 2^13");
+  return __umul24(r, kM) >> 20;
+}
+
 // nonzero-byte mask of a 32-bit half: bit b set iff byte b != 0
 __device__ __forceinline__ uint32_t nzmask4(uint32_t d) {
   uint32_t t = (((d & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d) & 0x80808080u;
@@ -562,8 +572,10 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
       if (cb < wend) {
         while (S < wend) {
           const uint32_t r = S - e;
-          const uint32_t ow_ = r / kDecChunk;
-          if ((visa[ow_] >> (r - ow_ * kDecChunk)) & 1) break;
+          const uint32_t ow_ = chunk_div<kDecChunk>(r);
+          uint32_t base = __umul24(ow_, kDecChunk);
+          asm("" : "+v"(base));  // (else folded into a quarter-rate v_mad_u64_u32)
+          if ((visa[ow_] >> (r - base)) & 1) break;
           const DecRec rr = rec_at(pkw, S);
           lw += rr.nw;
           S += rr.len;
@@ -574,7 +586,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
       // lane j's successor is the owner of its landing point (always a later
       // lane); the true records are on the lanes reachable from lane 0, found
       // by pointer doubling (6 rounds cover a chain of 64)
-      int nx = (cb < wend && S < wend) ? (int)((S - e) / kDecChunk) : 64;
+      int nx = (cb < wend && S < wend) ? (int)chunk_div<kDecChunk>(S - e) : 64;
       uint64_t R = 1ull << lane;
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
@@ -593,7 +605,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
           (uint32_t)__builtin_amdgcn_readlane((int)S, 63 - __builtin_clzll(onmask));
       // each on-path lane hands its landing point to its successor
       wave_lds_order();  // (phase 2's reads of visa are done)
-      if (((onmask >> lane) & 1) && S < wend) visa[(S - e) / kDecChunk] = (VisMask)S;
+      if (((onmask >> lane) & 1) && S < wend) visa[chunk_div<kDecChunk>(S - e)] = (VisMask)S;
       wave_lds_order();
       const uint32_t entry = lane == 0 ? e : (uint32_t)visa[lane];
       const bool on = (onmask >> lane) & 1;
