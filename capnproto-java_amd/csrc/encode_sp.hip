@@ -57,6 +57,9 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #else
 #define CPK_SP_STEP_FENCE()
 #endif
+#ifndef CPK_SP_PUT_PERM
+#define CPK_SP_PUT_PERM 1
+#endif
 #ifndef CPK_SP_UNI_BASE
 #define CPK_SP_UNI_BASE 1
 #endif
@@ -100,6 +103,12 @@ __device__ __forceinline__ uint64_t sp_rl(uint32_t lo, uint32_t hi, int j) {
 extern "C" __device__ int cpk_llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
 __device__ __forceinline__ uint32_t sp_wl(uint32_t old, uint32_t v, int j) {
   return (uint32_t)cpk_llvm_writelane((int)v, j, (int)old);
+}
+// index of the lowest set bit, 0xffffffff for 0 (v_ffbl_b32)
+__device__ __forceinline__ uint32_t sp_ffbl(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
 }
 // per lane: mask bit set ? b : a (one v_cndmask on the SGPR mask)
 __device__ __forceinline__ uint32_t sp_sel(uint32_t a, uint32_t b, uint64_t mask) {
@@ -574,12 +583,11 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
       const uint32_t X = (uint32_t)__builtin_amdgcn_readlane((int)R.ox, j);
       const uint64_t E = sp_rl(R.oel, R.oeh, j);
       const uint64_t e = E >> lane;
-      // ctz of e, 0xffffffff when e == 0 (the next run end is past the step)
-      const uint32_t z_lo = (uint32_t)e ? (uint32_t)__builtin_ctz((uint32_t)e) : 0xffffffffu;
-      const uint32_t z_hi = (uint32_t)(e >> 32) ? (uint32_t)__builtin_ctz((uint32_t)(e >> 32)) + 32u
-                                                : 0xffffffffu;
-      uint32_t tt = min(min(z_lo, z_hi), l64 + X);
-      tt = min(tt, 255u);
+      // ctz of e, 0xffffffff when e == 0 (the next run end is past the step):
+      // v_ffbl_b32 gives 0xffffffff for 0 itself (no compare / select)
+      const uint32_t z_lo = sp_ffbl((uint32_t)e);
+      const uint32_t z_hi = sp_ffbl((uint32_t)(e >> 32)) | 32u;  // (ctz < 32: | is +)
+      const uint32_t tt = min(min(z_lo, z_hi), min(l64 + X, 255u));
       const uint32_t cn = sp_sel(0u, tt, HC);
       cz = m == 0 ? cn : 0u;
       cd = cn - cz;
@@ -599,15 +607,25 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
   };
   // a string OR-ed into the ring at relative byte p
   auto put = [&](uint32_t p, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t nb) __attribute__((always_inline)) {
+#if CPK_SP_PUT_PERM
+    // the string shifted left by p & 3 bytes over four dwords: one v_perm
+    // each, selector bytes [4 - b, 8 - b) of (s_k : s_k-1)
+    const uint32_t b = p & 3;
+    const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, b, 0u);  // (b in every byte)
+    const uint32_t d0 = __builtin_amdgcn_perm(s0, 0u, sel), d1 = __builtin_amdgcn_perm(s1, s0, sel);
+    const uint32_t d2 = __builtin_amdgcn_perm(s2, s1, sel), d3 = __builtin_amdgcn_perm(0u, s2, sel);
+#else
     const uint32_t sh = (p & 3) * 8;
     const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
     const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
+    const uint32_t d0 = (uint32_t)a01, d1 = (uint32_t)(a01 >> 32), d2 = (uint32_t)(a12 >> 32);
     const uint32_t d3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
+#endif
     uint32_t *rp = ring + ((p >> 2) & (kSpRing / 4 - 1));
     if (nb) {  // (zero-length strings would all hit one address)
-      atomicOr(rp, (uint32_t)a01);
-      atomicOr(rp + 1, (uint32_t)(a01 >> 32));
-      atomicOr(rp + 2, (uint32_t)(a12 >> 32));
+      atomicOr(rp, d0);
+      atomicOr(rp + 1, d1);
+      atomicOr(rp + 2, d2);
       atomicOr(rp + 3, d3);
     }
   };
