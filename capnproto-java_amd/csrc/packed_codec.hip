@@ -338,6 +338,9 @@ static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 
 #ifndef CPK_DEC_UNI
 #define CPK_DEC_UNI 1
 #endif
+#ifndef CPK_DEC_MAP0
+#define CPK_DEC_MAP0 1  // a check-free round-0 map walk (no past-the-round-start test)
+#endif
 #ifndef CPK_DEC_ALLIN
 #define CPK_DEC_ALLIN 1  // an expansion without bound checks for windows whose records are all loaded
 #endif
@@ -648,6 +651,22 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
 #if CPK_DEC_LEANMAP
         if (!(chk && rb == 0)) {
           // no record here can fail or fill the piece: the map alone
+#if CPK_DEC_MAP0
+          if (rb == 0) {
+            // round 0 (usually the window's only one): every record's output
+            // is at or past the round's start, so it always marks a block
+            if (on) {
+              uint32_t rel = (uint32_t)o0;
+              for (uint32_t q = entry; q < S && rel <= (uint32_t)(kRound - kBlk);) {
+                const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+                const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+                atomicMax(&blk[(rel + kBlk - 1) / kBlk], ((rel + 256u) << 12) | (q - e));
+                rel += 1u + (zm & c1) + (fm & c9);
+                q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
+              }
+            }
+          } else
+#endif
           if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
             int rel = o0 - rb;  // round-relative output of the record (> -256 when live)
             // (records past the round's last block start mark nothing, nor
