@@ -827,6 +827,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
           int ofs = (int)(v >> 16);
 #endif
           const int wbase = ow + rb + kBlk * b;  // piece word of the block's first word
+          const int wleft = ow + T - wbase - 1;   // words of the window after the block's first
           uint64_t words[kBlk];
 #pragma unroll
           for (int i = 0; i < kBlk; ++i) {
@@ -863,7 +864,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
             }
             words[i] = x;
             // past the window's last word: stay put (never stored)
-            if (++ofs == nw && wbase + i + 1 < ow + T) {
+            if (++ofs == nw && i < wleft) {
               q += adv;
               ofs = 0;
             }
