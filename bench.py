@@ -24,6 +24,9 @@ Run:  python bench.py [--gpus N --steps K --warmup W --config C]
   itself (before any GPU call); under torchrun WORLD_SIZE must equal N.
   --stub: CPU-only rehearsal of the multi-rank path (gloo, the oracle as
   the "kernel"), used by tests/test_shard.py.
+  --same-device: every rank on cuda:0 with a gloo group (RCCL refuses two
+  ranks on one GPU): the real GPU rank path at N > 1 on a one-GPU box
+  (tests/test_gpu_bench_shapes.py); use a small --segments so the shards fit.
 """
 from __future__ import annotations
 
@@ -62,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--sample-check", type=int, default=64,
                     help="pieces re-packed on the host oracle and compared")
     ap.add_argument("--stub", action="store_true", help="CPU rehearsal (gloo, no GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="all ranks on cuda:0, gloo group (N > 1 rehearsal on one GPU)")
     return ap.parse_args(argv)
 
 
@@ -128,10 +133,15 @@ def run_rank(args, rank, world, local):
     import capnp_packed as cp
 
     dist = None
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.same_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     ctx = cp.Context(local)
 
@@ -266,7 +276,10 @@ def run_rank(args, rank, world, local):
         wall, enc_ms, dec_ms = mx[0], mx[1], mx[2]
         errors = int(sm[3])
         P_total, U_total = sm[4], sm[5]
-        per_rank = {"encode_ms_max": round(mx[1], 4), "decode_ms_max": round(mx[2], 4)}
+        per_rank = {"encode_ms_max": round(mx[1], 4), "decode_ms_max": round(mx[2], 4),
+                    "wall_s_max": round(mx[0], 4), "unpacked_bytes_total": int(U_total),
+                    "packed_bytes_total": int(P_total),
+                    "backend": dist.get_backend(), "same_device": bool(args.same_device)}
     else:
         errors = mism + bad_status
         P_total, U_total = float(P), float(U)
@@ -403,13 +416,39 @@ def cpu_baseline(args, params):
     cpu_threads() threads over independent pieces."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
-    sw = args.seg_words if args.config != 3 else 8192
-    m = 512  # 32 MiB per pass
-    swo = np.arange(0, (m + 1) * sw, sw, dtype=np.uint64)
     op = oracle.preset(args.config)
     op.cfg = params.cfg
-    data = oracle.generate(op, swo)
-    U1 = 8 * int(swo[-1])
+    if args.config == 3:
+        # the bench's own message layout: the first messages of the seeded
+        # 4 x (4-256 KiB) layout, each = table piece + 4 segment pieces
+        # (SerializePacked.write = Serialize.java:256-288), ~32 MiB per pass
+        seg_words = global_layout(args, 1)["seg_words"]
+        gswo = np.concatenate([[0], np.cumsum(seg_words)]).astype(np.uint64)
+        nm = int(np.searchsorted(gswo[4::4], 4 << 20)) + 1
+        segs = oracle.generate(op, gswo[: 4 * nm + 1])
+        table = np.zeros((nm, 3), np.uint64)  # [count - 1 | size0], [size1 | size2], [size3 | pad]
+        sw32 = seg_words[: 4 * nm].reshape(nm, 4).astype(np.uint64)
+        table[:, 0] = 3 | (sw32[:, 0] << 32)
+        table[:, 1] = sw32[:, 1] | (sw32[:, 2] << 32)
+        table[:, 2] = sw32[:, 3]
+        parts, sizes = [], []
+        for k in range(nm):
+            parts.append(table[k].view(np.uint8))
+            sizes.append(3)
+            a0, a1 = 8 * int(gswo[4 * k]), 8 * int(gswo[4 * k + 4])
+            parts.append(segs[a0:a1])
+            sizes.extend(int(x) for x in sw32[k])
+        data = np.concatenate(parts).astype(np.uint8)
+        swo = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+        m, U1 = len(sizes), 8 * int(gswo[4 * nm])
+        sample_desc = f"{nm} messages x (table + 4 segments, 4-256 KiB) of the config3 layout"
+    else:
+        sw = args.seg_words
+        m = 512  # 32 MiB per pass
+        swo = np.arange(0, (m + 1) * sw, sw, dtype=np.uint64)
+        data = oracle.generate(op, swo)
+        U1 = 8 * int(swo[-1])
+        sample_desc = f"{m} pieces x {8 * sw // 1024} KiB (config{args.config} generator)"
 
     def leg(threads, budget):
         t_enc = t_dec = 0.0
@@ -439,7 +478,7 @@ def cpu_baseline(args, params):
         "cores": T,
         "kind": "port",
         "cpu_model": cpu_model(),
-        "sample": f"{pT} passes x {m} pieces x {8 * sw // 1024} KiB (config{args.config} generator), "
+        "sample": f"{pT} passes x {sample_desc}, "
                   f"scalar C restatement of PackedOutputStream/PackedInputStream, {T} threads over "
                   f"independent pieces; single thread: {p1} passes",
         "encode_GiBps": round(eT, 3),

@@ -35,7 +35,9 @@ EXPORTS = [
     "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch", "cpk_ctx_take_error",
     "cpk_decode_messages", "cpk_encode_messages", "cpk_encode_messages_host",
     "cpk_decode_messages_host", "cpk_encode_host_gather", "cpk_encode_messages_host_gather",
+    "cpk_read_message", "cpk_read_message_host",
 ]
+MSG_HEAD_WORDS, MSG_INFO_WORDS = 257, 517  # CPK_MSG_HEAD_WORDS, CPK_MSG_INFO_WORDS
 
 
 class CodecError(RuntimeError):
@@ -93,6 +95,8 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_encode_messages_host": ([vp, vp, vp, u32, vp, u32, vp, u64, vp], i32),
         "cpk_encode_messages_host_gather": ([vp, vp, vp, u32, vp, u32, vp, u64, vp], i32),
         "cpk_decode_messages_host": ([vp, vp, vp, u32, u64, vp, u64, vp, u32, vp, vp, vp], i32),
+        "cpk_read_message": ([vp, vp, u64, u64, vp, u64, vp, vp], i32),
+        "cpk_read_message_host": ([vp, vp, u64, u64, vp, u64, vp], i32),
     }
     for name, (args, res) in sig.items():
         if not strict and not hasattr(L, name):
@@ -378,6 +382,52 @@ def _decode_stream_host(self, packed: np.ndarray, seg_word_off: np.ndarray, out:
 
 
 Context.decode_stream_host = _decode_stream_host
+
+
+def _read_message(self, d_packed, avail: int, d_out, d_info, traversal_limit_words: int = 8 * 1024 * 1024,
+                  stream=None):
+    """cpk_read_message: one message from the front of a device-resident
+    packed stream (Serialize.read, Serialize.java:119-178), no host sync.
+    d_out: int64 tensor of out_cap_words + MSG_HEAD_WORDS words; d_info:
+    int64[MSG_INFO_WORDS], written on the device."""
+    cap = d_out.numel() * d_out.element_size() // 8 - MSG_HEAD_WORDS
+    if cap < 0 or d_info.numel() * d_info.element_size() < 8 * MSG_INFO_WORDS:
+        raise ValueError("d_out / d_info too small")
+    _check(self._lib.cpk_read_message(self.handle, d_packed.data_ptr(), int(avail), int(traversal_limit_words),
+                                      d_out.data_ptr(), cap, d_info.data_ptr(), self._stream(stream)),
+           "cpk_read_message")
+
+
+def _read_message_host(self, packed, out_cap_words: int | None = None,
+                       traversal_limit_words: int = 8 * 1024 * 1024):
+    """cpk_read_message_host -> (status, [segment bytes], bytes consumed,
+    info row).  out_cap_words None: sized by a first call (CPK_ENOMEM gives
+    the words needed)."""
+    pk = np.ascontiguousarray(np.frombuffer(bytes(packed), np.uint8) if not isinstance(packed, np.ndarray)
+                              else packed, dtype=np.uint8)
+    info = np.zeros(MSG_INFO_WORDS, np.uint64)
+    cap = 0 if out_cap_words is None else int(out_cap_words)
+    for _ in range(2):
+        out = np.zeros(max(cap, 1), np.uint64)
+        rc = self._lib.cpk_read_message_host(self.handle, pk.ctypes.data if pk.size else None, pk.size,
+                                             int(traversal_limit_words), out.ctypes.data, cap,
+                                             info.ctypes.data)
+        if rc == ENOMEM and out_cap_words is None and int(info[3]) > cap:
+            cap = int(info[3])
+            continue
+        break
+    if rc in (EDEVICE, EINVAL) or (rc == ENOMEM and int(info.view(np.int64)[0]) != ENOMEM):
+        _check(rc, "cpk_read_message_host")
+    if rc != OK:
+        return rc, [], 0, info
+    n = int(info[2])
+    b = out.view(np.uint8)
+    segs = [b[8 * int(info[4 + i]): 8 * int(info[5 + i])].tobytes() for i in range(n)]
+    return rc, segs, int(info[1]), info
+
+
+Context.read_message = _read_message
+Context.read_message_host = _read_message_host
 
 
 def gen_params(cfg: int, z: float, lz: float, q: float) -> GenParams:

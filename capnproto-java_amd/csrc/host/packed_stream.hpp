@@ -165,35 +165,31 @@ class ChannelReader {
   size_t pos_ = 0, len_ = 0;
 };
 
-// Pieces of `swo` (word offsets) decoded back to back from the channel, as
-// PackedInputStream.read over BufferedInputStreamWrapper would
-// (PackedInputStream.java:35-140): a try on the bytes buffered so far; if
-// they end inside the pieces (CPK_ETRUNC), more are read -- everything the
-// channel has, then, until twice as many as at the last try are buffered,
-// more as they arrive, unless the channel stays idle for a millisecond.  The
-// channel's end inside the pieces is the reference's "premature EOF".
-inline void decodeFromChannel(Gpu &gpu, ChannelReader &in, const std::vector<uint64_t> &swo, uint8_t *out) {
-  const uint32_t n = (uint32_t)swo.size() - 1;
-  std::vector<uint64_t> bounds(n + 1);
-  std::vector<int32_t> st(n ? n : 1);
-  size_t tried = 0;
-  bool first = true;
+// One message (Serialize.read over PackedInputStream, Serialize.java:119-178)
+// from the front of `avail` packed bytes, in one library call
+// (cpk_read_message_host: table and segments on the device).  `words` is a
+// reusable output buffer, grown when the segments need more (CPK_ENOMEM
+// reports how many words); `info` gets the call's info row.
+inline int readMessageBytes(Gpu &gpu, const uint8_t *p, size_t avail, uint64_t limit,
+                            std::vector<uint64_t> &words, std::vector<uint64_t> &info) {
+  info.assign(CPK_MSG_INFO_WORDS, 0);
   for (;;) {
-    if (in.available() > tried || (first && swo[n] == swo[0])) {
-      const int rc = cpk_decode_stream_host(gpu.get(), in.data(), in.available(), swo.data(), n, out,
-                                            bounds.data(), st.data());
-      if (rc == CPK_OK) {
-        in.consume(bounds[n]);
-        return;
-      }
-      if (rc != CPK_ETRUNC) check(rc, "readFromUnbuffered");
-      tried = in.available();
+    const int rc = cpk_read_message_host(gpu.get(), p, avail, limit, words.empty() ? nullptr : words.data(),
+                                         words.size(), info.data());
+    if (rc == CPK_ENOMEM && (int64_t)info[0] == CPK_ENOMEM && info[3] > words.size()) {
+      words.resize(info[3]);
+      continue;
     }
-    first = false;
-    if (!in.fill()) throw DecodeException("premature EOF");  // BufferedInputStreamWrapper.java:98-108
-    while (in.available() < 2 * tried && in.channel().ready(1))
-      if (!in.fill()) break;
+    return rc;
   }
+}
+
+inline std::vector<std::vector<uint8_t>> segmentsOf(const std::vector<uint64_t> &words,
+                                                    const std::vector<uint64_t> &info) {
+  std::vector<std::vector<uint8_t>> segs;
+  const uint8_t *b = (const uint8_t *)words.data();
+  for (uint64_t i = 0; i < info[2]; ++i) segs.emplace_back(b + 8 * info[4 + i], b + 8 * info[5 + i]);
+  return segs;
 }
 
 // ---- PackedOutputStream: write(piece) == one PackedOutputStream.write ----
@@ -271,51 +267,17 @@ struct SerializePacked {
     return out;
   }
 
-  // Serialize.read (Serialize.java:119-178) over PackedInputStream.
+  // Serialize.read (Serialize.java:119-178) over PackedInputStream: the
+  // first word, the rest of the table and every segment in ONE library call
+  // (cpk_read_message_host); the stream advances past the message only.
   static std::vector<std::vector<uint8_t>> read(Gpu &gpu, ArrayInputStream &in,
                                                 uint64_t traversal_limit_words = 8ull << 20) {
-    PackedInputStream pin(gpu, in);
-    uint8_t first[8];
-    pin.read(first, 8);
-    int32_t raw, s0;
-    std::memcpy(&raw, first, 4);
-    std::memcpy(&s0, first + 4, 4);
-    if (raw < 0 || raw > 511) throw DecodeException("segment count must be between 0 and 512");
-    if (s0 < 0) throw DecodeException("segment 0 has more than 2^31 words, which is unsupported");
-    const uint32_t count = (uint32_t)raw + 1;
-    std::vector<uint64_t> sizes = {(uint64_t)s0};
-    uint64_t total = (uint64_t)s0;
-    if (count > 1) {
-      std::vector<uint8_t> rest(4 * (count & ~1u));
-      pin.read(rest.data(), rest.size());
-      for (uint32_t i = 0; i + 1 < count; ++i) {
-        int32_t s;
-        std::memcpy(&s, rest.data() + 4 * i, 4);
-        if (s < 0) throw DecodeException("segment has more than 2^31 words");
-        sizes.push_back((uint64_t)s);
-        total += (uint64_t)s;
-      }
-    }
-    if (total > traversal_limit_words) throw DecodeException("Message size exceeds traversal limit.");
-    for (auto s : sizes)  // makeByteBufferForWords (Serialize.java:45-53)
-      if (s > (1u << 28) - 1) throw DecodeException("segment has too many words");
-    // all segments in one stream-decode call (pieces back to back)
-    std::vector<uint64_t> swo = {0};
-    for (auto s : sizes) swo.push_back(swo.back() + s);
-    std::vector<uint8_t> out(8 * total + 8);
-    std::vector<uint64_t> bounds(count + 1);
-    std::vector<int32_t> st(count);
-    if (total) {
-      in.requireData();
-      check(cpk_decode_stream_host(gpu.get(), in.data(), in.remaining(), swo.data(), count,
-                                   out.data(), bounds.data(), st.data()),
-            "SerializePacked.read");
-      in.advance(bounds[count]);
-    }
-    std::vector<std::vector<uint8_t>> segs;
-    for (uint32_t i = 0; i < count; ++i)
-      segs.emplace_back(out.begin() + 8 * swo[i], out.begin() + 8 * swo[i + 1]);
-    return segs;
+    in.requireData();
+    thread_local std::vector<uint64_t> words, info;
+    check(readMessageBytes(gpu, in.data(), in.remaining(), traversal_limit_words, words, info),
+          "SerializePacked.read");
+    in.advance(info[1]);
+    return segmentsOf(words, info);
   }
 
   // SerializePacked.writeToUnbuffered (SerializePacked.java:119-134): the
@@ -326,41 +288,31 @@ struct SerializePacked {
   }
 
   // SerializePacked.readFromUnbuffered (SerializePacked.java:84-96): as read()
-  // above, over a channel (Serialize.read's checks, Serialize.java:119-178).
+  // above, over a channel.  A try on the bytes buffered so far; if they end
+  // inside the message (CPK_ETRUNC) more are read -- everything the channel
+  // has, then, until twice as many as at the last try are buffered, more as
+  // they arrive unless the channel stays idle for a millisecond (so a
+  // message of M bytes costs O(log M) tries, and a paused peer never waits on
+  // us).  The channel's end inside the message is the reference's "premature
+  // EOF" (BufferedInputStreamWrapper.java:98-108).
   static std::vector<std::vector<uint8_t>> readFromUnbuffered(Gpu &gpu, ChannelReader &in,
                                                               uint64_t traversal_limit_words = 8ull << 20) {
-    uint8_t first[8];
-    decodeFromChannel(gpu, in, {0, 1}, first);
-    int32_t raw, s0;
-    std::memcpy(&raw, first, 4);
-    std::memcpy(&s0, first + 4, 4);
-    if (raw < 0 || raw > 511) throw DecodeException("segment count must be between 0 and 512");
-    if (s0 < 0) throw DecodeException("segment 0 has more than 2^31 words, which is unsupported");
-    const uint32_t count = (uint32_t)raw + 1;
-    std::vector<uint64_t> sizes = {(uint64_t)s0};
-    uint64_t total = (uint64_t)s0;
-    if (count > 1) {
-      std::vector<uint8_t> rest(4 * (count & ~1u));
-      decodeFromChannel(gpu, in, {0, rest.size() / 8}, rest.data());
-      for (uint32_t i = 0; i + 1 < count; ++i) {
-        int32_t sz;
-        std::memcpy(&sz, rest.data() + 4 * i, 4);
-        if (sz < 0) throw DecodeException("segment has more than 2^31 words");
-        sizes.push_back((uint64_t)sz);
-        total += (uint64_t)sz;
+    thread_local std::vector<uint64_t> words, info;
+    size_t tried = 0;
+    for (;;) {
+      if (in.available() > tried) {
+        const int rc = readMessageBytes(gpu, in.data(), in.available(), traversal_limit_words, words, info);
+        if (rc == CPK_OK) {
+          in.consume(info[1]);
+          return segmentsOf(words, info);
+        }
+        if (rc != CPK_ETRUNC) check(rc, "readFromUnbuffered");
+        tried = in.available();
       }
+      if (!in.fill()) throw DecodeException("premature EOF");
+      while (in.available() < 2 * tried && in.channel().ready(1))
+        if (!in.fill()) break;
     }
-    if (total > traversal_limit_words) throw DecodeException("Message size exceeds traversal limit.");
-    for (auto sz : sizes)
-      if (sz > (1u << 28) - 1) throw DecodeException("segment has too many words");
-    std::vector<uint64_t> swo = {0};
-    for (auto sz : sizes) swo.push_back(swo.back() + sz);
-    std::vector<uint8_t> out(8 * total + 8);
-    if (total) decodeFromChannel(gpu, in, swo, out.data());
-    std::vector<std::vector<uint8_t>> segs;
-    for (uint32_t i = 0; i < count; ++i)
-      segs.emplace_back(out.begin() + 8 * swo[i], out.begin() + 8 * swo[i + 1]);
-    return segs;
   }
 
   // SerializePacked.tryReadFromUnbuffered (SerializePacked.java:67-79):

@@ -680,7 +680,8 @@ int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *
         }
         pipe_drain(p);
         rc = pipe_get(ctx, mi, tot[0] * 8, meta_need(mmsg, tot[1]), &p);
-        continue;  // (buffers replaced: stage the chunk again)
+        if (rc) break;  // (no pinned slots left: report it, stage nothing)
+        continue;       // (buffers replaced: stage the chunk again)
       }
       uint64_t *d_si = d_sw + (tot[1] + 1);
       int32_t *d_ss = (int32_t *)(d_si + (tot[1] + 1));
@@ -703,7 +704,10 @@ int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *
         h_msg_status[c.m0 + j] = mst[j];
         if (mst[j] != CPK_OK && first_bad == CPK_OK) first_bad = mst[j];
       }
-      for (uint64_t j = 0; j <= tot[1]; ++j) h_seg_word_off[S + j] = W + sw[j];
+      // (a chunk of broken messages has no segments: the sizing call, with no
+      //  segment array, still gets its statuses)
+      if (h_seg_word_off)
+        for (uint64_t j = 0; j <= tot[1]; ++j) h_seg_word_off[S + j] = W + sw[j];
       if (tot[0]) par_copy((uint8_t *)h_out + 8 * W, s.pin_out, tot[0] * 8);
       W += tot[0];
       S += tot[1];

@@ -1049,6 +1049,58 @@ __global__ void msg_final_kernel(const uint64_t *__restrict__ moff, uint32_t nm,
   mstatus[m] = st != CPK_OK ? st : (mend[m] != moff[m + 1] ? CPK_ETRAILING : CPK_OK);
 }
 
+// ---- one message from the front of a stream (cpk_read_message) -------------
+// Serialize.read over PackedInputStream (Serialize.java:119-178) when the
+// message's packed length is unknown: the table is read here, laid out as the
+// stream's pieces -- [first word] [rest of the table] [segment 0] ... -- and
+// padded with empty pieces (a read() of nothing consumes nothing,
+// PackedInputStream.java:38) to kRmPieces, so the stream decoder's launch
+// needs nothing from the host.  A failed table (or segments over the
+// caller's capacity) leaves every piece empty: nothing is decoded.
+constexpr uint32_t kRmHead = 257;              // table words at most (512 segments)
+constexpr uint32_t kRmPieces = 2 + 512;        // first word, rest of the table, segments
+constexpr uint32_t kRmInfo = 4 + 513;          // status, consumed, count, words, offsets
+
+__global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit,
+                                uint64_t cap_words, uint64_t *__restrict__ swo, uint64_t *__restrict__ info) {
+  if (threadIdx.x != 0) return;
+  uint64_t ip = 0, total = 0;
+  uint32_t count = 0;
+  // sizes parked in the info row (offsets written over them below)
+  int st = read_table(packed, avail, limit, ip, count, total,
+                      [&](uint32_t i, uint32_t sz) { info[5 + i] = sz; });
+  if (st == CPK_OK && total > cap_words) st = CPK_ENOMEM;
+  info[0] = (uint64_t)(int64_t)st;
+  info[1] = 0;
+  info[2] = st == CPK_OK || st == CPK_ENOMEM ? count : 0;
+  info[3] = st == CPK_OK || st == CPK_ENOMEM ? total : 0;
+  uint64_t w = 0;
+  swo[0] = 0;
+  if (st == CPK_OK) {
+    swo[1] = w = 1;
+    swo[2] = w += (count & ~1u) / 2;
+    for (uint32_t i = 0; i < count; ++i) {
+      const uint64_t sz = info[5 + i];
+      info[4 + i] = w;
+      swo[3 + i] = w += sz;
+    }
+    info[4 + count] = w;
+  } else {
+    swo[1] = swo[2] = 0;
+  }
+  for (uint32_t i = (st == CPK_OK ? count : 0) + 3; i <= kRmPieces; ++i) swo[i] = w;
+}
+
+// the message's status: its table's, else the stream's (a failed piece
+// stops the stream: the last piece carries it); the bytes consumed
+__global__ void rm_final_kernel(const uint64_t *__restrict__ in_off, const int32_t *__restrict__ pstatus,
+                                uint64_t *__restrict__ info) {
+  if (threadIdx.x != 0 || (int64_t)info[0] != CPK_OK) return;
+  const int32_t st = pstatus[kRmPieces - 1];
+  info[0] = (uint64_t)(int64_t)st;
+  info[1] = st == CPK_OK ? in_off[kRmPieces] : 0;
+}
+
 // ---- message write: Serialize.write = table piece + segment pieces --------
 // PackedOutputStream.write (:35-205) byte-serial over a word source, as the
 // oracle restates it (oracle/packed_oracle.c:cpko_pack); for the segment
@@ -1234,6 +1286,7 @@ struct cpk_ctx_s {
   HostPipe *pipe;         // cpk_encode_host / cpk_decode_host staging (lazy)
   uint64_t *ss_buf;       // parallel stream decode scratch (stream_split.hip)
   uint64_t ss_cap;        //   u64 entries
+  uint64_t *rm_buf;       // cpk_read_message: piece word offsets | piece ends | statuses (lazy)
 };
 
 namespace {
@@ -1351,6 +1404,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->sp_status) hipFree(ctx->sp_status);
   if (ctx->sp_desc) hipFree(ctx->sp_desc);
   if (ctx->ss_buf) hipFree(ctx->ss_buf);
+  if (ctx->rm_buf) hipFree(ctx->rm_buf);
   pipe_destroy(ctx->pipe);
   free(ctx);
 }
@@ -1765,6 +1819,38 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
   return hip_ok(hipGetLastError());
 }
 
+int cpk_read_message(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t traversal_limit_words,
+                     void *d_out, uint64_t out_cap_words, uint64_t *d_info, void *stream) {
+  using cpk::kRmPieces;
+  if (!ctx || !d_info || (avail && !d_packed) || !d_out) return CPK_EINVAL;
+  if (((uintptr_t)d_packed & 15) || ((uintptr_t)d_out & 7)) return CPK_EINVAL;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (!ctx->rm_buf && hipMalloc(&ctx->rm_buf, (2 * (kRmPieces + 1) + kRmPieces / 2) * 8ull) != hipSuccess)
+    return CPK_ENOMEM;
+  uint64_t *swo = ctx->rm_buf, *in_off = swo + kRmPieces + 1;
+  int32_t *pst = (int32_t *)(in_off + kRmPieces + 1);
+  hipLaunchKernelGGL(cpk::rm_table_kernel, dim3(1), dim3(64), 0, s, (const uint8_t *)d_packed, avail,
+                     traversal_limit_words, out_cap_words, swo, d_info);
+  // the pieces' sizes are on the device only: the stream decoder is sized by
+  // the bytes the caller's capacity can reach (10 per word at most)
+  const uint64_t reach = ss_reach(avail, out_cap_words + cpk::kRmHead);
+  int rc;
+  if (reach >= kSsMin && !getenv("CPK_STREAM_ONE_WAVE")) {
+    rc = ss_decode(ctx, (const uint8_t *)d_packed, avail, reach, swo, kRmPieces, (uint64_t *)d_out, in_off, pst, s);
+  } else {
+    if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
+      return CPK_EDEVICE;
+    dec_launch(ctx, true, 1, (const uint8_t *)d_packed, in_off, swo, kRmPieces, (uint64_t *)d_out, pst, avail,
+               cpk::DecStreams{nullptr, nullptr, nullptr, 1, in_off + kRmPieces}, s);
+    rc = hip_ok(hipGetLastError());
+  }
+  if (rc) return rc;
+  hipLaunchKernelGGL(cpk::rm_final_kernel, dim3(1), dim3(64), 0, s, (const uint64_t *)in_off,
+                     (const int32_t *)pst, d_info);
+  return hip_ok(hipGetLastError());
+}
+
 int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg_off, uint32_t nm,
                         uint64_t traversal_limit_words, void *d_out, uint64_t out_cap_words,
                         uint64_t *d_seg_word_off, uint64_t *d_seg_in_off, int32_t *d_seg_status,
@@ -1865,6 +1951,48 @@ int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
   if (words) par_copy((uint8_t *)h_out + 8 * h_swo[0], sl.pin_out, words * 8);
   for (uint32_t i = 0; i < n; ++i)
     if (h_status[i] != CPK_OK) return h_status[i];
+  return CPK_OK;
+}
+
+int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uint64_t traversal_limit_words,
+                          void *h_out, uint64_t out_cap_words, uint64_t *h_info) {
+  using cpk::kRmInfo;
+  if (!ctx || !h_info || (avail && !h_packed) || (out_cap_words && !h_out)) return CPK_EINVAL;
+  DeviceGuard g(ctx->device);
+  // only the bytes the caller's capacity can reach are staged (the rest of
+  // `avail` may be later messages)
+  const uint64_t R = ss_reach(avail, out_cap_words + cpk::kRmHead);
+  HostPipe *p = nullptr;
+  int rc = pipe_get(ctx, R, (out_cap_words + cpk::kRmHead) * 8, kRmInfo, &p);
+  if (rc) return rc;
+  HostSlot &sl = p->slot[0];
+  par_copy(sl.pin_in, h_packed, R);
+  memset((uint8_t *)sl.pin_in + R, 0, 64);  // (the decoder's read slack)
+  uint64_t *info = sl.pin_meta;
+  if (hipMemcpyAsync(sl.d_in, sl.pin_in, R + 64, hipMemcpyHostToDevice, p->sk))
+    return CPK_EDEVICE;
+  rc = cpk_read_message(ctx, sl.d_in, R, traversal_limit_words, sl.d_out, out_cap_words, sl.d_meta, p->sk);
+  if (rc) {
+    pipe_drain(p);
+    return rc;
+  }
+  if (hipMemcpyAsync(info, sl.d_meta, kRmInfo * 8ull, hipMemcpyDeviceToHost, p->sk) ||
+      hipStreamSynchronize(p->sk))
+    return CPK_EDEVICE;
+  const int st = (int)(int64_t)info[0];
+  const uint32_t count = (uint32_t)info[2];
+  h_info[0] = info[0];
+  h_info[1] = info[1];
+  h_info[2] = info[2];
+  h_info[3] = info[3];
+  if (st != CPK_OK) return st;
+  // the segments only (the table's words lead the device buffer)
+  const uint64_t w0 = info[4], words = info[4 + count] - w0;
+  if (words && (hipMemcpyAsync(sl.pin_out, (uint64_t *)sl.d_out + w0, words * 8, hipMemcpyDeviceToHost, p->sk) ||
+                hipStreamSynchronize(p->sk)))
+    return CPK_EDEVICE;
+  for (uint32_t i = 0; i <= count; ++i) h_info[4 + i] = info[4 + i] - w0;
+  if (words) par_copy(h_out, sl.pin_out, words * 8);
   return CPK_OK;
 }
 

@@ -1,13 +1,18 @@
 // Compression.GPU_PACKED for the reference's benchmark harness (SURVEY.md
-// §8f row 3): the same bytes as Packed (benchmark/.../Packed.java, i.e.
-// SerializePacked.write / read) with the packed codec on the MI355X through
-// org.capnproto.gpu.GpuDispatch.  integration/capnproto-java.patch adds it to
-// Compression.java:33-34, the "gpu-packed" argument to TestCase.java:188-195
-// and its runs to do_benchmarks.bash.
+// §8f row 3): the bytes of Packed (benchmark/.../Packed.java, i.e.
+// SerializePacked.write / read) with the codec on the MI355X through
+// org.capnproto.gpu.GpuDispatch, whatever -Dorg.capnproto.gpu says.
+// integration/capnproto-java.patch adds it to Compression.java:33-34, the
+// "gpu-packed" argument to TestCase.java:188-195 and its runs to
+// do_benchmarks.bash.  Messages below GpuDispatch.MIN_BYTES take the
+// reference's codec, as every dispatched SerializePacked call does
+// (-Dorg.capnproto.gpu.minBytes=0: every message on the GPU).
 package org.capnproto.benchmark;
 
 import java.io.IOException;
 
+import org.capnproto.ReaderOptions;
+import org.capnproto.SerializePacked;
 import org.capnproto.gpu.GpuDispatch;
 
 public final class GpuPacked implements Compression {
@@ -17,16 +22,21 @@ public final class GpuPacked implements Compression {
 
     public void writeBuffered(org.capnproto.BufferedOutputStream writer,
                               org.capnproto.MessageBuilder message) throws IOException {
-        // segment table + segments packed on the device in one call
-        // (cpk_encode_messages_host): SerializePacked.write's bytes
-        GpuDispatch.write(writer, message);
+        // table + segments packed on the device in one call
+        // (cpk_encode_messages_host), or the reference's PackedOutputStream
+        // for a small message
+        if (!GpuDispatch.write(writer, message.getSegmentsForOutput())) {
+            SerializePacked.write(writer, message);
+        }
+        writer.flush();
     }
 
     public org.capnproto.MessageReader newBufferedReader(
         org.capnproto.BufferedInputStream inputStream) throws IOException {
-        // "bytes" mode: the whole ArrayInputStream is the read buffer; client /
-        // server modes: BufferedInputStreamWrapper's 8 KiB windows are taken
-        // until the message decodes (GpuDispatch.read)
-        return GpuDispatch.read(inputStream, org.capnproto.ReaderOptions.DEFAULT_READER_OPTIONS);
+        // one cpk_read_message_host call ("bytes" mode: the whole
+        // ArrayInputStream; client / server: the wrapper's windows until the
+        // message decodes), or the reference's PackedInputStream
+        org.capnproto.MessageReader m = GpuDispatch.read(inputStream, ReaderOptions.DEFAULT_READER_OPTIONS);
+        return m != null ? m : SerializePacked.read(GpuDispatch.source(inputStream));
     }
 }

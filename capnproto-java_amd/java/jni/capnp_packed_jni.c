@@ -365,3 +365,39 @@ JNIEXPORT void JNICALL Java_org_capnproto_gpu_PackedGpu_nativeEncodeMessagesGath
   (*env)->ReleaseLongArrayElements(env, outOff, off, st == CPK_OK ? 0 : JNI_ABORT);
   if (st != CPK_OK) throw_status(env, st);
 }
+
+/* int PackedGpu.nativeReadMessage(long h, ByteBuffer packed, int position, int limit,
+ *                                 long traversalLimit, ByteBuffer out, long[] info)
+ * SerializePacked.read of one message from packed[position, limit) (direct)
+ * in one library call (cpk_read_message_host: table read and checked, every
+ * segment decoded, Serialize.java:119-178).  out (direct) gets the segments
+ * back to back; info[CPK_MSG_INFO_WORDS] = status, bytes consumed, segment
+ * count, words, segment word offsets.  Returns CPK_OK, or -- without
+ * throwing -- CPK_ETRUNC (the bytes end inside the message: the caller takes
+ * more) and CPK_ENOMEM with info[3] = the words needed (out too small); any
+ * other status throws (DecodeException for a malformed message). */
+JNIEXPORT jint JNICALL Java_org_capnproto_gpu_PackedGpu_nativeReadMessage(
+    JNIEnv *env, jclass k, jlong h, jobject packed, jint position, jint limit, jlong traversalLimit,
+    jobject out, jlongArray info) {
+  (void)k;
+  uint8_t *ppk = (uint8_t *)(*env)->GetDirectBufferAddress(env, packed);
+  void *pout = (*env)->GetDirectBufferAddress(env, out);
+  jlong ocap = pout ? (*env)->GetDirectBufferCapacity(env, out) : -1;
+  if (!ppk || !pout || ocap < 0 || position < 0 || limit < position ||
+      (*env)->GetDirectBufferCapacity(env, packed) < limit || !info ||
+      (*env)->GetArrayLength(env, info) < CPK_MSG_INFO_WORDS) {
+    throw_status(env, CPK_EINVAL);
+    return CPK_EINVAL;
+  }
+  uint64_t row[CPK_MSG_INFO_WORDS];
+  memset(row, 0, sizeof row);
+  int st = cpk_read_message_host((cpk_ctx)(intptr_t)h, ppk + position, (uint64_t)(limit - position),
+                                 (uint64_t)traversalLimit, pout, (uint64_t)ocap / 8, row);
+  (*env)->SetLongArrayRegion(env, info, 0, CPK_MSG_INFO_WORDS, (const jlong *)row);
+  if (st == CPK_ENOMEM && (int64_t)row[0] != CPK_ENOMEM) {  /* (a real allocation failure) */
+    throw_status(env, st);
+    return st;
+  }
+  if (st != CPK_OK && st != CPK_ETRUNC && st != CPK_ENOMEM) throw_status(env, st);
+  return st;
+}

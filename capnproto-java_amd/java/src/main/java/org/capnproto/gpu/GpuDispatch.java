@@ -1,17 +1,40 @@
-// The hook SerializePacked.write / read take when the MI355X codec is enabled
-// (integration/capnproto-java.patch adds the two dispatch lines to
-// runtime/src/main/java/org/capnproto/SerializePacked.java:58-61, :101-114).
+// The hook every public SerializePacked method takes when the MI355X codec is
+// enabled (integration/capnproto-java.patch adds one dispatch line to each of
+// runtime/src/main/java/org/capnproto/SerializePacked.java:35-134).
 //
 // Enabled by -Dorg.capnproto.gpu=true or CAPNP_GPU=1 (device: CAPNP_GPU_DEVICE,
-// default 0).  Output bytes and exceptions are the reference's: write packs the
-// segment table and segments on the device (Serialize.java:256-288); read runs
-// Serialize.read's sequence (Serialize.java:119-178) on the device over the
-// bytes the stream has buffered.
+// default 0).  Output bytes and exceptions are the reference's: a write packs
+// the segment table and segments on the device (Serialize.java:256-288); a
+// read runs Serialize.read's sequence (Serialize.java:119-178) on the device
+// in one library call (cpk_read_message_host).
+//
+// Size threshold: a message of fewer than MIN_BYTES unpacked bytes (table +
+// segments) stays on the reference's own PackedOutputStream /
+// PackedInputStream -- a GPU call costs tens of microseconds of launch and
+// copy latency, which only pays above the crossover measured in
+// INTEGRATION.md.  -Dorg.capnproto.gpu.minBytes=N (or CAPNP_GPU_MIN_BYTES)
+// moves it; 0 sends every message to the GPU.  For a read the size comes
+// from the message's segment table, peeked (not consumed) from the bytes the
+// stream has buffered.
+//
+// Streams: bytes a GPU read takes from a stream past its message (a
+// message's packed length is known only once it is decoded) stay in a
+// per-stream Source that every later SerializePacked call on that stream --
+// GPU or reference path -- reads first.  Such a stream must then only be read
+// through SerializePacked.  Channels (readFromUnbuffered) get one persistent
+// Source each, so, unlike the reference's per-call 8 KiB wrapper
+// (SerializePacked.java:92-96), no bytes past a message are dropped.  No lock
+// is held across a blocking read: the only shared state is the weak map of
+// Sources, locked for lookups.
 package org.capnproto.gpu;
 
 import java.io.IOException;
 import java.nio.ByteBuffer;
+import java.nio.channels.ReadableByteChannel;
+import java.nio.channels.WritableByteChannel;
+import java.util.Collections;
 import java.util.Map;
+import java.util.Optional;
 import java.util.WeakHashMap;
 
 public final class GpuDispatch {
@@ -19,6 +42,17 @@ public final class GpuDispatch {
 
     private static final boolean ENABLED =
         Boolean.getBoolean("org.capnproto.gpu") || "1".equals(System.getenv("CAPNP_GPU"));
+
+    /** Messages below this many unpacked bytes take the reference's CPU codec
+     *  (default: the crossover measured in INTEGRATION.md). */
+    public static final long DEFAULT_MIN_BYTES = 256L << 10;
+    public static final long MIN_BYTES = minBytes();
+
+    private static long minBytes() {
+        String v = System.getProperty("org.capnproto.gpu.minBytes");
+        if (v == null) v = System.getenv("CAPNP_GPU_MIN_BYTES");
+        return v == null ? DEFAULT_MIN_BYTES : Long.parseLong(v.trim());
+    }
 
     /** One context per process, created on first use (the library loads then). */
     private static final class Holder {
@@ -30,53 +64,316 @@ public final class GpuDispatch {
 
     public static PackedGpu gpu() { return Holder.GPU; }
 
-    /** SerializePacked.write(output, message): the packed bytes of
-     *  table + segments, written to `output` (flushed, as writeToUnbuffered
-     *  does, SerializePacked.java:119-124). */
-    public static void write(org.capnproto.BufferedOutputStream output,
-                             org.capnproto.MessageBuilder message) throws IOException {
-        PackedGpu.Packed p = gpu().encodeMessages(new ByteBuffer[][] {message.getSegmentsForOutput()});
-        ByteBuffer bytes = p.bytes.duplicate();
-        bytes.position(0);
-        while (bytes.hasRemaining()) output.write(bytes);
-        output.flush();
+    /** Unpacked bytes of a message: its segment table (Serialize.java:258)
+     *  plus its segments. */
+    static long messageBytes(ByteBuffer[] segments) {
+        long b = 4L * ((segments.length + 2) & ~1);
+        for (ByteBuffer s : segments) b += s.remaining();
+        return b;
     }
 
-    // Bytes taken from a channel-backed stream (BufferedInputStreamWrapper,
-    // 8 KiB at a time, BufferedInputStreamWrapper.java:28-108) but not yet
-    // used by a message: a message's packed length is known only once it is
-    // decoded, so the reader may take bytes past it.  Kept per stream.
-    private static final Map<org.capnproto.BufferedInputStream, ByteBuffer> CARRY = new WeakHashMap<>();
+    // ------------------------------------------------------------------ write
 
-    /** SerializePacked.read(input, options). */
-    public static synchronized org.capnproto.MessageReader read(org.capnproto.BufferedInputStream input,
-                                                                org.capnproto.ReaderOptions options)
+    /** SerializePacked.write(output, message) for a message of `segments`
+     *  (MessageBuilder.getSegmentsForOutput, BuilderArena.java:143-154, or a
+     *  MessageReader's segments, Serialize.java:293-299).  Returns false,
+     *  having written nothing, for a message below MIN_BYTES: the caller then
+     *  runs the reference's PackedOutputStream. */
+    public static boolean write(org.capnproto.BufferedOutputStream output, ByteBuffer[] segments)
             throws IOException {
-        if (input instanceof org.capnproto.ArrayInputStream) {
+        if (messageBytes(segments) < MIN_BYTES) return false;
+        ByteBuffer bytes = packed(segments);
+        while (bytes.hasRemaining()) output.write(bytes);
+        return true;
+    }
+
+    /** SerializePacked.writeToUnbuffered(channel, message): the packed bytes
+     *  straight to the channel -- the bytes the reference's 8 KiB
+     *  BufferedOutputStreamWrapper + flush put there (SerializePacked.java:
+     *  119-134).  False, nothing written, below MIN_BYTES. */
+    public static boolean writeToUnbuffered(WritableByteChannel output, ByteBuffer[] segments)
+            throws IOException {
+        if (messageBytes(segments) < MIN_BYTES) return false;
+        ByteBuffer bytes = packed(segments);
+        while (bytes.hasRemaining()) output.write(bytes);
+        return true;
+    }
+
+    private static ByteBuffer packed(ByteBuffer[] segments) throws IOException {
+        PackedGpu.Packed p = gpu().encodeMessages(new ByteBuffer[][] {segments});
+        ByteBuffer bytes = p.bytes.duplicate();
+        bytes.position(0);
+        return bytes;
+    }
+
+    // ------------------------------------------------------------------- read
+
+    private static final Map<Object, Source> SOURCES = Collections.synchronizedMap(new WeakHashMap<>());
+
+    /** The stream SerializePacked must read `input` through: its Source when
+     *  a GPU read left bytes there (or ever took bytes from it), else input. */
+    public static org.capnproto.BufferedInputStream source(org.capnproto.BufferedInputStream input) {
+        Source s = SOURCES.get(input);
+        return s != null ? s : input;
+    }
+
+    /** The persistent buffered stream of a channel (readFromUnbuffered /
+     *  tryReadFromUnbuffered read through it, GPU or reference path). */
+    public static org.capnproto.BufferedInputStream stream(ReadableByteChannel channel) {
+        synchronized (SOURCES) {
+            Source s = SOURCES.get(channel);
+            if (s == null) SOURCES.put(channel, s = new Source(channel));
+            return s;
+        }
+    }
+
+    private static Source sourceFor(org.capnproto.BufferedInputStream input) {
+        if (input instanceof Source) return (Source) input;
+        synchronized (SOURCES) {
+            Source s = SOURCES.get(input);
+            if (s == null) SOURCES.put(input, s = new Source(input));
+            return s;
+        }
+    }
+
+    /** SerializePacked.read(input, options): the message, read on the GPU;
+     *  null when it is below MIN_BYTES (or its table is not yet buffered) --
+     *  nothing consumed, the caller runs the reference path over
+     *  source(input). */
+    public static org.capnproto.MessageReader read(org.capnproto.BufferedInputStream input,
+                                                   org.capnproto.ReaderOptions options) throws IOException {
+        org.capnproto.BufferedInputStream in = source(input);
+        // (getReadBuffer: DecodeException at the end of the stream, as the
+        //  reference's first read throws)
+        ByteBuffer head = in.getReadBuffer();
+        if (!head.hasRemaining()) throw new org.capnproto.DecodeException("premature EOF");
+        long bytes = peekMessageBytes(head);
+        if (bytes < 0 || bytes < MIN_BYTES) return null;
+        long words = bytes / 8;
+        if (in instanceof org.capnproto.ArrayInputStream) {
             // the whole array is the read buffer (ArrayInputStream.java:53-58)
-            ByteBuffer buf = input.getReadBuffer();
-            ByteBuffer[] segs = gpu().readMessage(buf, options.traversalLimitInWords);
+            ByteBuffer[] segs = gpu().readMessage(head, options.traversalLimitInWords, words);
+            if (segs == null) throw new org.capnproto.DecodeException("Premature EOF");
             return new org.capnproto.MessageReader(segs, options);
         }
-        ByteBuffer acc = CARRY.get(input);
+        return readFrom(sourceFor(input), options, words);
+    }
+
+    /** SerializePacked.tryRead(input, options): Optional.empty() when the
+     *  stream ends before a message starts (the documented contract,
+     *  SerializePacked.java:31-46); null when the message is below MIN_BYTES
+     *  (the caller then runs the reference path over source(input)). */
+    public static Optional<org.capnproto.MessageReader> tryRead(org.capnproto.BufferedInputStream input,
+                                                                org.capnproto.ReaderOptions options)
+            throws IOException {
+        org.capnproto.BufferedInputStream in = source(input);
+        ByteBuffer head;
+        try {
+            head = in.getReadBuffer();
+        } catch (org.capnproto.DecodeException eof) {
+            return Optional.empty();
+        }
+        if (!head.hasRemaining()) return Optional.empty();
+        org.capnproto.MessageReader m = read(input, options);
+        return m == null ? null : Optional.of(m);
+    }
+
+    /** GPU read of one message from a Source: a try on the bytes buffered
+     *  so far; while they end inside the message, more are taken -- until
+     *  twice as many as at the last try are buffered, the upstream pauses
+     *  (a short read: waiting longer could wait on a peer that waits on us),
+     *  or the table's bound on the message's packed bytes is reached.  A
+     *  message of M bytes costs O(log M) tries plus one per pause, and the
+     *  buffer grows geometrically. */
+    private static org.capnproto.MessageReader readFrom(Source s, org.capnproto.ReaderOptions options,
+                                                        long words) throws IOException {
+        final long bound = 10 * (words + 1) + 16;   // packed bytes of the message, at most
+        long tried = 0;
         for (;;) {
-            if (acc != null && acc.hasRemaining()) {
-                try {
-                    ByteBuffer[] segs = gpu().readMessage(acc, options.traversalLimitInWords);
-                    CARRY.put(input, acc);   // (position now past the message)
-                    return new org.capnproto.MessageReader(segs, options);
-                } catch (org.capnproto.DecodeException e) {
-                    if (!PackedGpu.isTruncation(e)) throw e;
-                    // the bytes so far end inside the message: take more
+            if (s.buf.remaining() > tried) {
+                ByteBuffer[] segs = gpu().readMessage(s.buf, options.traversalLimitInWords, words);
+                if (segs != null) return new org.capnproto.MessageReader(segs, options);
+                tried = s.buf.remaining();
+            }
+            long target = Math.min(Math.max(2 * tried, tried + 1), bound);
+            // (a parse takes at most 10 bytes per word: with `bound` bytes
+            //  buffered the message cannot be cut short)
+            if (target <= s.buf.remaining()) throw new org.capnproto.DecodeException("premature EOF");
+            while (s.buf.remaining() < target) {
+                if (!s.fill()) break;   // (a short read: the upstream paused)
+            }
+        }
+    }
+
+    // ------------------------------------------------------------------ peek
+
+    /** Unpacked bytes (table + segments) of the message whose packed bytes
+     *  start at b.position(), from its segment table alone (Serialize.java:
+     *  119-163: the first word, then 4 * (count & ~1) bytes); -1 when b does
+     *  not hold the whole table or the table is invalid (the reference path
+     *  then reads more, or throws the reference's exception).  Reads with
+     *  absolute gets: b is not consumed. */
+    static long peekMessageBytes(ByteBuffer b) {
+        long[] first = new long[1];
+        int p = unpackWords(b, b.position(), b.limit(), first, 1);
+        if (p < 0) return -1;
+        int raw = (int) first[0];
+        int s0 = (int) (first[0] >>> 32);
+        if (raw < 0 || raw > 511 || s0 < 0) return -1;
+        int count = raw + 1;
+        long total = s0;
+        int more = (count & ~1) / 2;
+        if (more > 0) {
+            long[] sizes = new long[more];
+            if (unpackWords(b, p, b.limit(), sizes, more) < 0) return -1;
+            for (int i = 0; i < count - 1; ++i) {
+                int sz = (int) (sizes[i / 2] >>> (32 * (i & 1)));
+                if (sz < 0) return -1;
+                total += sz;
+            }
+        }
+        return 8L * (1 + more) + 8L * total;
+    }
+
+    /** `n` words unpacked from b[p, end) into out (PackedInputStream.java:
+     *  49-134's record rules); the position after them, or -1 if the bytes
+     *  end first or a run passes the n words. */
+    private static int unpackWords(ByteBuffer b, int p, int end, long[] out, int n) {
+        int wi = 0;
+        while (wi < n) {
+            if (p >= end) return -1;
+            int tag = b.get(p++) & 0xff;
+            long w = 0;
+            for (int i = 0; i < 8; ++i) {
+                if ((tag >>> i & 1) != 0) {
+                    if (p >= end) return -1;
+                    w |= (long) (b.get(p++) & 0xff) << (8 * i);
                 }
             }
-            ByteBuffer src = input.getReadBuffer();   // blocks for >= 1 byte; DecodeException at EOF
-            int have = acc == null ? 0 : acc.remaining();
-            ByteBuffer grown = ByteBuffer.allocateDirect(have + src.remaining());
-            if (acc != null) grown.put(acc);
-            grown.put(src);   // (src.position reaches its limit: the bytes are taken)
+            out[wi++] = w;
+            if (tag == 0 || tag == 0xff) {
+                if (p >= end) return -1;
+                int run = b.get(p++) & 0xff;
+                if (run > n - wi) return -1;
+                for (int k = 0; k < run; ++k) {
+                    long v = 0;
+                    if (tag == 0xff) {
+                        if (end - p < 8) return -1;
+                        for (int i = 0; i < 8; ++i) v |= (long) (b.get(p++) & 0xff) << (8 * i);
+                    }
+                    out[wi++] = v;
+                }
+            }
+        }
+        return p;
+    }
+
+    // ---------------------------------------------------------------- Source
+
+    /** A BufferedInputStream (BufferedInputStream.java:27-38) over a carry
+     *  buffer that an upstream stream or channel refills: what the GPU path
+     *  reads from, and what the reference path reads when bytes were carried.
+     *  Direct memory (passed to JNI zero-copy), grown by doubling. */
+    static final class Source implements org.capnproto.BufferedInputStream {
+        private final org.capnproto.BufferedInputStream upstream;   // or
+        private final ReadableByteChannel channel;
+        ByteBuffer buf;   // [position, limit): bytes not yet consumed
+
+        Source(org.capnproto.BufferedInputStream upstream) {
+            this.upstream = upstream;
+            this.channel = null;
+            this.buf = PackedGpu.directBuffer(1 << 16);
+            this.buf.limit(0);
+        }
+
+        Source(ReadableByteChannel channel) {
+            this.upstream = null;
+            this.channel = channel;
+            this.buf = PackedGpu.directBuffer(1 << 16);
+            this.buf.limit(0);
+        }
+
+        /** Room for `more` bytes after the limit: compact, or grow by doubling. */
+        private void reserve(int more) {
+            if (buf.capacity() - buf.limit() >= more) return;
+            int have = buf.remaining();
+            if (buf.capacity() - have >= more && buf.position() >= buf.capacity() / 2) {
+                ByteBuffer rest = buf.slice();
+                buf.clear();
+                buf.put(rest);   // (no overlap: at most cap/2 bytes from past cap/2)
+                buf.flip();
+                return;
+            }
+            int cap = buf.capacity();
+            while (cap - have < more) cap = Math.multiplyExact(cap, 2);
+            ByteBuffer grown = PackedGpu.directBuffer(cap);
+            grown.put(buf);
             grown.flip();
-            acc = grown;
+            buf = grown;
+        }
+
+        /** One read from upstream appended to the buffer (blocking for >= 1
+         *  byte).  DecodeException("premature EOF") at the end of the stream
+         *  (BufferedInputStreamWrapper.java:98-108).  True if the read filled
+         *  all the room it was offered (more may be ready). */
+        boolean fill() throws IOException {
+            if (channel != null) {
+                reserve(8192);
+                int lim = buf.limit();
+                ByteBuffer w = buf.duplicate();
+                w.position(lim).limit(buf.capacity());
+                int offered = w.remaining();
+                int n = 0;
+                while (n == 0) {
+                    n = channel.read(w);
+                    if (n < 0) throw new org.capnproto.DecodeException("premature EOF");
+                }
+                buf.limit(lim + n);
+                return n == offered;
+            }
+            ByteBuffer src = upstream.getReadBuffer();   // DecodeException at EOF
+            int n = src.remaining();
+            if (n == 0) throw new org.capnproto.DecodeException("premature EOF");
+            reserve(n);
+            int lim = buf.limit();
+            ByteBuffer w = buf.duplicate();
+            w.position(lim).limit(lim + n);
+            boolean full = n == src.capacity();
+            w.put(src);   // (src.position reaches its limit: the bytes are taken)
+            buf.limit(lim + n);
+            return full;
+        }
+
+        @Override
+        public ByteBuffer getReadBuffer() throws IOException {
+            if (!buf.hasRemaining()) {
+                buf.clear();
+                buf.limit(0);
+                fill();
+            }
+            return buf;
+        }
+
+        @Override
+        public int read(ByteBuffer dst) throws IOException {
+            int want = dst.remaining();
+            while (buf.remaining() < want) fill();   // (premature EOF thrown at the end)
+            ByteBuffer from = buf.duplicate();
+            from.limit(from.position() + want);
+            dst.put(from);
+            buf.position(buf.position() + want);
+            return want;
+        }
+
+        @Override
+        public boolean isOpen() {
+            return channel != null ? channel.isOpen() : upstream.isOpen();
+        }
+
+        @Override
+        public void close() throws IOException {
+            if (channel != null) channel.close();
+            else upstream.close();
         }
     }
 }

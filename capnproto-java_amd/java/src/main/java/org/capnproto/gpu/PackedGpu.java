@@ -38,6 +38,14 @@ public final class PackedGpu implements AutoCloseable {
                                                           ByteBuffer out, long[] outOff);
     private static native long nativeDecodeStream(long handle, ByteBuffer packed, int position,
                                                   int limit, long[] segWordOff, ByteBuffer out);
+    private static native int nativeReadMessage(long handle, ByteBuffer packed, int position, int limit,
+                                                long traversalLimit, ByteBuffer out, long[] info);
+
+    /** Status codes nativeReadMessage returns instead of throwing
+     *  (include/capnp_packed.h). */
+    static final int CPK_OK = 0, CPK_ETRUNC = -2, CPK_ENOMEM = -5;
+    /** CPK_MSG_INFO_WORDS: status, consumed, count, words, offsets. */
+    static final int MSG_INFO_WORDS = 517;
 
     private long handle;
 
@@ -61,11 +69,26 @@ public final class PackedGpu implements AutoCloseable {
         return ByteBuffer.allocateDirect((int) bytes).order(ByteOrder.LITTLE_ENDIAN);
     }
 
+    /** A little-endian direct buffer of `bytes` bytes (GpuDispatch's stream
+     *  buffers). */
+    static ByteBuffer directBuffer(int bytes) {
+        return ByteBuffer.allocateDirect(bytes).order(ByteOrder.LITTLE_ENDIAN);
+    }
+
     /** `b`'s remaining bytes in a direct buffer (itself when already direct). */
     private static ByteBuffer asDirect(ByteBuffer b) throws IOException {
+        return asDirect(b, Long.MAX_VALUE);
+    }
+
+    /** At most `max` of `b`'s remaining bytes in a direct buffer (b itself
+     *  when already direct): a heap buffer is copied only as far as a read
+     *  can reach. */
+    private static ByteBuffer asDirect(ByteBuffer b, long max) throws IOException {
         if (b.isDirect()) return b;
-        ByteBuffer d = direct(b.remaining());
-        d.put(b.duplicate()).flip();
+        ByteBuffer src = b.duplicate();
+        if (src.remaining() > max) src.limit(src.position() + (int) max);
+        ByteBuffer d = direct(src.remaining());
+        d.put(src).flip();
         return d;
     }
 
@@ -252,55 +275,50 @@ public final class PackedGpu implements AutoCloseable {
     }
 
     /** SerializePacked.read of one message from the front of `packed`
-     *  (Serialize.java:119-178 over PackedInputStream): the first word, then
-     *  4 * (count & ~1) bytes of sizes, then every segment in one stream
-     *  decode; the same checks and messages as doRead.  packed.position
-     *  advances past the message.  Returns the segments (little-endian). */
-    public ByteBuffer[] readMessage(ByteBuffer packed, long traversalLimitInWords) throws IOException {
-        // a heap buffer is copied to direct memory once for the three reads
-        ByteBuffer pk = asDirect(packed);
-        int at = pk.position();
-        ByteBuffer first = ByteBuffer.allocate(8).order(ByteOrder.LITTLE_ENDIAN);
-        at += (int) decodeStreamDirect(pk, at, new ByteBuffer[] {first});
-        int rawCount = first.getInt(0);
-        if (rawCount < 0 || rawCount > 511)
-            throw new org.capnproto.DecodeException("segment count must be between 0 and 512");
-        int count = 1 + rawCount;
-        int[] sizes = new int[count];
-        sizes[0] = first.getInt(4);
-        if (sizes[0] < 0)
-            throw new org.capnproto.DecodeException("segment 0 has more than 2^31 words, which is unsupported");
-        long total = sizes[0];
-        if (count > 1) {
-            ByteBuffer more = ByteBuffer.allocate(4 * (count & ~1)).order(ByteOrder.LITTLE_ENDIAN);
-            at += (int) decodeStreamDirect(pk, at, new ByteBuffer[] {more});
-            for (int i = 0; i < count - 1; ++i) {
-                sizes[i + 1] = more.getInt(i * 4);
-                if (sizes[i + 1] < 0)
-                    throw new org.capnproto.DecodeException("segment " + (i + 1) +
-                                                            " has more than 2^31 words, which is unsupported");
-                total += sizes[i + 1];
+     *  (Serialize.java:119-178 over PackedInputStream) in ONE library call
+     *  (cpk_read_message_host): the device reads the first word and the rest
+     *  of the table, runs doRead's checks (count, sizes, traversal limit,
+     *  makeByteBufferForWords's bound) and decodes every segment.  The
+     *  segments come back as slices of one direct buffer (zero-copy for JNI,
+     *  SURVEY.md §8f row 4), little-endian; packed.position advances past the
+     *  message.  Returns null, consuming nothing, when the bytes end inside
+     *  the message (a channel reader takes more and calls again).
+     *  @param wordsHint expected unpacked words (e.g. from the table), 0 if
+     *         unknown: the output is sized by a first call then
+     *  @throws org.capnproto.DecodeException for a malformed message */
+    public ByteBuffer[] readMessage(ByteBuffer packed, long traversalLimitInWords, long wordsHint)
+            throws IOException {
+        long cap = Math.max(wordsHint, 0);
+        // a heap buffer is copied to direct memory once, only as far as a
+        // message of `cap` words can reach (10 bytes per word at most)
+        ByteBuffer pk = asDirect(packed, cap > 0 ? 10 * (cap + 257) + 16 : Long.MAX_VALUE);
+        long[] info = new long[MSG_INFO_WORDS];
+        for (;;) {
+            ByteBuffer out = direct(8 * cap + 8);
+            int st = nativeReadMessage(handle, pk, pk.position(), pk.limit(), traversalLimitInWords, out, info);
+            if (st == CPK_ENOMEM && info[3] > cap) {   // (the table says how many words)
+                cap = info[3];
+                continue;
             }
+            if (st == CPK_ETRUNC) return null;
+            if (st != CPK_OK) throw new IOException("cpk_read_message_host: status " + st);
+            packed.position(packed.position() + (int) info[1]);
+            int count = (int) info[2];
+            ByteBuffer[] segs = new ByteBuffer[count];
+            for (int i = 0; i < count; ++i) {
+                ByteBuffer seg = out.duplicate();
+                seg.position((int) (info[4 + i] * 8)).limit((int) (info[5 + i] * 8));
+                segs[i] = seg.slice().order(ByteOrder.LITTLE_ENDIAN);
+            }
+            return segs;
         }
-        if (total > traversalLimitInWords)
-            throw new org.capnproto.DecodeException("Message size exceeds traversal limit.");
-        // All segments land in ONE direct buffer (zero-copy for JNI, SURVEY.md
-        // §8f row 4) that the returned slices share; one stream decode.
-        long[] swo = new long[count + 1];
-        for (int i = 0; i < count; ++i) {
-            if (sizes[i] > MAX_SEGMENT_WORDS)   // Serialize.makeByteBufferForWords, Serialize.java:45-53
-                throw new org.capnproto.DecodeException("segment has too many words (" + sizes[i] + ")");
-            swo[i + 1] = swo[i] + sizes[i];
-        }
-        ByteBuffer out = direct(swo[count] * 8 + 8);
-        at += (int) nativeDecodeStream(handle, pk, at, pk.limit(), swo, out);
-        packed.position(packed.position() + (at - pk.position()));
-        ByteBuffer[] segs = new ByteBuffer[count];
-        for (int i = 0; i < count; ++i) {
-            ByteBuffer seg = out.duplicate();
-            seg.position((int) (swo[i] * 8)).limit((int) (swo[i + 1] * 8));
-            segs[i] = seg.slice().order(ByteOrder.LITTLE_ENDIAN);
-        }
+    }
+
+    /** readMessage with the output sized by the call itself; a message cut
+     *  short is the reference's premature EOF (ArrayInputStream.java:53-58). */
+    public ByteBuffer[] readMessage(ByteBuffer packed, long traversalLimitInWords) throws IOException {
+        ByteBuffer[] segs = readMessage(packed, traversalLimitInWords, 0);
+        if (segs == null) throw new org.capnproto.DecodeException(TRUNCATED);
         return segs;
     }
 

@@ -85,8 +85,11 @@ int cpk_ctx_device(cpk_ctx ctx);
 
 /* Batch encode of n pieces, device-resident (replaces n calls of
  * PackedOutputStream.write, PackedOutputStream.java:35-205).  Pieces of any
- * size (the default encoder walks each piece with one wave: a size pass, a
- * scan of the sizes, an emit pass).
+ * size.  The encoder is chosen on the device from the piece sizes (no host
+ * sync): like-sized pieces of 1-8 Ki words take the single-pass encoder
+ * (read the words once, write the packed bytes once, offsets by a decoupled
+ * look-back over the pieces); other batches the two-pass one (a size pass, a
+ * scan of the sizes, an emit pass; DESIGN.md section 4).
  *   d_in            : 8-byte aligned words; piece i is words
  *                     [d_seg_word_off[i], d_seg_word_off[i+1]).
  *   d_seg_word_off  : uint64[n+1], device.
@@ -183,12 +186,43 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
                         uint32_t seg_cap, uint64_t *d_msg_seg_off, int32_t *d_msg_status,
                         uint64_t *h_totals, void *stream);
 
+/* One message from the front of a packed byte stream whose length is not
+ * known in advance (SerializePacked.read / readFromUnbuffered: Serialize.read
+ * over PackedInputStream, Serialize.java:119-178), in one enqueue with no
+ * host sync.  The device reads the segment table as the reference does (the
+ * first word, then 4 * (count & ~1) bytes), validates it (count <= 512,
+ * sizes >= 0, total <= traversal_limit_words, segments <= 2^28-1 words,
+ * Serialize.java:45-53, :125-163) and decodes every segment back to back
+ * from where the table ends.  Bytes after the message are left alone.
+ *   d_packed : the stream's first `avail` bytes, 16-byte aligned, readable
+ *              up to round_up(avail, 16).
+ *   d_out    : 8-byte aligned, out_cap_words + CPK_MSG_HEAD_WORDS words: the
+ *              table's words land first, segment i is words
+ *              [d_info[4 + i], d_info[5 + i]).
+ *   d_info   : uint64[CPK_MSG_INFO_WORDS], device, written: [0] status (as
+ *              int64), [1] bytes consumed, [2] segment count, [3] total
+ *              segment words, [4 .. 4 + count] segment word offsets.
+ * Status: CPK_OK; CPK_ETRUNC when the bytes end inside the message (a
+ * channel reader takes more and calls again); CPK_EFRAME / CPK_EOVERRUN as
+ * Serialize.read would throw; CPK_ENOMEM when the segments exceed
+ * out_cap_words (nothing decoded; [2] and [3] say how many).  Only
+ * min(avail, 10 * (out_cap_words + CPK_MSG_HEAD_WORDS) + 16) bytes are read. */
+#define CPK_MSG_HEAD_WORDS 257
+#define CPK_MSG_INFO_WORDS 517
+int cpk_read_message(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t traversal_limit_words,
+                     void *d_out, uint64_t out_cap_words, uint64_t *d_info, void *stream);
+
 /* Host-memory convenience forms (the socket/file ByteBuffer path,
  * SerializePacked.java:75-96, :119-134).  Synchronous.  encode_host and
  * decode_host pipeline the batch in chunks of whole pieces through pinned
  * staging kept in the context (CPK_HOST_CHUNK_MB, default 256;
- * CPK_HOST_THREADS copy threads, default 8); decode_stream_host stages the
- * whole stream.
+ * CPK_HOST_THREADS copy threads, default 8); decode_stream_host and
+ * read_message_host stage only the bytes the pieces can reach (10 per word
+ * at most), the rest of `avail` may be later messages.
+ *   cpk_read_message_host: cpk_read_message over host memory; h_out gets the
+ *                    segments only, back to back (out_cap_words words), and
+ *                    h_info[4 + i] their word offsets from 0.  Two syncs (the
+ *                    info row, then the words).
  *   cpk_encode_host: h_out capacity >= cpk_batch_packed_capacity();
  *                    h_out_off[n+1] written.
  *   cpk_decode_host: h_status[n] written; returns CPK_OK iff all pieces OK. */
@@ -207,6 +241,8 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
 int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
                            const uint64_t *h_seg_word_off, uint32_t n, void *h_out,
                            uint64_t *h_in_off, int32_t *h_status);
+int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uint64_t traversal_limit_words,
+                          void *h_out, uint64_t out_cap_words, uint64_t *h_info);
 
 /* Host-memory forms of the message batches (staged whole through device
  * memory; synchronous).

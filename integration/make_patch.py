@@ -2,8 +2,8 @@
 capnproto-java maintainer applies (patch -p1 at the repository root) to
 select the MI355X codec.
 
-  runtime/.../SerializePacked.java  read / write dispatch to GpuDispatch when
-                                    enabled (SerializePacked.java:58-61, :101-114)
+  runtime/.../SerializePacked.java  every public method dispatches to GpuDispatch
+                                    when enabled (SerializePacked.java:35-134)
   benchmark/.../Compression.java    Compression.GPU_PACKED (Compression.java:33-34)
   benchmark/.../TestCase.java       the "gpu-packed" argument (TestCase.java:188-195)
   do_benchmarks.bash                gpu-packed runs beside each packed run
@@ -48,21 +48,52 @@ def main():
                 (d / f).parent.mkdir(parents=True, exist_ok=True)
                 shutil.copy(ref / f, d / f)
         sp = b / EDITED[0]
-        edit(sp, "    public static MessageReader read(BufferedInputStream input, ReaderOptions options) "
-                 "throws java.io.IOException {\n",
-             "    public static MessageReader read(BufferedInputStream input, ReaderOptions options) "
-             "throws java.io.IOException {\n"
-             "        if (org.capnproto.gpu.GpuDispatch.enabled()) {\n"
-             "            return org.capnproto.gpu.GpuDispatch.read(input, options);\n"
-             "        }\n")
-        edit(sp, "    public static void write(BufferedOutputStream output,\n"
-                 "                             MessageBuilder message) throws java.io.IOException {\n",
-             "    public static void write(BufferedOutputStream output,\n"
-             "                             MessageBuilder message) throws java.io.IOException {\n"
-             "        if (org.capnproto.gpu.GpuDispatch.enabled()) {\n"
-             "            org.capnproto.gpu.GpuDispatch.write(output, message);\n"
-             "            return;\n"
-             "        }\n")
+        G = "org.capnproto.gpu.GpuDispatch"
+        # every public method dispatches (SerializePacked.java:35-134); the
+        # one-argument overloads delegate to the two-argument ones
+        for sig, kind in ((" tryRead(BufferedInputStream input, ReaderOptions options) throws java.io.IOException {\n",
+                           "tryRead"),
+                          (" read(BufferedInputStream input, ReaderOptions options) throws java.io.IOException {\n",
+                           "read")):
+            ret = "Optional<MessageReader>" if kind == "tryRead" else "MessageReader"
+            edit(sp, sig, sig +
+                 f"        if ({G}.enabled()) {{\n"
+                 f"            {ret} m = {G}.{kind}(input, options);\n"
+                 f"            if (m != null) return m;  // (null: below {G}.MIN_BYTES, the codec below)\n"
+                 f"            input = {G}.source(input);  // (bytes a GPU read carried past its message first)\n"
+                 f"        }}\n")
+        for tail, kind in (("        return Serialize.tryRead(packedInput, options);\n", "tryRead"),
+                           ("        return Serialize.read(packedInput, options);\n", "read")):
+            body = ("        PackedInputStream packedInput = new PackedInputStream(new BufferedInputStreamWrapper(input));\n"
+                    + tail)
+            edit(sp, "ReaderOptions options) throws java.io.IOException {\n" + body,
+                 "ReaderOptions options) throws java.io.IOException {\n"
+                 f"        if ({G}.enabled()) {{  // (one persistent buffered stream per channel)\n"
+                 f"            return {kind}({G}.stream(input), options);\n"
+                 "        }\n" + body)
+        for msg, segs in (("MessageBuilder", "message.getSegmentsForOutput()"), ("MessageReader", "segmentsOf(message)")):
+            edit(sp, f"{msg} message) throws java.io.IOException {{\n        PackedOutputStream packedOutputStream",
+                 f"{msg} message) throws java.io.IOException {{\n"
+                 f"        if ({G}.enabled() && {G}.write(output, {segs})) {{\n"
+                 "            return;  // (false: below MIN_BYTES, the codec below)\n"
+                 "        }\n"
+                 "        PackedOutputStream packedOutputStream")
+            edit(sp, f"{msg} message) throws java.io.IOException {{\n        BufferedOutputStreamWrapper buffered",
+                 f"{msg} message) throws java.io.IOException {{\n"
+                 f"        if ({G}.enabled() && {G}.writeToUnbuffered(output, {segs})) {{\n"
+                 "            return;  // (the packed bytes straight to the channel)\n"
+                 "        }\n"
+                 "        BufferedOutputStreamWrapper buffered")
+        t = sp.read_text()
+        k = t.rstrip().rindex("}")
+        sp.write_text(t[:k] + "    // a MessageReader's segments, as Serialize.write(channel, MessageReader) takes them\n"
+                      "    private static java.nio.ByteBuffer[] segmentsOf(MessageReader message) {\n"
+                      "        java.nio.ByteBuffer[] s = new java.nio.ByteBuffer[message.arena.segments.size()];\n"
+                      "        for (int i = 0; i < s.length; ++i) {\n"
+                      "            s[i] = message.arena.segments.get(i).buffer.duplicate();\n"
+                      "        }\n"
+                      "        return s;\n"
+                      "    }\n" + t[k:])
         edit(b / EDITED[1], "    public final Compression UNCOMPRESSED = new Uncompressed();",
              "    public final Compression UNCOMPRESSED = new Uncompressed();\n"
              "    public final Compression GPU_PACKED = new GpuPacked();")

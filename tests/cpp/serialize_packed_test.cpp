@@ -10,6 +10,9 @@
 #include <vector>
 
 #include "../../capnproto-java_amd/csrc/host/packed_stream.hpp"
+extern "C" {
+#include "../../oracle/packed_oracle.h"  // the checker (test infrastructure only)
+}
 
 using namespace capnp_amd;
 using Bytes = std::vector<uint8_t>;
@@ -46,6 +49,24 @@ static void assertPacksTo(Gpu &gpu, const Bytes &unpacked, const Bytes &packed) 
     EXPECT(n == unpacked.size(), "read length");
     EXPECT(bytes == unpacked, "unpacked bytes");
   }
+}
+
+// the oracle's Serialize.write through PackedOutputStream (SerializePacked.write)
+static Bytes oracleWrite(const std::vector<Bytes> &segs) {
+  std::vector<Bytes> padded;
+  std::vector<const uint8_t *> ptrs;
+  std::vector<uint32_t> words;
+  size_t cap = cpko_packed_bound(segs.size() + 2) + 16;
+  for (auto &sg : segs) {
+    padded.push_back(sg);
+    padded.back().resize(sg.size() + 8, 0);
+    words.push_back((uint32_t)(sg.size() / 8));
+    cap += cpko_packed_bound(sg.size() / 8);
+  }
+  for (auto &pb : padded) ptrs.push_back(pb.data());
+  Bytes out(cap);
+  out.resize(cpko_write_message(ptrs.data(), words.data(), (uint32_t)segs.size(), out.data()));
+  return out;
 }
 
 static Bytes rep(Bytes b, int times) {
@@ -234,6 +255,28 @@ int main() {
     close(fds[0]);
     std::printf("pipe: %zu messages, %.1f MiB of words, %.3f s: %.3f GiB/s, %.0f messages/s\n", msgs.size(),
                 words * 8 / 1048576.0, dt, words * 8 / dt / (1 << 30), msgs.size() / dt);
+    // the wire itself: what writeToUnbuffered puts on the channel is, message
+    // by message, the oracle's Serialize.write through PackedOutputStream
+    EXPECT(pipe(fds) == 0, "pipe");
+    std::thread wire_writer([&]() {
+      Gpu wg(0);
+      FdChannel out(fds[1]);
+      for (int m = 0; m < 300; ++m) SerializePacked::writeToUnbuffered(wg, out, msgs[m]);
+      close(fds[1]);
+    });
+    Bytes wire, expect;
+    {
+      FdChannel raw(fds[0]);
+      std::vector<uint8_t> buf(1 << 16);
+      for (size_t k; (k = raw.readSome(buf.data(), buf.size())) > 0;) wire.insert(wire.end(), buf.begin(), buf.begin() + k);
+    }
+    wire_writer.join();
+    close(fds[0]);
+    for (int m = 0; m < 300; ++m) {
+      Bytes b = oracleWrite(msgs[m]);
+      expect.insert(expect.end(), b.begin(), b.end());
+    }
+    EXPECT(wire == expect, "wire bytes == oracle Serialize.write per message");
     // the same messages packed in one GPU call, then read one by one
     EXPECT(pipe(fds) == 0, "pipe");
     const auto t1 = std::chrono::steady_clock::now();
@@ -268,6 +311,45 @@ int main() {
     }
     EXPECT(threw, "truncated channel must throw DecodeException");
     close(fds[0]);
+  }
+  // SerializePacked.read of one 64 MiB single-segment message (one library
+  // call: cpk_read_message_host) against the oracle's bytes, and the same
+  // message read as three PackedInputStream.read calls (first word, table,
+  // segment: the round-2 sequence)
+  {
+    const size_t W = 8u << 20;  // 64 MiB of words
+    Bytes seg(8 * W, 0);
+    uint32_t rs = 777;
+    auto rnd = [&]() { return rs = rs * 1103515245u + 12345u, rs >> 8; };
+    for (size_t w = 0; w < W; ++w)
+      if (rnd() % 2)
+        for (int b = 0; b < 8; ++b) seg[8 * w + b] = (rnd() % 4) ? (uint8_t)(1 + rnd() % 255) : 0;
+    const std::vector<Bytes> msg = {seg};
+    Bytes pk = oracleWrite(msg);
+    EXPECT(SerializePacked::write(gpu, msg) == pk, "64 MiB message: write == oracle");
+    const int reps = 5;
+    double best1 = 1e9, best3 = 1e9;
+    for (int r = 0; r < reps; ++r) {
+      ArrayInputStream in(pk.data(), pk.size());
+      const auto t0 = std::chrono::steady_clock::now();
+      auto got = SerializePacked::read(gpu, in);
+      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      best1 = dt < best1 ? dt : best1;
+      EXPECT(got.size() == 1 && got[0] == seg && in.remaining() == 0, "64 MiB message: read == oracle input");
+      ArrayInputStream in3(pk.data(), pk.size());
+      PackedInputStream pin(gpu, in3);
+      Bytes first(8), out(8 * W);
+      const auto t1 = std::chrono::steady_clock::now();
+      pin.read(first.data(), 8);  // (count 1: no second table read)
+      pin.read(out.data(), out.size());
+      const double dt3 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+      best3 = dt3 < best3 ? dt3 : best3;
+      EXPECT(out == seg, "64 MiB message: per-read sequence");
+    }
+    std::printf("read 64 MiB single-segment message (%.1f MiB packed): one call %.2f ms = %.2f GiB/s of words; "
+                "per-read calls %.2f ms = %.2f GiB/s\n",
+                pk.size() / 1048576.0, best1 * 1e3, 8.0 * W / best1 / (1 << 30), best3 * 1e3,
+                8.0 * W / best3 / (1 << 30));
   }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);

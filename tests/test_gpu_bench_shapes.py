@@ -138,3 +138,34 @@ def test_sparse_messages_multi_round(ctx, oracle):
     assert int((d_mst != 0).sum().item()) == 0 and int((d_ss != 0).sum().item()) == 0
     assert np.array_equal(d_sw.cpu().numpy().astype(np.uint64), swo)
     assert np.array_equal(d_out[:words].cpu().numpy().view(np.uint8), host)
+
+
+@pytest.mark.parametrize("config,segments", [(2, 4096), (3, 512)])
+def test_bench_two_ranks_same_device(config, segments):
+    """bench.py's real GPU rank path at N = 2 (config 5 readiness) on a
+    one-GPU box: both ranks on cuda:0 with a gloo group (--same-device; RCCL
+    refuses two ranks on one GPU).  Shard planning, per-rank generation, the
+    barrier-bracketed timing and the max/sum reduction are the code the
+    8-GPU run takes; both shards must round-trip bit-exact and rank 0's
+    oracle sample must equal the device bytes."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2", "--same-device",
+                          "--config", str(config), "--segments", str(segments), "--steps", "3",
+                          "--warmup", "1", "--no-cpu", "--sample-check", "16"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    print(json.dumps(line))
+    assert line["n_gpus"] == 2 and line["per_rank"]["backend"] == "gloo"
+    assert line["parity"]["mismatched_words_plus_bad_status"] == 0
+    assert line["parity"]["oracle_sample_equal"] is True
+    per = 8 * 8192 * segments if config == 2 else None
+    if per:
+        assert line["per_rank"]["unpacked_bytes_total"] == 2 * per
+    assert line["value"] > 0

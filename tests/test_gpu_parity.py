@@ -653,3 +653,22 @@ def test_message_host_forms(ctx, oracle, chunk_kb, monkeypatch):
         ost = oracle.ETRAILING
     assert st[7] == ost and ost != oracle.OK
     assert all(st[i] == 0 and got[i] == msgs[i] for i in range(len(msgs)) if i != 7)
+
+
+@pytest.mark.parametrize("chunk_kb", [None, "4"])
+def test_message_host_forms_all_broken(ctx, oracle, chunk_kb, monkeypatch):
+    """A batch made only of broken messages (no segment anywhere): the
+    sizing call has no segment array and must still return the statuses
+    (it wrote the segment offsets through NULL)."""
+    if chunk_kb:
+        monkeypatch.setenv("CPK_HOST_CHUNK_KB", chunk_kb)
+    for pk, moff in [(b"\x0f", [0, 1]),
+                     (b"\x0f" * 4, [0, 1, 2, 3, 4]),
+                     (b"\x01\x05" * 3000, list(range(0, 6001, 2)))]:
+        st, got = ctx.decode_messages_host(pk, np.array(moff, np.uint64))
+        for i in range(len(moff) - 1):
+            ost, _, used = oracle.read_message(pk[moff[i]: moff[i + 1]])
+            if ost == oracle.OK and used != moff[i + 1] - moff[i]:
+                ost = oracle.ETRAILING
+            assert ost != oracle.OK and st[i] == ost, (i, st[i], ost)
+            assert got[i] == []
