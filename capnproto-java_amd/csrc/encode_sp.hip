@@ -1,9 +1,9 @@
 // encode_sp.hip -- single-pass encoder (the default).  Included from
 // packed_codec.hip (namespace cpk); uses encode_v4.hip's e4_tag.
 //
-// One 256-thread workgroup per piece, pieces taken in order from a ticket,
-// the piece held in VGPRs: wave w owns the 64-word steps [32w, 32w + 32) of an
-// 8192-word chunk, lane = word.  Per piece:
+// One 256-thread workgroup per chunk of a piece (a unit, below), units taken
+// in order from a ticket, the chunk held in VGPRs: wave w owns the 64-word
+// steps [32w, 32w + 32) of the 8192-word chunk, lane = word.  Per unit:
 //   A1  load the wave's steps (32 x 8 B per lane, all in flight); per word the
 //       nonzero-byte tag m (PackedOutputStream.java:64-117; kept packed four
 //       per VGPR); per step the Z / DL / D ballots (zero word, <= 1 zero
@@ -17,15 +17,16 @@
 //       earlier steps' masks.  The packed bytes of the wave follow from
 //       popcounts.  tools/step_model.py is this algebra in Python, checked
 //       against the oracle (tests/test_step_model.py);
-//   look-back  the piece's size is published and its offset found by a
-//       decoupled look-back over the pieces before it (epoch-tagged 8-byte
+//   look-back  the unit's size is published and its offset found by a
+//       decoupled look-back over the units before it (epoch-tagged 8-byte
 //       status words);
 //   B   each word's string (tag + v_perm-compacted bytes + count, or the 8
 //       bytes of a literal-run member) OR-ed into a per-wave LDS ring at its
 //       offset from a wave scan; complete 16-byte lines stream out.
-// Traffic U + P: the piece is read once.  A piece over one chunk is sized
-// chunk by chunk (run state carried from chunk to chunk), then read again
-// and emitted: 2U + P for those pieces only.
+// Work is ticketed per chunk of 8192 words ("unit"): a piece over one chunk
+// is several units, each emitting its own bytes, the run state handed from
+// chunk to chunk (the state a chunk leaves is published for the next);
+// every unit is read once: traffic U + P for any mix of piece sizes.
 
 #ifndef CPK_SP_WAVES
 #define CPK_SP_WAVES 4
@@ -773,12 +774,6 @@ __device__ uint64_t sp_lookback(uint64_t *status, uint32_t p, uint64_t agg, uint
   return excl;
 }
 
-__device__ __forceinline__ SpSt sp_get_state(const uint64_t *scr, int par) {
-  const uint64_t a = sp_ld(&scr[6 + 2 * par]), b = sp_ld(&scr[7 + 2 * par]);
-  SpSt s = {(uint32_t)a, (uint32_t)(b & 1), (uint32_t)(b >> 1)};
-  return s;
-}
-
 // (stats build: A1 alone into phase slot 7)
 #ifdef CPK_PHASE_STATS
 #define SP_A1_PARAMS , unsigned long long &wph_last, unsigned long long *wph_acc
@@ -789,13 +784,27 @@ __device__ __forceinline__ SpSt sp_get_state(const uint64_t *scr, int par) {
 #define SP_A1_ARGS
 #define SP_A1_STAMP
 #endif
-// One chunk's A1 + A2 for this wave (all waves call it; two barriers).
-// Returns the chunk's packed bytes (all waves); wbefore: bytes of the waves
-// before this one.  cst: the state entering the chunk -> leaving it.
+// run state <-> a look-back value (zl < 2^31, dlo, hd <= 256: 41 bits)
+__device__ __forceinline__ uint64_t sp_pack_state(SpSt s) {
+  return (uint64_t)s.zl | ((uint64_t)s.dlo << 31) | ((uint64_t)s.hd << 32);
+}
+__device__ __forceinline__ SpSt sp_unpack_state(uint64_t v) {
+  SpSt s = {(uint32_t)v & 0x7fffffffu, (uint32_t)(v >> 31) & 1u, (uint32_t)(v >> 32) & 0x1ffu};
+  return s;
+}
+
+// One chunk's A1 + A2 for this wave (all waves call it; two barriers, three
+// when the chunk continues a piece).  Returns the chunk's packed bytes (all
+// waves); wbefore: bytes of the waves before this one.  The state entering
+// the chunk is fresh (a piece's first chunk) or the run state the
+// predecessor chunk of the piece published (prev, epoch-tagged, flag 2),
+// waited for once this chunk's masks are in LDS; the state leaving it is
+// published at next when the piece continues.
 __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restrict__ pw, uint32_t W,
-                                             uint32_t c, uint64_t *msk, uint64_t *scr, SpSt &cst,
-                                             int w, int lane, bool kEmit, int &cnt, uint32_t &Xlast,
-                                             uint64_t &wbefore, uint64_t &wmine SP_A1_PARAMS) {
+                                             uint32_t c, uint64_t *msk, uint64_t *scr, uint64_t *prev,
+                                             uint64_t *next, uint32_t ep, uint32_t *err, int w, int lane,
+                                             int &cnt, uint32_t &Xlast, uint64_t &wbefore,
+                                             uint64_t &wmine SP_A1_PARAMS) {
   const uint32_t ns = (W + 63) >> 6;
   const uint32_t cs0 = c * kSpCS;
   const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
@@ -814,6 +823,25 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   }
   SP_A1_STAMP
   __syncthreads();  // the chunk's masks in LDS
+  SpSt cst = {0u, 0u, 0u};
+  if (prev) {
+    // the run state entering the chunk: the predecessor chunk (an earlier
+    // ticket, so resident and running) publishes it after its own A2
+    if (threadIdx.x == 0) {
+      uint32_t spins = 0;
+      uint64_t v;
+      while (sp_flag(v = ld_status(prev), ep) != 2u) {
+        if (++spins > (1u << 24)) {  // cannot happen: see above
+          atomicOr(err, 4u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      scr[12] = v & kSpValMask;
+    }
+    __syncthreads();
+    cst = sp_unpack_state(sp_ld(&scr[12]));
+  }
   SpSt st = cst;
   uint32_t bytes = 0;
   const bool last = cnt && sa + cnt == cs;  // this wave holds the chunk's last step
@@ -821,7 +849,7 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
     st = sp_state_at(msk, sa, cst);
     uint32_t nz0 = 0, ndl0 = 0;
     Xlast = 0;
-    if (kEmit) {
+    {
       // the step after the wave's last: in the chunk, or past it (look-ahead)
       uint32_t laz = 0, ladl = 0;
       const uint32_t wend = wfirst + 64u * cnt;
@@ -842,18 +870,16 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
     }
     uint32_t rb = 0;
     if (!sp_a2p(R, cnt, wrem, st, nz0, ndl0, lane, rb)) rb = sp_a2_seq(R, cnt, wrem, st, nz0, ndl0);
-    if (kEmit) sp_xs(R, cnt, Xlast, lane);
+    sp_xs(R, cnt, Xlast, lane);
     bytes = rb + (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)acc), 63);
   }
-  if (last) st = sp_state_at(msk, cs, cst);  // the state leaving the chunk
-  if (lane == 0) {
-    scr[16 + w] = bytes;
-    if (last) {
-      scr[6 + 2 * (c & 1)] = st.zl;
-      scr[7 + 2 * (c & 1)] = (uint64_t)st.dlo | ((uint64_t)st.hd << 1);
-    }
+  if (last && next) {
+    // the state leaving the chunk, for the piece's next chunk
+    st = sp_state_at(msk, cs, cst);
+    if (lane == 0) st_status(next, sp_word(ep, 2u, sp_pack_state(st)));
   }
-  __syncthreads();  // wave bytes and the exit state in LDS
+  if (lane == 0) scr[16 + w] = bytes;
+  __syncthreads();  // wave bytes in LDS
   uint64_t tot = 0;
   wbefore = 0;
   wmine = 0;
@@ -864,19 +890,26 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
     if (q == w) wmine = b;
     tot += b;
   }
-  cst = sp_get_state(scr, c & 1);
   return tot;
 }
 
 // kMsg = false: piece p is words [swo[p], swo[p+1]) of `in`.  kMsg = true:
 // pdesc[2p] = first word (bit 63: of `tin`, the segment tables) and
 // pdesc[2p+1] = words.
+// Units: a ticket is one chunk of kSpCS steps (8192 words) of one piece --
+// utab[u] = piece << 32 | chunk, *nunits of them (utab == nullptr: every
+// piece is one chunk, unit = piece).  Every unit publishes its packed bytes
+// for the decoupled look-back over units, and a chunk that continues a
+// piece takes the run state its predecessor leaves (ustate[u - 1]), so a
+// large piece is encoded by many workgroups at once and read once (U + P),
+// and no piece waits for a large one before it to be emitted.
 template <bool kMsg>
 __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo,
     const uint64_t *__restrict__ pdesc, const uint64_t *__restrict__ tin, uint32_t n,
     uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status, uint32_t ep,
-    uint32_t *ticket, uint32_t ppt, uint64_t hint, uint32_t *err, const uint64_t *ocapp) {
+    uint32_t *ticket, const uint64_t *__restrict__ utab, const uint64_t *__restrict__ nunits,
+    uint64_t *ustate, uint64_t hint, uint32_t *err, const uint64_t *ocapp) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // a bound on the output buffer's size: sum of 9 w + 1 over the pieces
   // (cpk_packed_bound(w) <= 9 w + 1), + 16
@@ -894,6 +927,7 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
   R.zl = R.zh = R.dll = R.dlh = R.dl_ = R.dh_ = 0;
   R.ozl = R.ozh = R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = 0;
   if (threadIdx.x == 0) scr[11] = 0;  // (LDS holds whatever the last kernel left)
+  const uint32_t nu = utab ? (uint32_t)*nunits : n;
   WPH_INIT
   for (;;) {
     WPH(3)
@@ -901,100 +935,77 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     __syncthreads();
     const uint32_t t = (uint32_t)sp_ld(&scr[0]);
     __syncthreads();  // (scr[0] read by all before the next ticket)
-    const uint64_t pfirst = (uint64_t)t * ppt;
     WPH(0)
-    if (pfirst >= n) break;
-
-    const uint32_t plast = (uint32_t)min(pfirst + ppt, (uint64_t)n);
-    for (uint32_t p = (uint32_t)pfirst; p < plast; ++p) {
-      // an opaque copy of the lane id: nothing lane-dependent is hoisted out
-      // of the piece loop into registers that stay live across it
-      int lane = lane0;
-      asm volatile("" : "+v"(lane));
-      uint64_t w0, W64;
-      const uint64_t *base = in;
-      if (kMsg) {
-        w0 = pdesc[2 * (uint64_t)p];
-        W64 = pdesc[2 * (uint64_t)p + 1];
-        if (w0 >> 63) base = tin;
-        w0 &= ~(1ull << 63);
-      } else {
-        w0 = swo[p];
-        W64 = swo[p + 1] - w0;
-      }
-      bool bad = W64 >= (1ull << 31);
-      if ((bad || (hint && W64 > hint)) && threadIdx.x == 0) atomicOr(err, 1u);
-      const uint32_t W = bad ? 0u : (uint32_t)W64;  // (unsupported: sized 0, output undefined)
-      const uint64_t *pw = base + w0;
-      const uint32_t nch = (((W + 63) >> 6) + kSpCS - 1) / kSpCS;
-      int cnt = 0;
-      uint32_t Xlast = 0;
-      uint64_t wbefore = 0, wmine = 0, total = 0, cbase = 0;
-      SpSt cst = {0u, 0u, 0u};
-      // one chunk: A1, A2, offset, B.  More: every chunk sized (pass 0),
-      // the offset, every chunk read again and emitted (pass 1).  One copy
-      // of each phase in the code (uniform branches).
-      const uint32_t iters = nch > 1 ? 2 * nch : 1;
-      for (uint32_t it = 0; it < iters; ++it) {
-        const bool emit = nch <= 1 || it >= nch;
-        const uint32_t c = nch > 1 ? (emit ? it - nch : it) : 0;
-        if (emit && c == 0) cst = SpSt{0u, 0u, 0u};
-        const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, cst, w, lane, emit, cnt, Xlast, wbefore, wmine SP_A1_ARGS);
-        WPH(1)
-        if (!emit) {
-          total += ct;
-          continue;
-        }
-        if (c == 0 && nch <= 1) total = ct;
-        if (c == 0 && w == 0 && lane == 0) {
-          // the piece's size, published before its strings are laid out: the
-          // pieces after it find it there when they look back
-          st_status(&status[p], sp_word(ep, p == 0 ? 2u : 1u, total));
-        }
-        WPH(2)
-        if (cnt) {
-          // the offset: known past chunk 0; for chunk 0 the look-back (wave 0)
-          // runs once the waves have laid out kSpDefer steps
-          auto getbase = [&]() -> uint64_t {
-            WPH(4)
-            if (w == 0) {
-              const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
-              if (lane == 0) {
-                scr[5] = excl;
-                out_off[p] = excl;
-                if (p + 1 == n) out_off[n] = excl + total;
-                __builtin_amdgcn_s_waitcnt(0xc07f);  // (the offset before the flag)
-                scr[11] = (uint64_t)p + 1;
-              }
-              WPH(5)
-              return excl + wbefore;
-            }
-            while ((uint32_t)sp_ld(&scr[11]) != p + 1) __builtin_amdgcn_s_sleep(1);
-            WPH(6)
-            return sp_ld(&scr[5]) + wbefore;
-          };
-          sp_b(R, cnt, lut, ring, out, c != 0, CPK_SP_FITS_WAVES(w) && wmine + 16 <= kSpRing, cbase + wbefore,
-               lane, ocap, getbase);
-        } else if (c == 0 && w == 0) {
-          // wave 0 runs the look-back even without steps (an empty piece)
-          const uint64_t excl = sp_lookback(status, p, total, ep, err, lane);
-          if (lane == 0) {
-            scr[5] = excl;
-            out_off[p] = excl;
-            if (p + 1 == n) out_off[n] = excl + total;
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            scr[11] = (uint64_t)p + 1;
-          }
-        }
-        if (c == 0) {
-          // (every wave knows the piece's offset from here on)
-          while ((uint32_t)sp_ld(&scr[11]) != p + 1) __builtin_amdgcn_s_sleep(1);
-          cbase = sp_ld(&scr[5]);
-        }
-        cbase += ct;
-        WPH(4)
-      }
+    if (t >= nu) break;
+    const uint64_t ud = utab ? utab[t] : (uint64_t)t << 32;
+    const uint32_t p = (uint32_t)(ud >> 32), c = (uint32_t)ud;
+    // an opaque copy of the lane id: nothing lane-dependent is hoisted out
+    // of the unit loop into registers that stay live across it
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    uint64_t w0, W64;
+    const uint64_t *base = in;
+    if (kMsg) {
+      w0 = pdesc[2 * (uint64_t)p];
+      W64 = pdesc[2 * (uint64_t)p + 1];
+      if (w0 >> 63) base = tin;
+      w0 &= ~(1ull << 63);
+    } else {
+      w0 = swo[p];
+      W64 = swo[p + 1] - w0;
     }
+    bool bad = W64 >= (1ull << 31) || (!utab && W64 > 64ull * kSpCS);
+    if ((bad || (hint && W64 > hint)) && threadIdx.x == 0 && c == 0) atomicOr(err, 1u);
+    const uint32_t W = bad ? 0u : (uint32_t)W64;  // (unsupported: sized 0, output undefined)
+    const uint64_t *pw = base + w0;
+    const uint32_t nch = max((((W + 63) >> 6) + kSpCS - 1) / kSpCS, 1u);
+    const bool lastc = c + 1 >= nch;  // (the piece's last chunk)
+    int cnt = 0;
+    uint32_t Xlast = 0;
+    uint64_t wbefore = 0, wmine = 0;
+    const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, c ? ustate + (t - 1) : nullptr,
+                                 lastc ? nullptr : ustate + t, ep, err, w, lane, cnt, Xlast, wbefore,
+                                 wmine SP_A1_ARGS);
+    WPH(1)
+    if (w == 0 && lane == 0) {
+      // the unit's size, published before its strings are laid out: the
+      // units after it find it there when they look back
+      st_status(&status[t], sp_word(ep, t == 0 ? 2u : 1u, ct));
+    }
+    WPH(2)
+    // the offset: the look-back (wave 0) runs once the waves have laid out
+    // kSpDefer steps (or all of them, when they fit the ring)
+    auto getoff = [&]() {
+      const uint64_t excl = sp_lookback(status, t, ct, ep, err, lane);
+      if (lane == 0) {
+        scr[5] = excl;
+        if (c == 0) out_off[p] = excl;
+        if (p + 1 == n && lastc) out_off[n] = excl + ct;
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // (the offset before the flag)
+        scr[11] = (uint64_t)t + 1;
+      }
+      return excl;
+    };
+    if (cnt) {
+      auto getbase = [&]() -> uint64_t {
+        WPH(4)
+        if (w == 0) {
+          const uint64_t excl = getoff();
+          WPH(5)
+          return excl + wbefore;
+        }
+        while ((uint32_t)sp_ld(&scr[11]) != t + 1) __builtin_amdgcn_s_sleep(1);
+        WPH(6)
+        return sp_ld(&scr[5]) + wbefore;
+      };
+      sp_b(R, cnt, lut, ring, out, false, CPK_SP_FITS_WAVES(w) && wmine + 16 <= kSpRing, wbefore, lane, ocap,
+           getbase);
+    } else if (w == 0) {
+      getoff();  // wave 0 runs the look-back even without steps (an empty piece)
+    }
+    // (no wave takes the next ticket before the unit's offset is out: scr[5])
+    while ((uint32_t)sp_ld(&scr[11]) != t + 1) __builtin_amdgcn_s_sleep(1);
+    WPH(4)
   }
   WPH_FLUSH(32)
 }
@@ -1024,4 +1035,23 @@ __global__ void sp_msg_prep_kernel(const uint64_t *__restrict__ swo, const uint6
     d[2 * (1 + s - s0)] = swo[s];
     d[2 * (1 + s - s0) + 1] = swo[s + 1] - swo[s];
   }
+}
+
+// Units of the single-pass encoder (sp_encode_kernel): a piece of W words is
+// max(1, ceil(W / 8192)) units, one per chunk.  ucnt[p] = its unit count
+// (scanned into ustart by the e4 scan kernels), then utab[ustart[p] + k] =
+// p << 32 | k.
+__global__ void sp_units_count_kernel(const uint64_t *__restrict__ swo, const uint64_t *__restrict__ pdesc,
+                                      uint32_t n, uint64_t *__restrict__ ucnt) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint64_t W = pdesc ? pdesc[2 * (uint64_t)p + 1] : swo[p + 1] - swo[p];
+  const uint64_t steps = (W + 63) >> 6;
+  ucnt[p] = steps > (uint64_t)kSpCS ? (steps + kSpCS - 1) / kSpCS : 1;
+}
+__global__ void sp_units_fill_kernel(const uint64_t *__restrict__ ustart, uint32_t n, uint64_t *__restrict__ utab) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint64_t a = ustart[p], b = ustart[p + 1];
+  for (uint64_t k = a; k < b; ++k) utab[k] = ((uint64_t)p << 32) | (k - a);
 }

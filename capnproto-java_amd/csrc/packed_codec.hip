@@ -7,13 +7,20 @@
 //   (PackedOutputStream.java:36-43 re-initialises all run state per call).
 //
 // Design (DESIGN.md has the full derivation and the rooflines):
-//   encoder        encode_v4.hip: one wave per piece, a size pass, a scan of
-//                  the sizes, an emit pass (tag + v_perm-compacted bytes +
-//                  count per word into an LDS ring, 16-byte line stores).
-//   decode_kernel  one wave per piece: packed bytes staged in LDS window by
-//                  window, the tag chain found by speculative per-lane walks
-//                  with pointer-doubling validation, then a gather-expand of
-//                  every 4-word output block from its covering record.
+//   encoders       encode_sp.hip (single pass, the default for like-sized
+//                  pieces and small batches): a workgroup per 8192-word chunk,
+//                  the chunk in VGPRs, roles by mask algebra, a decoupled
+//                  look-back for the offsets, strings (tag + v_perm-compacted
+//                  bytes + count) OR-ed into an LDS ring, 16-byte line
+//                  stores; encode_v4.hip (two passes, mixed-size batches):
+//                  one wave per piece, a size pass, a scan, an emit pass.
+//   decoders       decode_kernel: one wave per piece, packed bytes staged in
+//                  LDS window by window, the tag chain found by speculative
+//                  per-lane walks with pointer-doubling validation, then a
+//                  gather-expand of every 4-word output block from its
+//                  covering record; decode_v2.hip (sparse batches): a record
+//                  index per window instead of the block map;
+//                  stream_split.hip: one long stream cut into blocks.
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include <stdint.h>
@@ -1061,8 +1068,13 @@ constexpr uint32_t kRmHead = 257;              // table words at most (512 segme
 constexpr uint32_t kRmPieces = 2 + 512;        // first word, rest of the table, segments
 constexpr uint32_t kRmInfo = 4 + 513;          // status, consumed, count, words, offsets
 
+// sdesc: the one-wave decoder's stream descriptor (DecStreams with one
+// stream): [0] its first byte, [1] its end, [2..3] its pieces (the table's
+// two and the segments only: the padding is the parallel path's); [5] the
+// parallel path's piece count
 __global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit,
-                                uint64_t cap_words, uint64_t *__restrict__ swo, uint64_t *__restrict__ info) {
+                                uint64_t cap_words, uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
+                                uint64_t *__restrict__ sdesc) {
   if (threadIdx.x != 0) return;
   uint64_t ip = 0, total = 0;
   uint32_t count = 0;
@@ -1089,16 +1101,22 @@ __global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t ava
     swo[1] = swo[2] = 0;
   }
   for (uint32_t i = (st == CPK_OK ? count : 0) + 3; i <= kRmPieces; ++i) swo[i] = w;
+  sdesc[0] = 0;
+  sdesc[1] = avail;
+  sdesc[2] = 0;
+  sdesc[3] = st == CPK_OK ? count + 2 : 0;
+  sdesc[5] = kRmPieces;  // (the parallel path decodes every piece)
 }
 
 // the message's status: its table's, else the stream's (a failed piece
 // stops the stream: the last piece carries it); the bytes consumed
-__global__ void rm_final_kernel(const uint64_t *__restrict__ in_off, const int32_t *__restrict__ pstatus,
-                                uint64_t *__restrict__ info) {
+// (end: where the stream's pieces ended; npieces: how many were decoded)
+__global__ void rm_final_kernel(const uint64_t *__restrict__ end, const int32_t *__restrict__ pstatus,
+                                const uint64_t *__restrict__ npieces, uint64_t *__restrict__ info) {
   if (threadIdx.x != 0 || (int64_t)info[0] != CPK_OK) return;
-  const int32_t st = pstatus[kRmPieces - 1];
+  const int32_t st = pstatus[*npieces - 1];
   info[0] = (uint64_t)(int64_t)st;
-  info[1] = st == CPK_OK ? in_off[kRmPieces] : 0;
+  info[1] = st == CPK_OK ? *end : 0;
 }
 
 // ---- message write: Serialize.write = table piece + segment pieces --------
@@ -1287,6 +1305,8 @@ struct cpk_ctx_s {
   uint64_t *ss_buf;       // parallel stream decode scratch (stream_split.hip)
   uint64_t ss_cap;        //   u64 entries
   uint64_t *rm_buf;       // cpk_read_message: piece word offsets | piece ends | statuses (lazy)
+  uint64_t *sp_units;     // single pass, pieces over one chunk: unit counts | starts | block sums | unit table
+  uint64_t sp_units_cap;  //   u64 entries
 };
 
 namespace {
@@ -1405,6 +1425,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->sp_desc) hipFree(ctx->sp_desc);
   if (ctx->ss_buf) hipFree(ctx->ss_buf);
   if (ctx->rm_buf) hipFree(ctx->rm_buf);
+  if (ctx->sp_units) hipFree(ctx->sp_units);
   pipe_destroy(ctx->pipe);
   free(ctx);
 }
@@ -1412,28 +1433,29 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
 int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
 
 // Single-pass encoder (encode_sp.hip): one launch, the look-back words
-// epoch-tagged (cleared only when the epoch wraps or the array grows).
-// The single-pass encoder takes batches of like-sized pieces of 1024-8192
-// words: its ordered look-back makes every piece wait for the size of the
-// pieces before it, which a larger piece publishes late (sized chunk by
-// chunk) and tiny pieces each cost a workgroup round -- mixed 4-256 KiB
-// segments measured 2.4x slower than the two-pass encoder, mixed 4-64 KiB
-// 2.2x, uniform 64 KiB 14 % faster.  sp_takes screens the bound; the
-// device then checks the sizes themselves (e4_gate_kernel).
+// epoch-tagged (cleared only when the epoch wraps or the array grows).  Work
+// is ticketed per 8192-word chunk of a piece (a unit); a batch whose pieces
+// may be larger than one chunk (the hint) first gets its unit table (three
+// small kernels and the e4 scan, no host sync: the unit count stays on the
+// device).  sp_takes screens which batches it takes; cpk_encode_batch lets
+// the device choose by the piece sizes (e4_gate_kernel).
 static bool sp_takes(cpk_ctx ctx, uint64_t max_seg_words) {
   if (ctx->encoder == 0) return true;  // (CPK_ENCODER=0: single pass for every batch)
   return ctx->encoder != 4 && max_seg_words != 0 && max_seg_words <= 64ull * cpk::kSpCS;
 }
 
+// `units`: a bound on the batch's units when its pieces may exceed one
+// chunk (0: every piece is one unit)
 int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64_t *pdesc,
               const uint64_t *tin, uint32_t n, uint64_t hint, void *d_out, uint64_t *d_out_off,
-              hipStream_t s, bool gated = false) {
+              hipStream_t s, bool gated = false, uint64_t units = 0) {
+  const uint64_t ucap = units ? units : n;  // look-back words (+ as many run-state words)
   bool fresh = false;
-  if (n > ctx->sp_cap) {
+  if (2 * ucap > ctx->sp_cap) {
     if (ctx->sp_status) hipFree(ctx->sp_status);
     ctx->sp_status = nullptr;
     ctx->sp_cap = 0;
-    const uint64_t cap = n < 4096 ? 4096 : (uint64_t)n + n / 4;
+    const uint64_t cap = 2 * ucap < 8192 ? 8192 : 2 * ucap + ucap / 2;
     if (hipMalloc(&ctx->sp_status, cap * 8) != hipSuccess) return CPK_ENOMEM;
     ctx->sp_cap = cap;
     fresh = true;
@@ -1443,13 +1465,35 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
     fresh = true;
   }
   if (fresh && hipMemsetAsync(ctx->sp_status, 0, ctx->sp_cap * 8, s) != hipSuccess) return CPK_EDEVICE;
+  uint64_t *ustate = ctx->sp_status + ucap;
+  const uint64_t *utab = nullptr, *nunits = nullptr;
+  if (units) {
+    // unit counts -> starts (e4 scan) -> unit table
+    const uint32_t nb = (uint32_t)((n + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
+    const uint64_t need = (uint64_t)n + (n + 1) + nb + 1 + units;
+    if (need > ctx->sp_units_cap) {
+      if (ctx->sp_units) hipFree(ctx->sp_units);
+      ctx->sp_units = nullptr;
+      ctx->sp_units_cap = 0;
+      const uint64_t cap = need + need / 4;
+      if (hipMalloc(&ctx->sp_units, cap * 8) != hipSuccess) return CPK_ENOMEM;
+      ctx->sp_units_cap = cap;
+    }
+    uint64_t *ucnt = ctx->sp_units, *ustart = ucnt + n, *bsum = ustart + (n + 1), *tab = bsum + nb + 1;
+    const unsigned tb = 256, tg = (n + tb - 1) / tb;
+    hipLaunchKernelGGL(cpk::sp_units_count_kernel, dim3(tg), dim3(tb), 0, s, d_swo, pdesc, n, ucnt);
+    hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s, (const uint64_t *)ucnt, n,
+                       bsum);
+    hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bsum, nb);
+    hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s, (const uint64_t *)ucnt, n,
+                       (const uint64_t *)bsum, ustart);
+    hipLaunchKernelGGL(cpk::sp_units_fill_kernel, dim3(tg), dim3(tb), 0, s, (const uint64_t *)ustart, n, tab);
+    utab = tab;
+    nunits = ustart + n;
+  }
   // (gated: the ticket was set by e4_gate_kernel -- exhausted unless the
   // batch is the single pass's)
   if (!gated && hipMemsetAsync(ctx->tickets + cpk::kTkPlan, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
-  // one piece per ticket: a workgroup holding two pieces would publish the
-  // second's size only after emitting the first, and the pieces after it
-  // would wait on that (a serial chain through the tickets)
-  const uint32_t ppt = 1u;
   if (cpk::kSpLds > 65536) {  // (more than the default dynamic LDS limit)
     static bool attr = false;
     if (!attr) {
@@ -1461,19 +1505,26 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
     }
   }
   unsigned grid = (unsigned)(CPK_SP_WPE * ctx->cus);
-  const uint64_t tickets = ((uint64_t)n + ppt - 1) / ppt;
-  if (grid > tickets) grid = (unsigned)tickets;
+  if (grid > ucap) grid = (unsigned)ucap;
   if (pdesc)
     hipLaunchKernelGGL(cpk::sp_encode_kernel<true>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
-                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, ppt, hint,
+                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
                        ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr);
   else
     hipLaunchKernelGGL(cpk::sp_encode_kernel<false>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
-                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, ppt, hint,
+                       ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
                        ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr);
   return hip_ok(hipGetLastError());
+}
+
+// a bound on the units of n pieces of at most `hint` words (0: every piece
+// one unit); over 2^32 units: unsupported
+static uint64_t sp_unit_bound(uint64_t n, uint64_t hint) {
+  if (hint <= 64ull * cpk::kSpCS) return 0;
+  const uint64_t per = (hint + 64ull * cpk::kSpCS - 1) / (64ull * cpk::kSpCS);
+  return n * per;
 }
 
 // Encoder v4 (encode_v4.hip): size pass, scan, emit pass.  Pieces of any
@@ -1548,9 +1599,10 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
   if (nm == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
   const uint64_t np = (uint64_t)nm + nseg;  // pieces: a table per message + the segments
   if (np > 0xffffffffull) return CPK_EINVAL;
-  if (ctx->encoder == 0) {
-    // single pass (forced; the segment tables make a message batch one of
-    // mixed sizes, which the two passes handle faster): piece descriptors in
+  if (ctx->encoder == 0 || (ctx->encoder != 4 && np <= 1024)) {
+    // single pass (forced, or a small batch -- one SerializePacked.write:
+    // two launches instead of the two passes' nine; a large batch of mixed
+    // sizes takes the two passes, faster there): piece descriptors in
     // message order + the tables' words
     const uint64_t need = 2 * np + (uint64_t)nseg / 2 + nm + 2;
     if (need > ctx->sp_desc_cap) {
@@ -1566,7 +1618,10 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
     const unsigned tb = 256, tg = (nm + tb - 1) / tb;
     hipLaunchKernelGGL(cpk::sp_msg_prep_kernel, dim3(tg), dim3(tb), 0, s, d_swo, d_msg_seg_off, nm, pdesc,
                        tbuf, tbuf - 1);
-    return sp_launch(ctx, d_in, nullptr, pdesc, tbuf, (uint32_t)np, max_seg_words, d_out, d_out_off, s);
+    // (tables are at most 257 words: the segments' hint bounds the units)
+    const uint64_t ub = sp_unit_bound(np, max_seg_words);
+    if (ub > 0xffffffffull) return CPK_EUNSUPPORTED;
+    return sp_launch(ctx, d_in, nullptr, pdesc, tbuf, (uint32_t)np, max_seg_words, d_out, d_out_off, s, false, ub);
   }
   const uint32_t nb = (uint32_t)((np + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
   // scratch: segment sizes | table sizes | message-order sizes | segment offsets | block sums
@@ -1619,7 +1674,22 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
   if (!sp_takes(ctx, max_seg_words)) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
-  if (ctx->encoder == 0) return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s);
+  if (ctx->encoder == 0) {
+    // (forced single pass: pieces of any size, several units for a large one)
+    uint64_t hint = max_seg_words;
+    if (!hint) {  // (no bound given: the batch's words bound every piece)
+      uint64_t ends[2];
+      if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return CPK_EDEVICE;
+      hint = ends[1] - ends[0];
+    }
+    uint64_t ub = sp_unit_bound(n, hint);
+    if (hint > 64ull * cpk::kSpCS && !max_seg_words) ub = n + hint / (64ull * cpk::kSpCS) + 1;
+    if (ub > 0xffffffffull) return CPK_EUNSUPPORTED;
+    return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s, false, ub);
+  }
   // by piece size: both enqueued, the device picks one (e4_gate_kernel)
   int rc = e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s, true);
   if (rc) return rc;
@@ -1826,28 +1896,35 @@ int cpk_read_message(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t
   if (((uintptr_t)d_packed & 15) || ((uintptr_t)d_out & 7)) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
-  if (!ctx->rm_buf && hipMalloc(&ctx->rm_buf, (2 * (kRmPieces + 1) + kRmPieces / 2) * 8ull) != hipSuccess)
+  // swo [515] | in_off [515] | statuses [514 x i32] | stream descriptor [4] | stream end [1] | pieces [1]
+  if (!ctx->rm_buf && hipMalloc(&ctx->rm_buf, (2 * (kRmPieces + 1) + kRmPieces / 2 + 8) * 8ull) != hipSuccess)
     return CPK_ENOMEM;
   uint64_t *swo = ctx->rm_buf, *in_off = swo + kRmPieces + 1;
   int32_t *pst = (int32_t *)(in_off + kRmPieces + 1);
+  uint64_t *sdesc = in_off + kRmPieces + 1 + kRmPieces / 2, *send_out = sdesc + 4, *npad = sdesc + 5;
   hipLaunchKernelGGL(cpk::rm_table_kernel, dim3(1), dim3(64), 0, s, (const uint8_t *)d_packed, avail,
-                     traversal_limit_words, out_cap_words, swo, d_info);
+                     traversal_limit_words, out_cap_words, swo, d_info, sdesc);
   // the pieces' sizes are on the device only: the stream decoder is sized by
   // the bytes the caller's capacity can reach (10 per word at most)
   const uint64_t reach = ss_reach(avail, out_cap_words + cpk::kRmHead);
   int rc;
-  if (reach >= kSsMin && !getenv("CPK_STREAM_ONE_WAVE")) {
+  const bool par = reach >= kSsMin && !getenv("CPK_STREAM_ONE_WAVE");
+  if (par) {
+    // every piece, the padding included, gets a status; the last carries the stream's
     rc = ss_decode(ctx, (const uint8_t *)d_packed, avail, reach, swo, kRmPieces, (uint64_t *)d_out, in_off, pst, s);
   } else {
+    // one wave over the table's pieces and the segments (the piece count is
+    // on the device: a one-stream descriptor), none of the padding
     if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
       return CPK_EDEVICE;
     dec_launch(ctx, true, 1, (const uint8_t *)d_packed, in_off, swo, kRmPieces, (uint64_t *)d_out, pst, avail,
-               cpk::DecStreams{nullptr, nullptr, nullptr, 1, in_off + kRmPieces}, s);
+               cpk::DecStreams{sdesc, sdesc + 1, sdesc + 2, 1, send_out}, s);
     rc = hip_ok(hipGetLastError());
   }
   if (rc) return rc;
-  hipLaunchKernelGGL(cpk::rm_final_kernel, dim3(1), dim3(64), 0, s, (const uint64_t *)in_off,
-                     (const int32_t *)pst, d_info);
+  hipLaunchKernelGGL(cpk::rm_final_kernel, dim3(1), dim3(64), 0, s, par ? (const uint64_t *)(in_off + kRmPieces)
+                                                                        : (const uint64_t *)send_out,
+                     (const int32_t *)pst, par ? (const uint64_t *)npad : (const uint64_t *)(sdesc + 3), d_info);
   return hip_ok(hipGetLastError());
 }
 

@@ -29,6 +29,7 @@
 package org.capnproto.gpu;
 
 import java.io.IOException;
+import java.lang.ref.WeakReference;
 import java.nio.ByteBuffer;
 import java.nio.channels.ReadableByteChannel;
 import java.nio.channels.WritableByteChannel;
@@ -275,22 +276,39 @@ public final class GpuDispatch {
      *  reads from, and what the reference path reads when bytes were carried.
      *  Direct memory (passed to JNI zero-copy), grown by doubling. */
     static final class Source implements org.capnproto.BufferedInputStream {
-        private final org.capnproto.BufferedInputStream upstream;   // or
-        private final ReadableByteChannel channel;
+        // (weak: the map's value must not keep its key alive -- the entry
+        // goes when the caller drops the stream or channel)
+        private final WeakReference<org.capnproto.BufferedInputStream> upstreamRef;   // or
+        private final WeakReference<ReadableByteChannel> channelRef;
+        private final boolean isChannel;
         ByteBuffer buf;   // [position, limit): bytes not yet consumed
 
         Source(org.capnproto.BufferedInputStream upstream) {
-            this.upstream = upstream;
-            this.channel = null;
+            this.upstreamRef = new WeakReference<>(upstream);
+            this.channelRef = null;
+            this.isChannel = false;
             this.buf = PackedGpu.directBuffer(1 << 16);
             this.buf.limit(0);
         }
 
         Source(ReadableByteChannel channel) {
-            this.upstream = null;
-            this.channel = channel;
+            this.upstreamRef = null;
+            this.channelRef = new WeakReference<>(channel);
+            this.isChannel = true;
             this.buf = PackedGpu.directBuffer(1 << 16);
             this.buf.limit(0);
+        }
+
+        private org.capnproto.BufferedInputStream upstream() throws IOException {
+            org.capnproto.BufferedInputStream u = upstreamRef.get();
+            if (u == null) throw new IOException("stream closed");
+            return u;
+        }
+
+        private ReadableByteChannel channel() throws IOException {
+            ReadableByteChannel c = channelRef.get();
+            if (c == null) throw new IOException("channel closed");
+            return c;
         }
 
         /** Room for `more` bytes after the limit: compact, or grow by doubling. */
@@ -317,7 +335,8 @@ public final class GpuDispatch {
          *  (BufferedInputStreamWrapper.java:98-108).  True if the read filled
          *  all the room it was offered (more may be ready). */
         boolean fill() throws IOException {
-            if (channel != null) {
+            if (isChannel) {
+                ReadableByteChannel channel = channel();
                 reserve(8192);
                 int lim = buf.limit();
                 ByteBuffer w = buf.duplicate();
@@ -331,7 +350,7 @@ public final class GpuDispatch {
                 buf.limit(lim + n);
                 return n == offered;
             }
-            ByteBuffer src = upstream.getReadBuffer();   // DecodeException at EOF
+            ByteBuffer src = upstream().getReadBuffer();   // DecodeException at EOF
             int n = src.remaining();
             if (n == 0) throw new org.capnproto.DecodeException("premature EOF");
             reserve(n);
@@ -367,13 +386,15 @@ public final class GpuDispatch {
 
         @Override
         public boolean isOpen() {
-            return channel != null ? channel.isOpen() : upstream.isOpen();
+            Object o = isChannel ? channelRef.get() : upstreamRef.get();
+            return o != null && (isChannel ? ((ReadableByteChannel) o).isOpen()
+                                           : ((org.capnproto.BufferedInputStream) o).isOpen());
         }
 
         @Override
         public void close() throws IOException {
-            if (channel != null) channel.close();
-            else upstream.close();
+            if (isChannel) channel().close();
+            else upstream().close();
         }
     }
 }

@@ -50,3 +50,17 @@ def ctx(request):
                 os.environ[k] = v
     yield c
     c.close()
+
+
+def pytest_assertrepr_compare(op, left, right):
+    """Short report for unequal large byte strings: pytest's default diff
+    of megabytes (difflib) runs for minutes and trips the GPU tests' time
+    limit before the failure is shown."""
+    if op == "==" and isinstance(left, (bytes, bytearray)) and isinstance(right, (bytes, bytearray)) \
+            and max(len(left), len(right)) > 4096:
+        n = min(len(left), len(right))
+        first = next((i for i in range(n) if left[i] != right[i]), n)
+        return [f"byte strings differ: lengths {len(left)} / {len(right)}, first difference at byte {first}",
+                f"left[{first}:{first + 16}] = {bytes(left[first:first + 16]).hex()}",
+                f"right[{first}:{first + 16}] = {bytes(right[first:first + 16]).hex()}"]
+    return None

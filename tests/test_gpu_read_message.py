@@ -20,7 +20,10 @@ def _rd(ctx, data: bytes, **kw):
 
 
 def _expect(oracle, data: bytes, limit=8 * 1024 * 1024):
-    st, segs, used = oracle.read_message(data, traversal_limit_words=limit)
+    # (an output capacity for any table, up to a 2^28-word segment: the
+    # oracle's CPK_EINVAL for a short buffer would hide the real status;
+    # the zero pages are never touched beyond the message's words)
+    st, segs, used = oracle.read_message(data, traversal_limit_words=limit, out_cap=(1 << 31) + 4096)
     return st, segs, used
 
 
