@@ -70,6 +70,9 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #ifndef CPK_SP_A1FULL
 #define CPK_SP_A1FULL 1
 #endif
+#ifndef CPK_SP_HCBR
+#define CPK_SP_HCBR 1  // head counts only in steps with heads (a branch per step: -2 % encode)
+#endif
 #ifndef CPK_SP_WPE
 #define CPK_SP_WPE 3  // waves per SIMD the registers must allow (3 workgroups per CU)
 #endif
@@ -192,9 +195,14 @@ __device__ int sp_first_d(const uint64_t *msk, int x, int lim) {
 }
 
 // State entering chunk step s0 from the masks of the steps before it and
-// the chunk's entering state (tools/step_model.py: state_at)
-__device__ SpSt sp_state_at(const uint64_t *msk, int s0, SpSt cst) {
-  if (s0 == 0) return cst;
+// the chunk's entering state (tools/step_model.py: state_at); dep is set
+// when the result used the entering state (a zero run or D/L stretch over
+// every step before s0)
+__device__ SpSt sp_state_at(const uint64_t *msk, int s0, SpSt cst, bool &dep) {
+  if (s0 == 0) {
+    dep = true;
+    return cst;
+  }
   SpSt st = {0u, 0u, 0u};
   const uint64_t Zp = sp_ld(&msk[3 * (s0 - 1)]), DLp = sp_ld(&msk[3 * (s0 - 1) + 1]);
   if (Zp >> 63) {
@@ -207,6 +215,7 @@ __device__ SpSt sp_state_at(const uint64_t *msk, int s0, SpSt cst) {
       z = sp_ld(&msk[3 * q]);
     }
     st.zl = zl + (q >= 0 ? (uint32_t)__builtin_clzll(~z) : cst.zl);
+    dep |= q < 0;
   }
   if (!(DLp >> 63)) return st;
   st.dlo = 1;
@@ -225,6 +234,7 @@ __device__ SpSt sp_state_at(const uint64_t *msk, int s0, SpSt cst) {
   } else {
     h = -(int)cst.hd;
   }
+  dep |= q < 0;
   for (;;) {
     const int h2 = sp_first_d(msk, max(h + 256, 0), P);
     if (h2 >= P) break;
@@ -257,7 +267,7 @@ struct SpRegs {
   uint64_t v[kSpWS];       // the words, step j in v[j]
   uint32_t mp[kSpWS / 4];  // tags, four per register
   uint32_t zl, zh, dll, dlh, dl_, dh_;                 // A1 stash: Z, DL, D (lane = step)
-  uint32_t ozl, ozh, oml, omh, ohl, ohh, oel, oeh;     // A2 stash: ZO, Mem, HC, E
+  uint32_t oml, omh, ohl, ohh, oel, oeh;               // A2 stash: Mem, HC, E
   uint32_t ox;                                         //   X: words past the step to the next run end
 };
 
@@ -311,9 +321,10 @@ __device__ __forceinline__ void sp_put_masks(const SpRegs &R, uint64_t *msk, int
 }
 
 // A2, sequential form (scalar ALU, one step at a time): the roles of the
-// wave's steps from the state entering its first step; stashes ZO (no
-// output: zero-run members, past the end), Mem, HC (heads with a count byte)
-// and E (run ends) at lane = step; returns the steps' packed bytes beyond
+// wave's steps from the state entering its first step; stashes Mem
+// (literal-run members), HC (heads with a count byte) and E (run ends) at
+// lane = step (B needs no mask of the words without output: they are the
+// zero words that are no head); returns the steps' packed bytes beyond
 // their nonzero bytes.  nz0 / ndl0: bit 0 of the step after the wave's last.
 // Used when a D/L stretch longer than 192 words enters a step (a literal run
 // may end inside it); sp_a2p otherwise.
@@ -334,8 +345,6 @@ __device__ __forceinline__ uint32_t sp_a2_seq(SpRegs &R, int cnt, uint32_t wrem,
       d0 = (uint32_t)__builtin_amdgcn_readlane((int)R.dll, j + 1) & 1u;
     }
     const uint64_t E = (Z & ~((Z >> 1) | (z0 << 63))) | (DL & ~((DL >> 1) | (d0 << 63)));
-    R.ozl = sp_wl(R.ozl, (uint32_t)ZO, j);
-    R.ozh = sp_wl(R.ozh, (uint32_t)(ZO >> 32), j);
     R.oml = sp_wl(R.oml, (uint32_t)Mem, j);
     R.omh = sp_wl(R.omh, (uint32_t)(Mem >> 32), j);
     R.ohl = sp_wl(R.ohl, (uint32_t)HC, j);
@@ -416,8 +425,6 @@ __device__ __forceinline__ bool sp_a2p(SpRegs &R, int cnt, uint32_t wrem, SpSt s
                                 __builtin_popcountll(HC))
                    : 0u;
   bytes = (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)b), 63);
-  R.ozl = (uint32_t)ZO;
-  R.ozh = (uint32_t)(ZO >> 32);
   R.oml = (uint32_t)Mem;
   R.omh = (uint32_t)(Mem >> 32);
   R.ohl = (uint32_t)HC;
@@ -571,15 +578,19 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
   // step j's string per lane (s0..s2, nb bytes)
   auto strings = [&](const int j, uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &nb)
       __attribute__((always_inline)) {
-    const uint64_t ZO = sp_rl(R.ozl, R.ozh, j), Mem = sp_rl(R.oml, R.omh, j);
+    const uint64_t Mem = sp_rl(R.oml, R.omh, j);
     const uint64_t HC = sp_rl(R.ohl, R.ohh, j);
     const uint32_t m = (R.mp[j >> 2] >> (8 * (j & 3))) & 0xffu;
     const uint32_t lo = (uint32_t)R.v[j], hi = (uint32_t)(R.v[j] >> 32);
     const uint64_t sel = lut[m];
     const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
     const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
+    const bool zw = m == 0;
     uint32_t cz = 0, cd = 0;
-    if (HC) {
+#if CPK_SP_HCBR
+    if (HC)
+#endif
+    {
       // a head's count: words to its run's end, at most 255 (:119-131, :143-164)
       const uint32_t X = (uint32_t)__builtin_amdgcn_readlane((int)R.ox, j);
       const uint64_t E = sp_rl(R.oel, R.oeh, j);
@@ -590,7 +601,7 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
       const uint32_t z_hi = sp_ffbl((uint32_t)(e >> 32)) | 32u;  // (ctz < 32: | is +)
       const uint32_t tt = min(min(z_lo, z_hi), min(l64 + X, 255u));
       const uint32_t cn = sp_sel(0u, tt, HC);
-      cz = m == 0 ? cn : 0u;
+      cz = zw ? cn : 0u;
       cd = cn - cz;
     }
     // the string: tag, the nonzero bytes, the count after a 0x00 / 0xFF tag
@@ -604,7 +615,10 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     s2 = sp_sel(s2, 0u, Mem);
     nb = (uint32_t)__builtin_popcount(m) + sp_sel(1u, 2u, HC);
     nb = sp_sel(nb, 8u, Mem);
-    nb = sp_sel(nb, 0u, ZO);
+    // no bytes: a zero word that is no head -- a zero-run member, or a word
+    // past the piece's end (A1 left its tag 0, and it is in no mask): the
+    // ZO mask, without its two lane reads
+    nb = sp_sel(zw ? 0u : nb, nb, HC);
   };
   // a string OR-ed into the ring at relative byte p
   auto put = [&](uint32_t p, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t nb) __attribute__((always_inline)) {
@@ -824,6 +838,19 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   SP_A1_STAMP
   __syncthreads();  // the chunk's masks in LDS
   SpSt cst = {0u, 0u, 0u};
+  // the state leaving the chunk depends on the one entering it only when a
+  // zero run or D/L stretch covers the whole chunk: otherwise it is
+  // published now, before this chunk waits for its own entering state, so
+  // the chunks of a piece do not wait on one another in a chain
+  bool early = false;
+  if (next && cnt && sa + cnt == cs) {
+    bool dep = false;
+    const SpSt ex = sp_state_at(msk, cs, cst, dep);
+    if (!dep) {
+      early = true;
+      if (lane == 0) st_status(next, sp_word(ep, 2u, sp_pack_state(ex)));
+    }
+  }
   if (prev) {
     // the run state entering the chunk: the predecessor chunk (an earlier
     // ticket, so resident and running) publishes it after its own A2
@@ -846,7 +873,8 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   uint32_t bytes = 0;
   const bool last = cnt && sa + cnt == cs;  // this wave holds the chunk's last step
   if (cnt) {
-    st = sp_state_at(msk, sa, cst);
+    bool dep_ = false;
+    st = sp_state_at(msk, sa, cst, dep_);
     uint32_t nz0 = 0, ndl0 = 0;
     Xlast = 0;
     {
@@ -873,9 +901,10 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
     sp_xs(R, cnt, Xlast, lane);
     bytes = rb + (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)acc), 63);
   }
-  if (last && next) {
+  if (last && next && !early) {
     // the state leaving the chunk, for the piece's next chunk
-    st = sp_state_at(msk, cs, cst);
+    bool dep_ = false;
+    st = sp_state_at(msk, cs, cst, dep_);
     if (lane == 0) st_status(next, sp_word(ep, 2u, sp_pack_state(st)));
   }
   if (lane == 0) scr[16 + w] = bytes;
@@ -925,7 +954,7 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
   SpRegs R;
   R.zl = R.zh = R.dll = R.dlh = R.dl_ = R.dh_ = 0;
-  R.ozl = R.ozh = R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = 0;
+  R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = 0;
   if (threadIdx.x == 0) scr[11] = 0;  // (LDS holds whatever the last kernel left)
   const uint32_t nu = utab ? (uint32_t)*nunits : n;
   WPH_INIT
