@@ -1774,6 +1774,7 @@ namespace {
 // streams of at least this many bytes (after the bound below) are cut into
 // blocks and decoded in parallel (stream_split.hip); shorter ones by one wave
 constexpr uint64_t kSsMin = 256 * 1024;
+constexpr uint64_t kRmSsMin = 64 * 1024;  // cpk_read_message
 
 // the bytes a stream of `words` words may take: 10 per word at most
 uint64_t ss_reach(uint64_t avail, uint64_t words) {
@@ -1908,7 +1909,9 @@ int cpk_read_message(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t
   // the bytes the caller's capacity can reach (10 per word at most)
   const uint64_t reach = ss_reach(avail, out_cap_words + cpk::kRmHead);
   int rc;
-  const bool par = reach >= kSsMin && !getenv("CPK_STREAM_ONE_WAVE");
+  // (a lower bar than cpk_decode_stream's: a message's one-wave decode is
+  //  ~0.5 GB/s, the parallel path ~250 us of fixed cost: even at 64 KiB)
+  const bool par = reach >= kRmSsMin && !getenv("CPK_STREAM_ONE_WAVE");
   if (par) {
     // every piece, the padding included, gets a status; the last carries the stream's
     rc = ss_decode(ctx, (const uint8_t *)d_packed, avail, reach, swo, kRmPieces, (uint64_t *)d_out, in_off, pst, s);

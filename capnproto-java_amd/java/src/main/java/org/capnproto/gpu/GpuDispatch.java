@@ -46,7 +46,7 @@ public final class GpuDispatch {
 
     /** Messages below this many unpacked bytes take the reference's CPU codec
      *  (default: the crossover measured in INTEGRATION.md). */
-    public static final long DEFAULT_MIN_BYTES = 256L << 10;
+    public static final long DEFAULT_MIN_BYTES = 1L << 20;
     public static final long MIN_BYTES = minBytes();
 
     private static long minBytes() {

@@ -4,7 +4,7 @@ packed stream whose length is not known in advance -- the table read and
 validated on the device, then every segment decoded back to back, in one
 enqueue.  Each case is checked against the oracle's Serialize.read
 (oracle/packed_oracle.c:cpko_read_message): status, segments and the bytes
-consumed; streams of 256 KiB and more take the parallel block path, and the
+consumed; streams reaching 64 KiB and more take the parallel block path, and the
 one-wave decoder (CPK_STREAM_ONE_WAVE=1) must agree with it.
 """
 import os

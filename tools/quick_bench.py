@@ -13,8 +13,14 @@ libs = sys.argv[1:]
 hint = int(__import__("os").environ.get("QB_HINT", __import__("os").environ.get("QB_W", "8192")))  # 0: tiled encoder path
 W = int(__import__("os").environ.get("QB_W", "8192"))  # words per piece
 swo = np.arange(0, (n + 1) * W, W, dtype=np.uint64)
+if __import__("os").environ.get("QB_MIXED"):
+    # config-3 segment sizes (4-256 KiB, bench.CFG3_SEG_WORDS), seeded; W = mean
+    _sz = np.random.default_rng(3).choice([512, 1024, 2048, 4096, 8192, 16384, 32768], size=n).astype(np.uint64)
+    swo = np.concatenate([[0], np.cumsum(_sz)]).astype(np.uint64)
+    hint = 32768
+    W = int(swo[-1]) // n
 d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
-d_in = torch.empty(n * W, dtype=torch.int64, device="cuda")
+d_in = torch.empty(int(swo[-1]), dtype=torch.int64, device="cuda")
 cap = cp.batch_capacity(swo)
 d_pk = torch.empty((cap + 255) // 256 * 256, dtype=torch.uint8, device="cuda")
 d_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
@@ -41,7 +47,7 @@ for cfg in cfgs:
     cp._lib = handles[0][1]
     handles[0][2].generate(cp.preset(cfg), d_swo, d_in)
     torch.cuda.synchronize()
-    U = n * W * 8
+    U = int(swo[-1]) * 8
     print(f"config {cfg}: n={n}", flush=True)
     for name, L, ctx in handles:
         cp._lib = L
@@ -55,7 +61,7 @@ for cfg in cfgs:
             if rnd:
                 te.append(e[0].elapsed_time(e[1])); td.append(e[1].elapsed_time(e[2]))
         err = ctx.take_error() if hasattr(L, "cpk_ctx_take_error") else 0
-        cnt.zero_(); ctx.count_mismatch(d_in, d_out, n * W, cnt)
+        cnt.zero_(); ctx.count_mismatch(d_in, d_out, int(swo[-1]), cnt)
         P = int(d_off[-1].item())
         me, md = np.median(te), np.median(td)
         print(f"  {name:44s} enc {me:8.3f} ms ({U / me / 1e6:7.1f} GB/s)  dec {md:8.3f} ms ({U / md / 1e6:7.1f} GB/s)"
