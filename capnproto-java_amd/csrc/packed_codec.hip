@@ -1388,10 +1388,12 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
   if (!c) return CPK_ENOMEM;
   c->device = device;
   {
-    // Encoders: the single pass (encode_sp.hip) for batches of pieces up to
-    // 8192 words (4.35 against 5.05 ms per 131,072 config-2 pieces), the two
-    // passes (encode_v4.hip) for larger ones (sp_takes).  CPK_ENCODER=0 / 4
-    // force one of them for every batch.
+    // Encoders: the single pass (encode_sp.hip) for batches of like-sized
+    // pieces of 1 Ki words and more (3.65 against 5.06 ms per 131,072
+    // config-2 pieces of 8 Ki words; 3.96 against 5.50 ms for 16,384 of
+    // 64 Ki words), the two passes (encode_v4.hip) for mixed sizes and
+    // message batches; chosen on the device (e4_gate_kernel) among the
+    // batches sp_takes admits.  CPK_ENCODER=0 / 4 force one of them.
     const char *e = getenv("CPK_ENCODER");
     c->encoder = (e && e[0] == '4') ? 4 : (e && e[0] == '0') ? 0 : 5;
     // CPK_DECODER=1 selects the block-map decoder, 2 the record-index one
@@ -1439,9 +1441,13 @@ int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
 // small kernels and the e4 scan, no host sync: the unit count stays on the
 // device).  sp_takes screens which batches it takes; cpk_encode_batch lets
 // the device choose by the piece sizes (e4_gate_kernel).
-static bool sp_takes(cpk_ctx ctx, uint64_t max_seg_words) {
+static uint64_t sp_unit_bound(uint64_t n, uint64_t hint);
+// whether the single pass is enqueued at all (for the device to choose): a
+// size hint, and a unit table of bounded size for pieces over one chunk (a
+// loose hint would otherwise size it for nothing)
+static bool sp_takes(cpk_ctx ctx, uint32_t n, uint64_t max_seg_words) {
   if (ctx->encoder == 0) return true;  // (CPK_ENCODER=0: single pass for every batch)
-  return ctx->encoder != 4 && max_seg_words != 0 && max_seg_words <= 64ull * cpk::kSpCS;
+  return ctx->encoder != 4 && max_seg_words != 0 && sp_unit_bound(n, max_seg_words) <= (1ull << 25);
 }
 
 // `units`: a bound on the batch's units when its pieces may exceed one
@@ -1567,7 +1573,8 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
     uint32_t *mm = ctx->tickets + cpk::kTkGate;
     if (hipMemsetAsync(mm, 0xff, 4, s) != hipSuccess || hipMemsetAsync(mm + 1, 0, 4, s) != hipSuccess)
       return CPK_EDEVICE;
-    hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3((n + 1023) / 1024), dim3(256), 0, s, d_swo, n, mm);
+    const unsigned mg = n < 256u * 256u ? (unsigned)((n + 255) / 256) : 256u;
+    hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3(mg), dim3(256), 0, s, d_swo, n, mm);
     hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets);
   }
   unsigned grid = (unsigned)(8 * ctx->cus);
@@ -1673,7 +1680,7 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
-  if (!sp_takes(ctx, max_seg_words)) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
+  if (!sp_takes(ctx, n, max_seg_words)) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
   if (ctx->encoder == 0) {
     // (forced single pass: pieces of any size, several units for a large one)
     uint64_t hint = max_seg_words;
@@ -1690,10 +1697,12 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
     if (ub > 0xffffffffull) return CPK_EUNSUPPORTED;
     return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s, false, ub);
   }
-  // by piece size: both enqueued, the device picks one (e4_gate_kernel)
+  // by piece size: both enqueued, the device picks one (e4_gate_kernel);
+  // pieces over one chunk go to the single pass as several units
   int rc = e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s, true);
   if (rc) return rc;
-  return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s, true);
+  return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s, true,
+                   sp_unit_bound(n, max_seg_words));
 }
 
 int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {

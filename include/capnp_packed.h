@@ -86,10 +86,12 @@ int cpk_ctx_device(cpk_ctx ctx);
 /* Batch encode of n pieces, device-resident (replaces n calls of
  * PackedOutputStream.write, PackedOutputStream.java:35-205).  Pieces of any
  * size.  The encoder is chosen on the device from the piece sizes (no host
- * sync): like-sized pieces of 1-8 Ki words take the single-pass encoder
- * (read the words once, write the packed bytes once, offsets by a decoupled
- * look-back over the pieces); other batches the two-pass one (a size pass, a
- * scan of the sizes, an emit pass).
+ * sync): like-sized pieces of 1 Ki words or more (the largest at most twice
+ * the smallest) take the single-pass encoder (read the words once, write the
+ * packed bytes once, work ticketed per 8192-word chunk, offsets by a decoupled
+ * look-back over the chunks; pieces over one chunk need max_seg_words);
+ * other batches the two-pass one (a size pass, a scan of the sizes, an emit
+ * pass).
  *   d_in            : 8-byte aligned words; piece i is words
  *                     [d_seg_word_off[i], d_seg_word_off[i+1]).
  *   d_seg_word_off  : uint64[n+1], device.

@@ -311,6 +311,24 @@ def test_tiled_boundary_runs(ctx, oracle):
         _check_batch(ctx, oracle, data, _swo([len(p) // 8 for p in parts]))
 
 
+def test_like_sized_large_pieces(ctx, oracle):
+    """Like-sized pieces over one 8192-word chunk (the default choice sends
+    them to the single pass as several units each, chained by their run
+    state): random sizes within a factor of two, runs crossing every chunk
+    boundary, and dense config-3 pieces of 64 Ki words."""
+    rng = np.random.default_rng(31)
+    sizes = [int(s) for s in rng.integers(12000, 24000, size=20)]
+    pieces = [_runs_piece(rng, s) for s in sizes]
+    T = 8192
+    pieces += [np.concatenate([Z8] * (2 * T + 5)), np.concatenate([D8] * (2 * T - 3)),
+               np.concatenate([L8] * (T - 100) + [D8] + [L8] * (T + 200)),
+               np.concatenate([D8] * (T + 300) + [Z8] * (T - 300) + [D8] * 20)]
+    data = np.concatenate(pieces)
+    _check_batch(ctx, oracle, data, _swo([len(p) // 8 for p in pieces]))
+    swo = _swo([65536] * 6)
+    _check_batch(ctx, oracle, oracle.generate(oracle.preset(3), swo), swo)
+
+
 def test_config3_messages(ctx, oracle):
     """messages of 4 segments of 4-256 KiB, dense
     (<10 % zero words), each preceded by its segment-table piece."""
