@@ -165,7 +165,11 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
 #pragma unroll
         for (int j = 0; j < kD2LinesPerLane; ++j) {
           const uint32_t L = lane + 64 * j;
+#if CPK_DEC_NTLD
+          l[j] = L < lines ? ld_stream16(gsrc + L) : make_uint4(0u, 0u, 0u, 0u);
+#else
           l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
+#endif
         }
 #pragma unroll
         for (int j = 0; j < kD2LinesPerLane; ++j) {
@@ -393,7 +397,11 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
             const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
             const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
             const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
+#if CPK_DEC_NT
+            if (wv < re) __builtin_nontemporal_store((uint64_t)x0 | ((uint64_t)x1 << 32), &dst_w[wv]);
+#else
             if (wv < re) dst_w[wv] = (uint64_t)x0 | ((uint64_t)x1 << 32);
+#endif
           }
         }
         // the record covering the next round's first word

@@ -73,6 +73,15 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #ifndef CPK_SP_HCBR
 #define CPK_SP_HCBR 1  // head counts only in steps with heads (a branch per step: -2 % encode)
 #endif
+#ifndef CPK_SP_NTLD
+#define CPK_SP_NTLD 1  // nontemporal loads of the words (A1; config 3 encode -1.5 %)
+#endif
+#ifndef CPK_SP_NTST
+#define CPK_SP_NTST 1  // nontemporal stores of the packed lines (flush; config 3 encode -1 %)
+#endif
+#ifndef CPK_SP_PRIO_A1
+#define CPK_SP_PRIO_A1 1  // raised wave priority while A1 issues its loads (configs 3 / 4 encode -1 %)
+#endif
 #ifndef CPK_SP_WPE
 #define CPK_SP_WPE 3  // waves per SIMD the registers must allow (3 workgroups per CU)
 #endif
@@ -282,10 +291,20 @@ __device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict_
                                           int cnt, int lane) {
   // loads clamped to the piece, not predicated: step j's lanes read
   // min(lane, last valid lane of the step) (one lane register for all steps)
+#if CPK_SP_PRIO_A1
+  __builtin_amdgcn_s_setprio(1);  // (the loads out first)
+#endif
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j)
     if (kFull || j < cnt)
+#if CPK_SP_NTLD
+      R.v[j] = ld_stream(&(src + j * 64)[kFull ? (uint32_t)lane : min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))]);
+#else
       R.v[j] = (src + j * 64)[kFull ? (uint32_t)lane : min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))];
+#endif
+#if CPK_SP_PRIO_A1
+  __builtin_amdgcn_s_setprio(0);
+#endif
   uint32_t acc = 0;
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j) {
@@ -539,7 +558,11 @@ __device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t 
 #endif
     wave_lds_order();
     if (t < upto) {
+#if CPK_SP_NTST
+      if ((L0 + t) * 16 + 16 <= ocap) st_stream(v, out + (L0 + t) * 16);
+#else
       if ((L0 + t) * 16 + 16 <= ocap) *reinterpret_cast<uint4 *>(out + (L0 + t) * 16) = v;
+#endif
       if (t) sp_ring_clear(ring, t - 1);
     }
     wave_lds_order();

@@ -28,6 +28,18 @@ constexpr uint32_t kE4RingDw = kE4RingBytes / 4;
 
 // nonzero-byte tag of a word (PackedOutputStream.java:64-117): bit i set iff
 // byte i != 0.  SWAR: bit 7 of every byte of t = byte != 0, gathered by shifts.
+#ifndef CPK_E4_NTST
+#define CPK_E4_NTST 0  // nontemporal stores of the emit pass's packed lines
+#endif
+#ifndef CPK_E4_NTLD2
+#define CPK_E4_NTLD2 0  // nontemporal loads in the emit pass (the words' second and last read)
+#endif
+#if CPK_E4_NTLD2
+#define E4_LD2(p) ld_stream(p)
+#else
+#define E4_LD2(p) (*(p))
+#endif
+
 __device__ __forceinline__ uint32_t e4_tag(uint64_t v) {
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
   const uint32_t tl = ((lo & 0x7f7f7f7fu) + 0x7f7f7f7fu) | lo;
@@ -64,7 +76,11 @@ __device__ __forceinline__ void e4_flush(uint8_t *out, uint32_t *ring, uint64_t 
       uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kE4RingLines - 1));
       const uint4 val = *rl;
       *rl = make_uint4(0u, 0u, 0u, 0u);
+#if CPK_E4_NTST
+      st_stream(val, out + L * 16);
+#else
       *reinterpret_cast<uint4 *>(out + L * 16) = val;
+#endif
     }
   }
   fl = upto;
@@ -472,10 +488,10 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
     uint64_t vc[4], vl[4];
     const uint32_t kl = W32 - 1;  // loads clamped, not predicated
 #pragma unroll
-    for (int j = 0; j < 4; ++j) vc[j] = src[min(((uint32_t)j << 6) + lane, kl)];
+    for (int j = 0; j < 4; ++j) vc[j] = E4_LD2(src + min(((uint32_t)j << 6) + lane, kl));
     for (uint32_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) vl[j] = src[min(((s0 + 4 + j) << 6) + lane, kl)];
+      for (int j = 0; j < 4; ++j) vl[j] = E4_LD2(src + min(((s0 + 4 + j) << 6) + lane, kl));
       uint64_t bv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) bv[j] = s0 + j < nsteps ? bvp[s0 + j] : ~0ull;

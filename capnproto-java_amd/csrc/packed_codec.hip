@@ -205,6 +205,19 @@ __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("" ::: "memory");  // re-read LDS after this point (no forwarding)
 }
 
+// ------------------------------------------------------------ streaming hints
+// nontemporal (streaming) loads and stores: data read or written once
+typedef unsigned int cpk_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint64_t ld_stream(const uint64_t *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ uint4 ld_stream16(const uint4 *p) {
+  const cpk_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const cpk_u32x4 *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_stream(uint4 w, void *p) {
+  cpk_u32x4 v = {w.x, w.y, w.z, w.w};
+  __builtin_nontemporal_store(v, reinterpret_cast<cpk_u32x4 *>(p));
+}
+
 // ------------------------------------------------------------ look-back
 // status word per piece: [63:62] flag (1 aggregate, 2 inclusive prefix),
 // [61:0] value.  One 8-byte relaxed agent-scope granule: the data is the
@@ -350,6 +363,12 @@ static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 
 #endif
 #ifndef CPK_DEC_ALLIN
 #define CPK_DEC_ALLIN 1  // an expansion without bound checks for windows whose records are all loaded
+#endif
+#ifndef CPK_DEC_NTLD
+#define CPK_DEC_NTLD 0  // nontemporal loads of the window lines
+#endif
+#ifndef CPK_DEC_NT
+#define CPK_DEC_NT 1  // nontemporal stores of the expanded words (config 2 decode -9 %, config 4 -5 %)
 #endif
 #ifndef CPK_DEC_HOIST_CNT
 #define CPK_DEC_HOIST_CNT 0
@@ -544,7 +563,11 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
 #pragma unroll
         for (int j = 0; j < kWinLinesPerLane; ++j) {
           const uint32_t L = lane + 64 * j;
+#if CPK_DEC_NTLD
+          l[j] = L < lines ? ld_stream16(gsrc + L) : make_uint4(0u, 0u, 0u, 0u);
+#else
           l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
+#endif
         }
 #pragma unroll
         for (int j = 0; j < kWinLinesPerLane; ++j) {
@@ -886,7 +909,11 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
               v4.y = (uint32_t)(words[i] >> 32);
               v4.z = (uint32_t)words[i + 1];
               v4.w = (uint32_t)(words[i + 1] >> 32);
+#if CPK_DEC_NT
+              st_stream(v4, d + i);
+#else
               *reinterpret_cast<uint4 *>(d + i) = v4;
+#endif
             }
           } else {
 #pragma unroll
