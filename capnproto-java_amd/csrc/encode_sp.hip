@@ -35,7 +35,13 @@ constexpr int kSpWaves = CPK_SP_WAVES;
 constexpr int kSpThreads = 64 * kSpWaves;
 constexpr int kSpWS = 128 / kSpWaves;          // steps per wave
 constexpr int kSpCS = kSpWaves * kSpWS;        // steps per chunk (8192 words)
-constexpr uint32_t kSpRing = 8192;             // output ring per wave (bytes)
+#ifndef CPK_SP_RELOAD
+#define CPK_SP_RELOAD 0  // B reads the words again (L2) instead of keeping them in VGPRs from A1
+#endif
+#ifndef CPK_SP_RING
+#define CPK_SP_RING 8192
+#endif
+constexpr uint32_t kSpRing = CPK_SP_RING;      // output ring per wave (bytes)
 constexpr uint32_t kSpRingLines = kSpRing / 16;
 constexpr uint32_t kSpRingStride = kSpRing + 16;  // + one overhang line (line 0's spill)
 constexpr uint32_t kSpoLut = 0;                                      // u64[256]
@@ -272,8 +278,13 @@ __device__ uint32_t sp_cont(const uint64_t *msk, int s, int cs, int cls, uint32_
   return min(r, 256u);
 }
 
+#ifndef CPK_SP_A1G
+#define CPK_SP_A1G 8  // (reload form) steps whose loads A1 keeps in flight per group
+#endif
 struct SpRegs {
+#if !CPK_SP_RELOAD
   uint64_t v[kSpWS];       // the words, step j in v[j]
+#endif
   uint32_t mp[kSpWS / 4];  // tags, four per register
   uint32_t zl, zh, dll, dlh, dl_, dh_;                 // A1 stash: Z, DL, D (lane = step)
   uint32_t oml, omh, ohl, ohh, oel, oeh;               // A2 stash: Mem, HC, E
@@ -286,6 +297,55 @@ struct SpRegs {
 // step waits only for its own load (vmcnt(kSpWS - 1 - j)); with the per-step
 // branches of the general form the compiler waits for all of them at the
 // first step
+#if CPK_SP_RELOAD
+// reload form: the words are not kept for B; loads in groups of CPK_SP_A1G
+// steps, the next group's in flight while a group's tags are taken
+template <bool kFull>
+__device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict__ src, uint32_t wrem,
+                                          int cnt, int lane) {
+  constexpr int G = CPK_SP_A1G;
+  static_assert(kSpWS % G == 0, "A1 groups");
+  uint64_t v[2][G];
+  auto ld = [&](int j) __attribute__((always_inline)) -> uint64_t {
+    return (src + j * 64)[kFull ? (uint32_t)lane : min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))];
+  };
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+    if (kFull || i < cnt) v[0][i] = ld(i);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int g = 0; g < kSpWS / G; ++g) {
+    if (g + 1 < kSpWS / G) {
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int j = (g + 1) * G + i;
+        if (kFull || j < cnt) v[(g + 1) & 1][i] = ld(j);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int j = g * G + i;
+      if (kFull || j < cnt) {
+        const bool valid = kFull || (uint32_t)lane < wrem - 64u * j;
+        const uint32_t m = valid ? e4_tag(v[g & 1][i]) : 0u;
+        if (j & 3) R.mp[j >> 2] |= m << (8 * (j & 3));
+        else R.mp[j >> 2] = m;
+        const uint32_t pc = (uint32_t)__builtin_popcount(m);
+        acc += pc;
+        const uint64_t Z = __ballot(valid && m == 0), DL = __ballot(pc >= 7), D = __ballot(m == 0xffu);
+        R.zl = sp_wl(R.zl, (uint32_t)Z, j);
+        R.zh = sp_wl(R.zh, (uint32_t)(Z >> 32), j);
+        R.dll = sp_wl(R.dll, (uint32_t)DL, j);
+        R.dlh = sp_wl(R.dlh, (uint32_t)(DL >> 32), j);
+        R.dl_ = sp_wl(R.dl_, (uint32_t)D, j);
+        R.dh_ = sp_wl(R.dh_, (uint32_t)(D >> 32), j);
+      }
+    }
+    CPK_SP_STEP_FENCE();
+  }
+  return acc;
+}
+#else
 template <bool kFull>
 __device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict__ src, uint32_t wrem,
                                           int cnt, int lane) {
@@ -328,6 +388,7 @@ __device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict_
   }
   return acc;
 }
+#endif
 
 // the wave's masks to LDS (lane j = step sa + j)
 __device__ __forceinline__ void sp_put_masks(const SpRegs &R, uint64_t *msk, int sa, int cnt, int lane) {
@@ -575,7 +636,10 @@ __device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t 
 // (getbase: wave 0 runs the piece's look-back meanwhile -- the other waves
 // have had that many steps of work before they wait for it).
 #ifndef CPK_SP_DEFER
-#define CPK_SP_DEFER 12  // steps laid out before the offset is needed (12 x 640 B < kSpRing)
+#define CPK_SP_DEFER (((int)(kSpRing - 16) / 640) & ~1)  // steps laid out before the offset is needed (12 at 8 KiB)
+#endif
+#ifndef CPK_SP_BPF
+#define CPK_SP_BPF 2  // (reload form) step pairs whose words B has in flight ahead
 #endif
 constexpr int kSpDefer = CPK_SP_DEFER;
 // which waves may lay out all their steps before fetching the offset when
@@ -589,7 +653,16 @@ static_assert(kSpDefer * 640 + 16 <= (int)kSpRing && kSpDefer % 2 == 0, "deferre
 template <class GetBase>
 __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, uint32_t *ring, uint8_t *out,
                                      bool known, bool fits, uint64_t g0, int lane, uint64_t ocap,
-                                     GetBase getbase) {
+                                     const uint64_t *__restrict__ src, uint32_t wrem, GetBase getbase) {
+#if CPK_SP_RELOAD
+  // the words again (read by A1 moments ago: L2), CPK_SP_BPF pairs ahead
+  uint64_t pv[kSpWS];
+  auto ldw = [&](int j) __attribute__((always_inline)) {
+    if (j < kSpWS && j < cnt) pv[j] = ld_stream(&(src + j * 64)[min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))]);
+  };
+#pragma unroll
+  for (int j = 0; j < 2 * CPK_SP_BPF; ++j) ldw(j);
+#endif
   uint32_t rel = 0, ft = 0;
 #if CPK_SP_UNI_BASE
   // the output offset is wave-uniform: say so (readfirstlane), or the flush
@@ -604,7 +677,11 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     const uint64_t Mem = sp_rl(R.oml, R.omh, j);
     const uint64_t HC = sp_rl(R.ohl, R.ohh, j);
     const uint32_t m = (R.mp[j >> 2] >> (8 * (j & 3))) & 0xffu;
+#if CPK_SP_RELOAD
+    const uint32_t lo = (uint32_t)pv[j], hi = (uint32_t)(pv[j] >> 32);
+#else
     const uint32_t lo = (uint32_t)R.v[j], hi = (uint32_t)(R.v[j] >> 32);
+#endif
     const uint64_t sel = lut[m];
     const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
     const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
@@ -670,6 +747,10 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
   // steps j and j + 1 (when j + 1 < cnt): both byte counts in one wave scan
   // (16-bit halves: a step's strings total at most 640 bytes)
   auto step = [&](const int j) __attribute__((always_inline)) {
+#if CPK_SP_RELOAD
+    ldw(j + 2 * CPK_SP_BPF);
+    ldw(j + 2 * CPK_SP_BPF + 1);
+#endif
     {
       uint32_t a0, a1, a2, na, b0 = 0, b1 = 0, b2 = 0, nb2 = 0;
       strings(j, a0, a1, a2, na);
@@ -841,7 +922,8 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
                                              uint32_t c, uint64_t *msk, uint64_t *scr, uint64_t *prev,
                                              uint64_t *next, uint32_t ep, uint32_t *err, int w, int lane,
                                              int &cnt, uint32_t &Xlast, uint64_t &wbefore,
-                                             uint64_t &wmine SP_A1_PARAMS) {
+                                             uint64_t &wmine, const uint64_t *&wsrc,
+                                             uint32_t &wrem_o SP_A1_PARAMS) {
   const uint32_t ns = (W + 63) >> 6;
   const uint32_t cs0 = c * kSpCS;
   const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
@@ -849,6 +931,8 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   cnt = max(0, min(kSpWS, cs - sa));
   const uint32_t wfirst = (cs0 + (uint32_t)sa) * 64;  // the wave's first word
   const uint32_t wrem = cnt ? W - wfirst : 0;
+  wsrc = pw + wfirst;
+  wrem_o = wrem;
   uint32_t acc = 0;
   if (cnt) {
 #if CPK_SP_A1FULL
@@ -1015,9 +1099,11 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     int cnt = 0;
     uint32_t Xlast = 0;
     uint64_t wbefore = 0, wmine = 0;
+    const uint64_t *wsrc = pw;
+    uint32_t wrem = 0;
     const uint64_t ct = sp_chunk(R, pw, W, c, msk, scr, c ? ustate + (t - 1) : nullptr,
                                  lastc ? nullptr : ustate + t, ep, err, w, lane, cnt, Xlast, wbefore,
-                                 wmine SP_A1_ARGS);
+                                 wmine, wsrc, wrem SP_A1_ARGS);
     WPH(1)
     if (w == 0 && lane == 0) {
       // the unit's size, published before its strings are laid out: the
@@ -1051,7 +1137,7 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
         return sp_ld(&scr[5]) + wbefore;
       };
       sp_b(R, cnt, lut, ring, out, false, CPK_SP_FITS_WAVES(w) && wmine + 16 <= kSpRing, wbefore, lane, ocap,
-           getbase);
+           wsrc, wrem, getbase);
     } else if (w == 0) {
       getoff();  // wave 0 runs the look-back even without steps (an empty piece)
     }
