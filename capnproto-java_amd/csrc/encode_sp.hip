@@ -278,6 +278,9 @@ __device__ uint32_t sp_cont(const uint64_t *msk, int s, int cs, int cls, uint32_
   return min(r, 256u);
 }
 
+#ifndef CPK_SP_EVEN
+#define CPK_SP_EVEN 1  // a short chunk's steps spread over all waves (4 Ki-word pieces: encode -15 %)
+#endif
 #ifndef CPK_SP_A1G
 #define CPK_SP_A1G 8  // (reload form) steps whose loads A1 keeps in flight per group
 #endif
@@ -927,8 +930,16 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   const uint32_t ns = (W + 63) >> 6;
   const uint32_t cs0 = c * kSpCS;
   const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
+#if CPK_SP_EVEN
+  // a chunk's steps spread over all waves (a short piece keeps every wave
+  // busy, not wave 0 alone): per wave ceil(cs / waves), rounded up to a pair
+  const int per = min(kSpWS, ((cs + kSpWaves - 1) / kSpWaves + 1) & ~1);
+  const int sa = w * per;
+  cnt = max(0, min(per, cs - sa));
+#else
   const int sa = w * kSpWS;
   cnt = max(0, min(kSpWS, cs - sa));
+#endif
   const uint32_t wfirst = (cs0 + (uint32_t)sa) * 64;  // the wave's first word
   const uint32_t wrem = cnt ? W - wfirst : 0;
   wsrc = pw + wfirst;

@@ -546,13 +546,15 @@ __global__ __launch_bounds__(256) void e4_minmax_kernel(const uint64_t *__restri
     atomicMax(&mm[1], hi);
   }
 }
-// like-sized pieces (the largest at most twice the smallest) of 1024 words
-// or more: the single pass (its ticket left at 0, the two-pass kernels told
+// like-sized pieces (the largest at most twice the smallest) of 4096 words
+// or more: the single pass (measured crossover, 1 GiB batches, config 2 / 3:
+// 2 Ki-word pieces 1.07 / 1.22 ms against the two passes' 0.87 / 0.89, 4 Ki
+// words 0.69 / 0.82 against 0.85 / 0.87) (its ticket left at 0, the two-pass kernels told
 // to skip, tickets[kTkGate + 2]); else the reverse (the single pass's
 // ordered ticket exhausted)
 __global__ void e4_gate_kernel(uint32_t *tickets) {
   const uint32_t lo = tickets[kTkGate], hi = tickets[kTkGate + 1];
-  const bool sp = lo >= 1024u && 2u * lo >= hi;
+  const bool sp = lo >= 4096u && 2u * lo >= hi;
   if (threadIdx.x == 0) {
     tickets[kTkGate + 2] = sp ? 1u : 0u;
     tickets[kTkPlan] = sp ? 0u : 0x7fffffffu;

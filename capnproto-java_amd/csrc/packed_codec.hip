@@ -1416,7 +1416,7 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
   c->device = device;
   {
     // Encoders: the single pass (encode_sp.hip) for batches of like-sized
-    // pieces of 1 Ki words and more (3.65 against 5.06 ms per 131,072
+    // pieces of 4 Ki words and more (3.65 against 5.06 ms per 131,072
     // config-2 pieces of 8 Ki words; 3.96 against 5.50 ms for 16,384 of
     // 64 Ki words), the two passes (encode_v4.hip) for mixed sizes and
     // message batches; chosen on the device (e4_gate_kernel) among the

@@ -86,7 +86,7 @@ int cpk_ctx_device(cpk_ctx ctx);
 /* Batch encode of n pieces, device-resident (replaces n calls of
  * PackedOutputStream.write, PackedOutputStream.java:35-205).  Pieces of any
  * size.  The encoder is chosen on the device from the piece sizes (no host
- * sync): like-sized pieces of 1 Ki words or more (the largest at most twice
+ * sync): like-sized pieces of 4 Ki words or more (the largest at most twice
  * the smallest) take the single-pass encoder (read the words once, write the
  * packed bytes once, work ticketed per 8192-word chunk, offsets by a decoupled
  * look-back over the chunks; pieces over one chunk need max_seg_words);

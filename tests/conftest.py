@@ -26,7 +26,7 @@ def oracle():
 def ctx(request):
     """A context per encoder / decoder pair (CPK_ENCODER, CPK_DECODER are read
     at context creation): every parity case runs through the default choice
-    (the single pass for like-sized pieces of 1 Ki words or more, the two-pass
+    (the single pass for like-sized pieces of 4 Ki words or more, the two-pass
     encoder, encode_v4.hip, otherwise; the record-index decoder,
     decode_v2.hip, for sparse batches, the block-map decoder, decode_kernel,
     otherwise), through the single-pass encoder (encode_sp.hip) forced
