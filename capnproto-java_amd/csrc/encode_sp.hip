@@ -278,6 +278,9 @@ __device__ uint32_t sp_cont(const uint64_t *msk, int s, int cs, int cls, uint32_
   return min(r, 256u);
 }
 
+#ifndef CPK_SP_ABL
+#define CPK_SP_ABL 0  // ablations for timing only (wrong output): 1 no ring ORs, 2 no head counts, 4 no LUT read, 8 no line stores
+#endif
 #ifndef CPK_SP_EVEN
 #define CPK_SP_EVEN 1  // a short chunk's steps spread over all waves (4 Ki-word pieces: encode -15 %)
 #endif
@@ -623,7 +626,8 @@ __device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t 
     wave_lds_order();
     if (t < upto) {
 #if CPK_SP_NTST
-      if ((L0 + t) * 16 + 16 <= ocap) st_stream(v, out + (L0 + t) * 16);
+      if (!(CPK_SP_ABL & 8) && (L0 + t) * 16 + 16 <= ocap) st_stream(v, out + (L0 + t) * 16);
+      if (CPK_SP_ABL & 8) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
 #else
       if ((L0 + t) * 16 + 16 <= ocap) *reinterpret_cast<uint4 *>(out + (L0 + t) * 16) = v;
 #endif
@@ -685,12 +689,18 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
 #else
     const uint32_t lo = (uint32_t)R.v[j], hi = (uint32_t)(R.v[j] >> 32);
 #endif
+#if CPK_SP_ABL & 4
+    const uint64_t sel = 0x0706050403020100ull + m;  // (ablation: no LUT read)
+#else
     const uint64_t sel = lut[m];
+#endif
     const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
     const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
     const bool zw = m == 0;
     uint32_t cz = 0, cd = 0;
-#if CPK_SP_HCBR
+#if CPK_SP_ABL & 2
+    if (false)
+#elif CPK_SP_HCBR
     if (HC)
 #endif
     {
@@ -740,7 +750,8 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     const uint32_t d3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
 #endif
     uint32_t *rp = ring + ((p >> 2) & (kSpRing / 4 - 1));
-    if (nb) {  // (zero-length strings would all hit one address)
+    if (CPK_SP_ABL & 1) asm volatile("" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3), "v"(rp));
+    else if (nb) {  // (zero-length strings would all hit one address)
       atomicOr(rp, d0);
       atomicOr(rp + 1, d1);
       atomicOr(rp + 2, d2);
