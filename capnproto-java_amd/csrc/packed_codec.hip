@@ -370,6 +370,9 @@ static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 
 #ifndef CPK_DEC_NT
 #define CPK_DEC_NT 1  // nontemporal stores of the expanded words (config 2 decode -9 %, config 4 -5 %)
 #endif
+#ifndef CPK_DEC_ABL
+#define CPK_DEC_ABL 0  // ablations for timing only (wrong output): 1 no word stores, 2 no expansion, 4 no block-map walk
+#endif
 #ifndef CPK_DEC_HOIST_CNT
 #define CPK_DEC_HOIST_CNT 0
 #endif
@@ -685,7 +688,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
           if (rb == 0) {
             // round 0 (usually the window's only one): every record's output
             // is at or past the round's start, so it always marks a block
-            if (on) {
+            if (on && !(CPK_DEC_ABL & 4)) {
               uint32_t rel = (uint32_t)o0;
               for (uint32_t q = entry; q < S && rel <= (uint32_t)(kRound - kBlk);) {
                 const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
@@ -909,7 +912,9 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
               v4.y = (uint32_t)(words[i] >> 32);
               v4.z = (uint32_t)words[i + 1];
               v4.w = (uint32_t)(words[i + 1] >> 32);
-#if CPK_DEC_NT
+#if CPK_DEC_ABL & 1
+              asm volatile("" ::"v"(v4.x), "v"(v4.y), "v"(v4.z), "v"(v4.w));
+#elif CPK_DEC_NT
               st_stream(v4, d + i);
 #else
               *reinterpret_cast<uint4 *>(d + i) = v4;
@@ -922,6 +927,9 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
           }
         }
         };
+#if CPK_DEC_ABL & 2
+        if (false)
+#endif
 #if CPK_DEC_ALLIN
         if (enext + 12 <= lend) expand(std::true_type{});
         else
