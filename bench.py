@@ -300,8 +300,10 @@ def run_rank(args, rank, world, local):
     # (the library's choice: the single pass for like-sized 64 KiB pieces,
     # the two passes for message batches; CPK_ENCODER forces one)
     forced = os.environ.get("CPK_ENCODER", "")[:1]
+    # (like-sized pieces whose sampled words are >= 85 % zero, config 4: the
+    # single pass's sparse form, cpk_sparse::sp_encode_kernel)
     enc_kernel = "e4_size_kernel+e4_emit_kernel" if forced == "4" or (mso is not None and forced != "0") \
-        else "sp_encode_kernel"
+        else "cpk_sparse::sp_encode_kernel" if forced != "0" and args.config == 4 else "sp_encode_kernel"
     # (the batch decoder: the record-index one for sparse batches, packed
     # under 15 % of the words' bytes, else the block map; messages: block map)
     forced_d = os.environ.get("CPK_DECODER", "")[:1]

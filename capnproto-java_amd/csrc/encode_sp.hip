@@ -91,6 +91,7 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #ifndef CPK_SP_WPE
 #define CPK_SP_WPE 3  // waves per SIMD the registers must allow (3 workgroups per CU)
 #endif
+constexpr int kSpWpe = CPK_SP_WPE;  // workgroups per CU (the grid: kSpWpe x CUs)
 
 // status word per piece: [63:62] flag (1 aggregate, 2 inclusive prefix),
 // [61:46] launch epoch, [45:0] value (a relaxed 8-byte agent-scope granule:
@@ -1067,7 +1068,9 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     const uint64_t *__restrict__ pdesc, const uint64_t *__restrict__ tin, uint32_t n,
     uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status, uint32_t ep,
     uint32_t *ticket, const uint64_t *__restrict__ utab, const uint64_t *__restrict__ nunits,
-    uint64_t *ustate, uint64_t hint, uint32_t *err, const uint64_t *ocapp) {
+    uint64_t *ustate, uint64_t hint, uint32_t *err, const uint64_t *ocapp, const uint32_t *pick, uint32_t mine) {
+  // (pick: the device gate's choice between this form and the other one)
+  if (pick && (uint32_t)__builtin_amdgcn_readfirstlane((int)*pick) != mine) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // a bound on the output buffer's size: sum of 9 w + 1 over the pieces
   // (cpk_packed_bound(w) <= 9 w + 1), + 16

@@ -517,7 +517,19 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
 // ---- encoder choice on the device (cpk_encode_batch, no host sync) --------
 // min / max piece words of the batch (mm[0] preset to ~0, mm[1] to 0)
 __global__ __launch_bounds__(256) void e4_minmax_kernel(const uint64_t *__restrict__ swo, uint32_t n,
-                                                        uint32_t *mm) {
+                                                        uint32_t *mm, const uint64_t *__restrict__ in) {
+  // (and one word per thread, one in each of G equal stretches of the
+  // batch at a hashed position inside it -- not at a fixed phase, which
+  // would alias with the pieces' starts: zero words counted into mm[3] for
+  // the single pass's sparse form, e4_gate_kernel)
+  {
+    const uint64_t a = swo[0], T = swo[n] - a;
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x, G = (uint64_t)gridDim.x * 256;
+    const uint64_t st = T / G, h = (uint32_t)(g * 2654435761u) ^ ((uint32_t)g >> 7);
+    const bool z = in && T && in[a + g * T / G + (st ? h % st : 0)] == 0;
+    const uint64_t zb = __ballot(z);
+    if ((threadIdx.x & 63) == 0 && zb) atomicAdd(&mm[3], (uint32_t)__builtin_popcountll(zb));
+  }
   // grid-stride over the pieces, one atomic pair per workgroup (one per
   // wave put 8 K same-address atomics in line at 1 Mi pieces: 97 us)
   __shared__ uint32_t red[2][4];
@@ -552,10 +564,15 @@ __global__ __launch_bounds__(256) void e4_minmax_kernel(const uint64_t *__restri
 // words 0.69 / 0.82 against 0.85 / 0.87) (its ticket left at 0, the two-pass kernels told
 // to skip, tickets[kTkGate + 2]); else the reverse (the single pass's
 // ordered ticket exhausted)
-__global__ void e4_gate_kernel(uint32_t *tickets) {
+// Among single-pass batches, those whose sampled words are at least 85 %
+// zero take its sparse form (cpk_sparse: tickets[kTkGate + 6] = 1; config 4
+// encode -7 %, config 2 +36 %).
+__global__ void e4_gate_kernel(uint32_t *tickets, uint32_t samples) {
   const uint32_t lo = tickets[kTkGate], hi = tickets[kTkGate + 1];
   const bool sp = lo >= 4096u && 2u * lo >= hi;
+  const bool sparse = sp && (uint64_t)tickets[kTkGate + 3] * 100u >= (uint64_t)samples * 85u;
   if (threadIdx.x == 0) {
+    tickets[kTkGate + 6] = sparse ? 1u : 0u;
     tickets[kTkGate + 2] = sp ? 1u : 0u;
     tickets[kTkPlan] = sp ? 0u : 0x7fffffffu;
   }

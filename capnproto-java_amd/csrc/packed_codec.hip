@@ -51,7 +51,8 @@ constexpr int kTkEnc = 0;              // encoder counters [8]
 constexpr int kTkDec = 8 * kTkStride;  // decoder counters [8]
 constexpr int kTkPlan = 16 * kTkStride;
 constexpr int kTkErr = 17 * kTkStride;
-constexpr int kTkGate = 17 * kTkStride + 8;  // [0..1] min, max piece words, [2] encoder choice, [4..5] decoder choice
+constexpr int kTkGate = 17 * kTkStride + 8;  // [0..1] min, max piece words, [2] encoder choice, [3] sampled zero
+                                             // words, [4..5] decoder choice, [6] single pass's form (1: sparse)
 constexpr int kTkWords = 18 * kTkStride;
 __device__ __forceinline__ int xcc_id() {
   int x;
@@ -1318,6 +1319,39 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 
 }  // namespace cpk
 
+// The single pass's sparse form: encode_sp.hip compiled again with B
+// reading its words a second time (from L2) instead of holding them in 64
+// VGPRs, 4 KiB rings and 6 workgroups per CU.  Mostly-zero batches emit
+// little, so each wave's output fits its smaller ring and the extra
+// occupancy pays (config 4 encode 3.12 -> 2.89 ms per 131,072 pieces); on
+// config 2 a wave's ~6 KiB of output overflows the ring and it is 36 %
+// slower, so the device gate takes it only for batches whose sampled words
+// are >= 85 % zero (e4_gate_kernel).
+#pragma push_macro("CPK_SP_RELOAD")
+#pragma push_macro("CPK_SP_RING")
+#pragma push_macro("CPK_SP_WPE")
+#pragma push_macro("CPK_SP_A1G")
+#pragma push_macro("CPK_SP_DEFER")
+#undef CPK_SP_RELOAD
+#undef CPK_SP_RING
+#undef CPK_SP_WPE
+#undef CPK_SP_A1G
+#undef CPK_SP_DEFER
+#define CPK_SP_RELOAD 1
+#define CPK_SP_RING 4096
+#define CPK_SP_WPE 6
+#define CPK_SP_A1G 4
+namespace cpk_sparse {
+using namespace cpk;
+#include "encode_sp.hip"
+}  // namespace cpk_sparse
+#undef CPK_SP_DEFER
+#pragma pop_macro("CPK_SP_RELOAD")
+#pragma pop_macro("CPK_SP_RING")
+#pragma pop_macro("CPK_SP_WPE")
+#pragma pop_macro("CPK_SP_A1G")
+#pragma pop_macro("CPK_SP_DEFER")
+
 // ================================================================ C ABI
 struct HostPipe;  // host_pipe.hip: staging of the host-memory forms
 
@@ -1545,18 +1579,28 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
       attr = true;
     }
   }
-  unsigned grid = (unsigned)(CPK_SP_WPE * ctx->cus);
+  unsigned grid = (unsigned)(cpk::kSpWpe * ctx->cus);
   if (grid > ucap) grid = (unsigned)ucap;
+  // (gated: both forms enqueued, the one the gate did not pick returns at once)
+  const uint32_t *pick = gated ? ctx->tickets + cpk::kTkGate + 6 : nullptr;
   if (pdesc)
     hipLaunchKernelGGL(cpk::sp_encode_kernel<true>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
                        ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
-                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr);
+                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr, pick, 0u);
   else
     hipLaunchKernelGGL(cpk::sp_encode_kernel<false>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
                        ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
-                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr);
+                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr, pick, 0u);
+  if (gated && !pdesc) {
+    unsigned g2 = (unsigned)(cpk_sparse::kSpWpe * ctx->cus);
+    if (g2 > ucap) g2 = (unsigned)ucap;
+    hipLaunchKernelGGL(cpk_sparse::sp_encode_kernel<false>, dim3(g2), dim3(cpk_sparse::kSpThreads),
+                       cpk_sparse::kSpLds, s, (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out,
+                       d_out_off, ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate,
+                       hint, ctx->tickets + cpk::kTkErr, (const uint64_t *)nullptr, pick, 1u);
+  }
   return hip_ok(hipGetLastError());
 }
 
@@ -1606,11 +1650,12 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
     // kernels return at once (the scans then write offsets the single pass
     // overwrites)
     uint32_t *mm = ctx->tickets + cpk::kTkGate;
-    if (hipMemsetAsync(mm, 0xff, 4, s) != hipSuccess || hipMemsetAsync(mm + 1, 0, 4, s) != hipSuccess)
+    if (hipMemsetAsync(mm, 0xff, 4, s) != hipSuccess || hipMemsetAsync(mm + 1, 0, 4, s) != hipSuccess ||
+        hipMemsetAsync(mm + 3, 0, 4, s) != hipSuccess)
       return CPK_EDEVICE;
     const unsigned mg = n < 256u * 256u ? (unsigned)((n + 255) / 256) : 256u;
-    hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3(mg), dim3(256), 0, s, d_swo, n, mm);
-    hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets);
+    hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3(mg), dim3(256), 0, s, d_swo, n, mm, (const uint64_t *)d_in);
+    hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets, mg * 256u);
   }
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (n + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (n + cpk::kE4Waves - 1) / cpk::kE4Waves;

@@ -18,12 +18,13 @@ for f in sorted(root.glob("*/*_counter_collection.csv")):
         for r in csv.DictReader(fh):
             k = r["Kernel_Name"]
             short = ("e4_size_kernel" if "e4_size_kernel" in k else "e4_emit_kernel" if "e4_emit_kernel" in k
+                     else "sp_encode_sparse_kernel" if "cpk_sparse" in k and "sp_encode_kernel" in k
                      else "sp_encode_kernel" if "sp_encode_kernel" in k
                      else "decode2_kernel" if "decode2_kernel" in k
                      else "decode_kernel" if "decode_kernel" in k else k.split("(")[0][-40:])
             vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
-for kern in ("sp_encode_kernel", "e4_size_kernel", "e4_emit_kernel", "decode_kernel", "decode2_kernel"):
+for kern in ("sp_encode_kernel", "sp_encode_sparse_kernel", "e4_size_kernel", "e4_emit_kernel", "decode_kernel", "decode2_kernel"):
     if kern not in vals:
         continue
     d = {c: sum(v) / len(v) for c, v in vals[kern].items()}
@@ -48,8 +49,9 @@ if len(sys.argv) > 3 and sys.argv[2] == "--json":
     def traffic_of(d):
         return d.get("FETCH_SIZE", 0) + d.get("WRITE_SIZE", 0)
     enc = []
-    if "sp_encode_kernel" in out:
-        enc.append(out["sp_encode_kernel"])
+    for k in ("sp_encode_kernel", "sp_encode_sparse_kernel"):
+        if k in out:
+            enc.append(out[k])
     if "e4_size_kernel" in out and "e4_emit_kernel" in out:
         enc.append({c: out["e4_size_kernel"].get(c, 0) + out["e4_emit_kernel"].get(c, 0)
                     for c in ("FETCH_SIZE", "WRITE_SIZE")})
