@@ -89,9 +89,10 @@ int cpk_ctx_device(cpk_ctx ctx);
  * sync): like-sized pieces of 4 Ki words or more (the largest at most twice
  * the smallest) take the single-pass encoder (read the words once, write the
  * packed bytes once, work ticketed per 8192-word chunk, offsets by a decoupled
- * look-back over the chunks; pieces over one chunk need max_seg_words);
- * other batches the two-pass one (a size pass, a scan of the sizes, an emit
- * pass).
+ * look-back over the chunks; pieces over one chunk need max_seg_words), in
+ * its sparse form (twice the workgroups per CU) when >= 85 % of a sample of
+ * the words are zero; other batches the two-pass one (a size pass, a scan of
+ * the sizes, an emit pass).
  *   d_in            : 8-byte aligned words; piece i is words
  *                     [d_seg_word_off[i], d_seg_word_off[i+1]).
  *   d_seg_word_off  : uint64[n+1], device.

@@ -1,0 +1,9 @@
+# round-3 final tree: bench lines configs 2/3/4, kernel stats + HBM traffic (rocprofv3), GPU suite
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu"
+tools/gpu_steps.sh \
+ "200|r3Z_bench_config2|python bench.py --config 2 --steps 10 --warmup 2" \
+ "200|r3Z_bench_config3|python bench.py --config 3 --steps 10 --warmup 2" \
+ "200|r3Z_bench_config4|python bench.py --config 4 --steps 10 --warmup 2" \
+ "300|r3Z_prof2|tools/profile.sh r3Z_c2 -- $B --config 2" \
+ "300|r3Z_prof3|tools/profile.sh r3Z_c3 -- $B --config 3" \
+ "300|r3Z_prof4|tools/profile.sh r3Z_c4 -- $B --config 4"
