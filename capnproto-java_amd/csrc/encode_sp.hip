@@ -665,8 +665,13 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
 #if CPK_SP_RELOAD
   // the words again (read by A1 moments ago: L2), CPK_SP_BPF pairs ahead
   uint64_t pv[kSpWS];
+  // only the lanes whose word is nonzero load it (a zero word's string
+  // needs no bytes): a line of zero words is not fetched again at all
   auto ldw = [&](int j) __attribute__((always_inline)) {
-    if (j < kSpWS && j < cnt) pv[j] = ld_stream(&(src + j * 64)[min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))]);
+    if (j < kSpWS && j < cnt) {
+      const uint32_t m = (R.mp[j >> 2] >> (8 * (j & 3))) & 0xffu;
+      pv[j] = m ? ld_stream(&(src + j * 64)[min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))]) : 0ull;
+    }
   };
 #pragma unroll
   for (int j = 0; j < 2 * CPK_SP_BPF; ++j) ldw(j);
