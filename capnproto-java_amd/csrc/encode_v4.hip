@@ -89,6 +89,9 @@ __device__ __forceinline__ void e4_flush(uint8_t *out, uint32_t *ring, uint64_t 
 #ifndef CPK_E4_WPE
 #define CPK_E4_WPE 8
 #endif
+#ifndef CPK_E4_MASKROLES
+#define CPK_E4_MASKROLES 0  // size pass: roles as scalar mask algebra per step (sp_roles), not per-lane selects (measured +12 %)
+#endif
 #ifndef CPK_E4_PF
 #define CPK_E4_PF 4  // steps of loads in flight ahead of the size pass's classification
 #endif
@@ -210,6 +213,8 @@ __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &
   return r;
 }
 
+#include "sp_roles.hip"  // SpSt, sp_roles: the run roles as mask algebra (shared with encode_sp.hip)
+
 // next piece for this wave from the per-XCD counters (as the decoder)
 __device__ __forceinline__ uint32_t e4_next_piece(uint32_t *ticket, int &xq, int &dry, uint32_t n) {
   uint32_t seg;
@@ -249,6 +254,10 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     E4St st = {2, 0, 0};
     int gl = 2;
     uint32_t acc = 0;
+#if CPK_E4_MASKROLES
+    SpSt mst = {0u, 0u, 0u};  // (a fresh piece: no run enters it)
+    uint64_t sb = 0;          // wave-uniform bytes beyond the nonzero bytes
+#endif
     // (32-bit step / word indices: a piece is at most 2^31 words, Serialize
     // limits segments to 2^29 - 1, Serialize.java:45-53)
     const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;
@@ -270,10 +279,37 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
         const uint32_t k = ((s0 + j) << 6) + lane;
         const bool valid = k < W32;
         if (s0 + j < nsteps) {
+#if CPK_E4_MASKROLES
+          // per word only the tag, its popcount and three ballots; the
+          // roles of the step's words follow from the masks and the state
+          // carried in SGPRs (sp_roles, as the single pass's sequential
+          // form), its bytes from popcounts: tag + nonzero bytes of every
+          // word but zero-run members, a count after each head, 8 verbatim
+          // bytes per literal-run member (PackedOutputStream.java:64-193)
+          const uint32_t m = valid ? e4_tag(v[j]) : 0u;
+          const uint32_t pc = (uint32_t)__builtin_popcount(m);
+          acc += pc;
+          const uint64_t Z = __ballot(valid && m == 0), DL = __ballot(pc >= 7), D = __ballot(m == 0xffu);
+          const uint32_t vr = W32 - ((s0 + j) << 6);
+          const uint64_t Vm = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
+          // the emit pass's run boundaries (as e4_classify's BV): past the
+          // end, every M word, and a Z / D-or-L word whose predecessor is
+          // of another group (gl: the group of the word before the step)
+          const uint64_t Zp = (Z << 1) | (gl == 0 ? 1ull : 0ull), DLp = (DL << 1) | (gl == 1 ? 1ull : 0ull);
+          const uint64_t BV = ~Vm | (Vm & ~Z & ~DL) | (Z & ~Zp) | (DL & ~DLp);
+          gl = (Z >> 63) ? 0 : ((DL >> 63) ? 1 : 2);
+          uint64_t Zh, Mem;
+          sp_roles(Z, DL, D, mst, Zh, Mem);
+          const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~Vm;
+          sb += (uint64_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
+                           __builtin_popcountll(HC));
+          x = lane == j ? BV : x;
+#else
           const E4Cls c = e4_classify(v[j], valid, gl);
           const E4Role r = e4_roles(e4_tag(v[j]), valid, c, st, lane, lem);
           acc += r.nb;
           x = lane == j ? c.BV : x;
+#endif
         }
       }
       // the group's boundary rows for the emit pass: lanes 0..PF-1, one store
@@ -284,7 +320,11 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     // wave sum in two 16-bit halves (a piece's packed size may pass 2^31)
     const uint32_t thi = (uint32_t)wave_incl_add((int)(acc >> 16));
     const uint32_t tlo = (uint32_t)wave_incl_add((int)(acc & 0xffffu));
+#if CPK_E4_MASKROLES
+    if (lane == 63) sizes[seg] = ((uint64_t)thi << 16) + tlo + sb;
+#else
     if (lane == 63) sizes[seg] = ((uint64_t)thi << 16) + tlo;
+#endif
   }
 }
 

@@ -1341,10 +1341,12 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 #define CPK_SP_RING 4096
 #define CPK_SP_WPE 6
 #define CPK_SP_A1G 4
+#define CPK_SP_OWN_ROLES 1
 namespace cpk_sparse {
 using namespace cpk;
 #include "encode_sp.hip"
 }  // namespace cpk_sparse
+#undef CPK_SP_OWN_ROLES
 #undef CPK_SP_DEFER
 #pragma pop_macro("CPK_SP_RELOAD")
 #pragma pop_macro("CPK_SP_RING")

@@ -81,3 +81,51 @@ def test_parallel_roles_equal_sequential(oracle, ws):
                 Zh, Mem, _, s2 = sm.roles(Z, DL, D, s2)
                 assert par[j] == (Zh, Mem), (a, j)
     assert accepted > 10
+
+
+def _group(m, valid):
+    return 3 if not valid else (0 if m == 0 else (1 if bin(m).count("1") >= 7 else 2))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_size_pass_boundary_masks(seed):
+    """encode_v4.hip's size pass (CPK_E4_MASKROLES) derives the emit pass's
+    run-boundary rows from the step's Z / D-or-L masks: BV = past the end |
+    M words | a Z word after a non-Z | a D/L word after a non-D/L (the word
+    before the step: the carried group gl).  Checked against e4_classify's
+    per-lane rule (!valid || g != g_prev || g == 2) and its gl update."""
+    rng = np.random.default_rng(seed)
+    M64 = (1 << 64) - 1
+    for _ in range(400):
+        nvalid = int(rng.integers(1, 65))
+        gl = int(rng.integers(0, 3))
+        kind = rng.choice(["zero", "dense", "mixed"], p=[0.3, 0.3, 0.4])
+        tags = []
+        for lane in range(64):
+            r = rng.random()
+            if kind == "zero" and r < 0.7 or kind == "mixed" and r < 0.3:
+                tags.append(0)
+            elif kind == "dense" and r < 0.7 or kind == "mixed" and r < 0.6:
+                tags.append(int(rng.choice([0xFF, 0x7F, 0xFE, 0xBF])))
+            else:
+                tags.append(int(rng.integers(1, 256)))
+        valid = [lane < nvalid for lane in range(64)]
+        tags = [t if v else 0 for t, v in zip(tags, valid)]
+        # per-lane rule (e4_classify)
+        g = [_group(t, v) for t, v in zip(tags, valid)]
+        bv_ref = 0
+        for lane in range(64):
+            gp = gl if lane == 0 else g[lane - 1]
+            if not valid[lane] or g[lane] != gp or g[lane] == 2:
+                bv_ref |= 1 << lane
+        gl_ref = min(g[63], 2)
+        # mask form (e4_size_kernel, CPK_E4_MASKROLES)
+        Z = sum(1 << i for i in range(64) if valid[i] and tags[i] == 0)
+        DL = sum(1 << i for i in range(64) if bin(tags[i]).count("1") >= 7)
+        V = M64 if nvalid >= 64 else (1 << nvalid) - 1
+        Zp = ((Z << 1) & M64) | (1 if gl == 0 else 0)
+        DLp = ((DL << 1) & M64) | (1 if gl == 1 else 0)
+        bv = ((~V & M64) | (V & ~Z & ~DL & M64) | (Z & ~Zp & M64) | (DL & ~DLp & M64))
+        gl_new = 0 if Z >> 63 else (1 if DL >> 63 else 2)
+        assert bv == bv_ref
+        assert gl_new == gl_ref
