@@ -8,12 +8,16 @@
 //
 // Design (DESIGN.md has the full derivation and the rooflines):
 //   encoders       encode_sp.hip (single pass, the default for like-sized
-//                  pieces and small batches): a workgroup per 8192-word chunk,
-//                  the chunk in VGPRs, roles by mask algebra, a decoupled
-//                  look-back for the offsets, strings (tag + v_perm-compacted
-//                  bytes + count) OR-ed into an LDS ring, 16-byte line
-//                  stores; encode_v4.hip (two passes, mixed-size batches):
-//                  one wave per piece, a size pass, a scan, an emit pass.
+//                  pieces of 4 Ki words or more and small message batches):
+//                  a workgroup per 8192-word chunk, the chunk in VGPRs, roles
+//                  by mask algebra, a decoupled look-back for the offsets,
+//                  strings (tag + v_perm-compacted bytes + count) OR-ed into
+//                  an LDS ring, 16-byte line stores; its sparse form
+//                  (cpk_sparse, below: words re-read in B, twice the
+//                  workgroups) for batches whose sampled words are >= 85 %
+//                  zero; encode_v4.hip (two passes, mixed-size and small-
+//                  piece batches): one wave per piece, a size pass, a scan,
+//                  an emit pass.  The device chooses (e4_gate_kernel).
 //   decoders       decode_kernel: one wave per piece, packed bytes staged in
 //                  LDS window by window, the tag chain found by speculative
 //                  per-lane walks with pointer-doubling validation, then a
