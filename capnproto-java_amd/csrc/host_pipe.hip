@@ -96,6 +96,43 @@ void pipe_destroy(HostPipe *p) {
 }
 
 // the context's pipe with staging of at least the given sizes (grow-only)
+// One large transfer through a pinned slot, pipelined in chunks of
+// kPipeChunk: the threaded host copy of chunk k+1 overlaps the DMA of chunk k
+// (single-slot host forms: one message or stream of unknown length).
+constexpr uint64_t kPipeChunk = 16ull << 20;
+// host src -> pinned -> device: every chunk's H2D is enqueued on s as soon as
+// its bytes are in the pinned buffer (which is not reused before s drains)
+int h2d_pipelined(void *dev, void *pin, const void *src, uint64_t bytes, hipStream_t s) {
+  for (uint64_t a = 0; a < bytes; a += kPipeChunk) {
+    const uint64_t n = bytes - a < kPipeChunk ? bytes - a : kPipeChunk;
+    par_copy((char *)pin + a, (const char *)src + a, n);
+    if (hipMemcpyAsync((char *)dev + a, (const char *)pin + a, n, hipMemcpyHostToDevice, s) != hipSuccess)
+      return CPK_EDEVICE;
+  }
+  return CPK_OK;
+}
+// device -> pinned -> host dst: two chunks' D2H in flight on s, each copied
+// on to dst once its event fires (e0 / e1: two free events of the slot)
+int d2h_pipelined(void *dst, void *pin, const void *dev, uint64_t bytes, hipStream_t s, hipEvent_t e0,
+                  hipEvent_t e1) {
+  const uint64_t nc = (bytes + kPipeChunk - 1) / kPipeChunk;
+  hipEvent_t ev[2] = {e0, e1};
+  auto issue = [&](uint64_t k) {
+    const uint64_t a = k * kPipeChunk, n = bytes - a < kPipeChunk ? bytes - a : kPipeChunk;
+    return hipMemcpyAsync((char *)pin + a, (const char *)dev + a, n, hipMemcpyDeviceToHost, s) == hipSuccess &&
+           hipEventRecord(ev[k & 1], s) == hipSuccess;
+  };
+  for (uint64_t k = 0; k < nc && k < 2; ++k)
+    if (!issue(k)) return CPK_EDEVICE;
+  for (uint64_t k = 0; k < nc; ++k) {
+    if (hipEventSynchronize(ev[k & 1]) != hipSuccess) return CPK_EDEVICE;
+    const uint64_t a = k * kPipeChunk, n = bytes - a < kPipeChunk ? bytes - a : kPipeChunk;
+    if (k + 2 < nc && !issue(k + 2)) return CPK_EDEVICE;  // (its event: chunk k's, now consumed)
+    par_copy((char *)dst + a, (const char *)pin + a, n);
+  }
+  return CPK_OK;
+}
+
 int pipe_get(cpk_ctx ctx, uint64_t in_bytes, uint64_t out_bytes, uint64_t meta, HostPipe **out) {
   HostPipe *p = ctx->pipe;
   if (!p) {

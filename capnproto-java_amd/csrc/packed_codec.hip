@@ -2105,25 +2105,28 @@ int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
   int rc = pipe_get(ctx, R, words * 8, 2 * (n + 1ull) + n / 2 + 1, &p);
   if (rc) return rc;
   HostSlot &sl = p->slot[0];
-  par_copy(sl.pin_in, h_packed, R);
-  memset((uint8_t *)sl.pin_in + R, 0, 64);  // (the decoder's read slack)
   uint64_t *m = sl.pin_meta, *dm = sl.d_meta;
   for (uint32_t i = 0; i <= n; ++i) m[i] = h_swo[i] - h_swo[0];
-  if (hipMemcpyAsync(sl.d_in, sl.pin_in, R + 64, hipMemcpyHostToDevice, p->sk) ||
-      hipMemcpyAsync(dm, m, (n + 1) * 8ull, hipMemcpyHostToDevice, p->sk))
+  memset((uint8_t *)sl.pin_in + R, 0, 64);  // (the decoder's read slack)
+  if (hipMemcpyAsync(dm, m, (n + 1) * 8ull, hipMemcpyHostToDevice, p->sk) ||
+      h2d_pipelined(sl.d_in, sl.pin_in, h_packed, R, p->sk) ||
+      hipMemcpyAsync((uint8_t *)sl.d_in + R, (uint8_t *)sl.pin_in + R, 64, hipMemcpyHostToDevice, p->sk))
     return CPK_EDEVICE;
   rc = cpk_decode_stream(ctx, sl.d_in, R, dm, n, sl.d_out, dm + n + 1, (int32_t *)(dm + 2 * (n + 1ull)), p->sk);
   if (rc) {
     pipe_drain(p);
     return rc;
   }
-  if (hipMemcpyAsync(m + n + 1, dm + n + 1, (n + 1) * 8ull + n * 4ull, hipMemcpyDeviceToHost, p->sk) ||
-      (words && hipMemcpyAsync(sl.pin_out, sl.d_out, words * 8, hipMemcpyDeviceToHost, p->sk)) ||
-      hipStreamSynchronize(p->sk))
+  if (hipMemcpyAsync(m + n + 1, dm + n + 1, (n + 1) * 8ull + n * 4ull, hipMemcpyDeviceToHost, p->sk))
     return CPK_EDEVICE;
+  if (words) {
+    if (d2h_pipelined((uint8_t *)h_out + 8 * h_swo[0], sl.pin_out, sl.d_out, words * 8, p->sk, sl.eh, sl.ed))
+      return CPK_EDEVICE;
+  } else if (hipStreamSynchronize(p->sk)) {
+    return CPK_EDEVICE;
+  }
   memcpy(h_in_off, m + n + 1, (n + 1) * 8ull);
   memcpy(h_status, m + 2 * (n + 1ull), n * 4ull);
-  if (words) par_copy((uint8_t *)h_out + 8 * h_swo[0], sl.pin_out, words * 8);
   for (uint32_t i = 0; i < n; ++i)
     if (h_status[i] != CPK_OK) return h_status[i];
   return CPK_OK;
@@ -2141,10 +2144,12 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   int rc = pipe_get(ctx, R, (out_cap_words + cpk::kRmHead) * 8, kRmInfo, &p);
   if (rc) return rc;
   HostSlot &sl = p->slot[0];
-  par_copy(sl.pin_in, h_packed, R);
-  memset((uint8_t *)sl.pin_in + R, 0, 64);  // (the decoder's read slack)
   uint64_t *info = sl.pin_meta;
-  if (hipMemcpyAsync(sl.d_in, sl.pin_in, R + 64, hipMemcpyHostToDevice, p->sk))
+  // (the bytes chunk by chunk, DMA under the host copy; then the decoder's
+  // 64 bytes of read slack)
+  memset((uint8_t *)sl.pin_in + R, 0, 64);
+  if (h2d_pipelined(sl.d_in, sl.pin_in, h_packed, R, p->sk) ||
+      hipMemcpyAsync((uint8_t *)sl.d_in + R, (uint8_t *)sl.pin_in + R, 64, hipMemcpyHostToDevice, p->sk))
     return CPK_EDEVICE;
   rc = cpk_read_message(ctx, sl.d_in, R, traversal_limit_words, sl.d_out, out_cap_words, sl.d_meta, p->sk);
   if (rc) {
@@ -2163,11 +2168,10 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   if (st != CPK_OK) return st;
   // the segments only (the table's words lead the device buffer)
   const uint64_t w0 = info[4], words = info[4 + count] - w0;
-  if (words && (hipMemcpyAsync(sl.pin_out, (uint64_t *)sl.d_out + w0, words * 8, hipMemcpyDeviceToHost, p->sk) ||
-                hipStreamSynchronize(p->sk)))
-    return CPK_EDEVICE;
   for (uint32_t i = 0; i <= count; ++i) h_info[4 + i] = info[4 + i] - w0;
-  if (words) par_copy(h_out, sl.pin_out, words * 8);
+  // (the words chunk by chunk: each chunk's copy-out under the next's DMA)
+  if (words && d2h_pipelined(h_out, sl.pin_out, (uint64_t *)sl.d_out + w0, words * 8, p->sk, sl.eh, sl.ed))
+    return CPK_EDEVICE;
   return CPK_OK;
 }
 
