@@ -607,10 +607,10 @@ __global__ __launch_bounds__(256) void e4_minmax_kernel(const uint64_t *__restri
 // Among single-pass batches, those whose sampled words are at least 85 %
 // zero take its sparse form (cpk_sparse: tickets[kTkGate + 6] = 1; config 4
 // encode -7 %, config 2 +36 %).
-__global__ void e4_gate_kernel(uint32_t *tickets, uint32_t samples) {
+__global__ void e4_gate_kernel(uint32_t *tickets, uint32_t samples, uint32_t force) {
   const uint32_t lo = tickets[kTkGate], hi = tickets[kTkGate + 1];
   const bool sp = lo >= 4096u && 2u * lo >= hi;
-  const bool sparse = sp && (uint64_t)tickets[kTkGate + 3] * 100u >= (uint64_t)samples * 85u;
+  const bool sparse = sp && (force ? force == 2u : (uint64_t)tickets[kTkGate + 3] * 100u >= (uint64_t)samples * 85u);
   if (threadIdx.x == 0) {
     tickets[kTkGate + 6] = sparse ? 1u : 0u;
     tickets[kTkGate + 2] = sp ? 1u : 0u;

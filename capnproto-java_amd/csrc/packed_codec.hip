@@ -1368,6 +1368,7 @@ struct cpk_ctx_s {
   uint64_t status_cap;    // entries
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
   int encoder;            // 0: single pass (encode_sp.hip); 4: size + emit passes; 5: by piece size
+  int sp_form;            // the single pass's form: 0 by density, 1 dense, 2 sparse (CPK_SP_FORM)
   int decoder;            // 2: record index (decode_v2.hip); 1: block map (decode_kernel); 3: by density
   uint64_t *sp_status;    // single pass: look-back word per piece
   uint64_t sp_cap;        //   entries
@@ -1471,6 +1472,10 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     // batches sp_takes admits.  CPK_ENCODER=0 / 4 force one of them.
     const char *e = getenv("CPK_ENCODER");
     c->encoder = (e && e[0] == '4') ? 4 : (e && e[0] == '0') ? 0 : 5;
+    // CPK_SP_FORM=dense / sparse forces the single pass's form where the
+    // gate picks the single pass (A/B of the density threshold)
+    const char *f = getenv("CPK_SP_FORM");
+    c->sp_form = (f && f[0] == 'd') ? 1 : (f && f[0] == 's') ? 2 : 0;
     // CPK_DECODER=1 selects the block-map decoder, 2 the record-index one
     const char *d = getenv("CPK_DECODER");
     c->decoder = (d && d[0] == '2') ? 2 : (d && d[0] == '1') ? 1 : 3;
@@ -1661,7 +1666,7 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
       return CPK_EDEVICE;
     const unsigned mg = n < 256u * 256u ? (unsigned)((n + 255) / 256) : 256u;
     hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3(mg), dim3(256), 0, s, d_swo, n, mm, (const uint64_t *)d_in);
-    hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets, mg * 256u);
+    hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets, mg * 256u, (uint32_t)ctx->sp_form);
   }
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (n + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (n + cpk::kE4Waves - 1) / cpk::kE4Waves;

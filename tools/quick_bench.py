@@ -45,7 +45,11 @@ for spec in libs:
     handles.append((spec.split("/")[-1], L, ctx))
 for cfg in cfgs:
     cp._lib = handles[0][1]
-    handles[0][2].generate(cp.preset(cfg), d_swo, d_in)
+    gp = cp.preset(cfg)
+    if __import__("os").environ.get("QB_Z"):  # (a custom density: QB_Z zero fraction, QB_LZ mean zero run)
+        _e = __import__("os").environ
+        gp = cp.gen_params(cfg, float(_e["QB_Z"]), float(_e.get("QB_LZ", "16")), 0.25)
+    handles[0][2].generate(gp, d_swo, d_in)
     torch.cuda.synchronize()
     U = int(swo[-1]) * 8
     print(f"config {cfg}: n={n}", flush=True)
