@@ -262,7 +262,7 @@ void gather_copy(uint8_t *dst, const void *const *pieces, const uint64_t *swo, u
 // input slot
 template <class CopyIn>
 int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_t n, void *h_out,
-                     uint64_t h_out_cap, uint64_t *h_out_off) {
+                     uint64_t h_out_cap, uint64_t *h_out_off, const uint8_t *contig = nullptr) {
   if (n == 0) {
     h_out_off[0] = 0;
     return CPK_OK;
@@ -283,15 +283,28 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
   uint8_t *dst = (uint8_t *)h_out;
   uint64_t base = 0;          // output bytes so far
   const size_t K = cs.size();
+  // one large chunk (e.g. a single big piece): nothing to overlap it with,
+  // so its own transfers are pipelined in 16 MiB chunks instead
+  const bool one = K == 1 && cs[0].in_len >= 2 * kPipeChunk;
   for (size_t k = 0; k <= K + 1 && rc == CPK_OK; ++k) {
     if (k < K) {  // copy-in, H2D, kernels of chunk k
       const HostChunk &c = cs[k];
       HostSlot &s = p->slot[k & 1];
       const uint32_t nk = c.i1 - c.i0;
-      copy_in((uint8_t *)s.pin_in, c);
       for (uint32_t j = 0; j <= nk; ++j) s.pin_meta[j] = h_swo[c.i0 + j] - h_swo[c.i0];
-      if ((c.in_len && hipMemcpyAsync(s.d_in, s.pin_in, c.in_len, hipMemcpyHostToDevice, p->sh)) ||
-          hipMemcpyAsync(s.d_meta, s.pin_meta, (nk + 1) * 8ull, hipMemcpyHostToDevice, p->sh) ||
+      if (one && contig) {
+        if (h2d_pipelined(s.d_in, s.pin_in, contig + c.in0, c.in_len, p->sh)) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+      } else {
+        copy_in((uint8_t *)s.pin_in, c);
+        if (c.in_len && hipMemcpyAsync(s.d_in, s.pin_in, c.in_len, hipMemcpyHostToDevice, p->sh)) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+      }
+      if (hipMemcpyAsync(s.d_meta, s.pin_meta, (nk + 1) * 8ull, hipMemcpyHostToDevice, p->sh) ||
           hipEventRecord(s.eh, p->sh) || hipStreamWaitEvent(p->sk, s.eh, 0) ||
           (k >= 2 && hipStreamWaitEvent(p->sk, s.ed, 0))) {  // (d_out free: chunk k-2's D2H)
         rc = CPK_EDEVICE;
@@ -326,6 +339,16 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
         break;
       }
       for (uint32_t j = 0; j <= nk; ++j) h_out_off[c.i0 + j] = base + off[j];
+      if (one && P >= 2 * kPipeChunk) {
+        // (the one chunk's copy-out under its own D2H; the events of the
+        // other slot are free)
+        if (d2h_pipelined(dst + base, s.pin_out, s.d_out, P, p->sd, p->slot[1].eh, p->slot[1].ed)) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+        base += P;
+        break;
+      }
       if ((P && hipMemcpyAsync(s.pin_out, s.d_out, P, hipMemcpyDeviceToHost, p->sd)) ||
           hipEventRecord(s.ed, p->sd)) {
         rc = CPK_EDEVICE;
@@ -363,7 +386,7 @@ int cpk_encode_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_swo, uint32
   const uint8_t *src = (const uint8_t *)h_in;
   return encode_host_impl(
       ctx, [&](uint8_t *pin, const HostChunk &c) { par_copy(pin, src + c.in0, c.in_len); }, h_swo,
-      n, h_out, h_out_cap, h_out_off);
+      n, h_out, h_out_cap, h_out_off, src);
 }
 
 int cpk_encode_host_gather(cpk_ctx ctx, const void *const *h_pieces, const uint64_t *h_swo,
@@ -385,6 +408,27 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
     if (h_swo[i + 1] < h_swo[i] || h_in_off[i + 1] < h_in_off[i]) return CPK_EINVAL;
   if ((!h_packed && h_in_off[n] > h_in_off[0]) || (!h_out && h_swo[n] > h_swo[0])) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
+  if (n <= 32 && h_swo[n] - h_swo[0] >= ((uint64_t)n << 20)) {
+    // A few large pieces (>= 8 MiB of words each on average): the batch
+    // decoder gives a piece one wave (one 64 MiB piece: 104 ms), so decode
+    // them as one stream, 256-byte blocks in parallel (cpk_decode_stream),
+    // and keep that when every piece ended exactly where its packed range
+    // does -- then each read() consumed exactly its bytes, as the batch
+    // decode requires; otherwise (an error, or a piece ending elsewhere) the
+    // batch decoder below gives each piece its own status.
+    std::vector<uint64_t> sin(n + 1);
+    std::vector<int32_t> sst(n);
+    const uint8_t *sp = (const uint8_t *)h_packed + (h_packed ? h_in_off[0] : 0);
+    if (cpk_decode_stream_host(ctx, sp, h_in_off[n] - h_in_off[0], h_swo, n, h_out, sin.data(), sst.data()) ==
+        CPK_OK) {
+      bool same = true;
+      for (uint32_t i = 0; i <= n && same; ++i) same = sin[i] == h_in_off[i] - h_in_off[0];
+      if (same) {
+        for (uint32_t i = 0; i < n; ++i) h_status[i] = CPK_OK;
+        return CPK_OK;
+      }
+    }
+  }
   const std::vector<HostChunk> cs = host_chunks(h_swo, h_in_off, n, host_chunk_bytes());
   uint64_t mi = 0, mo = 0, mm = 0;
   for (const HostChunk &c : cs) {
@@ -399,20 +443,35 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
   const uint8_t *src = (const uint8_t *)h_packed;
   uint8_t *dst = (uint8_t *)h_out;
   const size_t K = cs.size();
+  // one large chunk (a single big piece): its own transfers pipelined in
+  // 16 MiB chunks (encode_host_impl likewise)
+  const bool one = K == 1 && cs[0].out_cap >= 2 * kPipeChunk;
   for (size_t k = 0; k <= K + 1 && rc == CPK_OK; ++k) {
     if (k < K) {  // copy-in, H2D, decode of chunk k
       const HostChunk &c = cs[k];
       HostSlot &s = p->slot[k & 1];
       const uint32_t nk = c.i1 - c.i0;
-      par_copy(s.pin_in, src + c.in0, c.in_len);
       memset((uint8_t *)s.pin_in + c.in_len, 0, 32);  // (the decoder reads whole 16-byte lines)
       for (uint32_t j = 0; j <= nk; ++j) {
         s.pin_meta[j] = h_swo[c.i0 + j] - h_swo[c.i0];
         s.pin_meta[nk + 1 + j] = h_in_off[c.i0 + j] - h_in_off[c.i0];
       }
       int32_t *st = (int32_t *)(s.d_meta + 2 * (nk + 1));
-      if (hipMemcpyAsync(s.d_in, s.pin_in, c.in_len + 32, hipMemcpyHostToDevice, p->sh) ||
-          hipMemcpyAsync(s.d_meta, s.pin_meta, 2 * (nk + 1) * 8ull, hipMemcpyHostToDevice, p->sh) ||
+      if (one) {
+        if (h2d_pipelined(s.d_in, s.pin_in, src + c.in0, c.in_len, p->sh) ||
+            hipMemcpyAsync((uint8_t *)s.d_in + c.in_len, (uint8_t *)s.pin_in + c.in_len, 32, hipMemcpyHostToDevice,
+                           p->sh)) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+      } else {
+        par_copy(s.pin_in, src + c.in0, c.in_len);
+        if (hipMemcpyAsync(s.d_in, s.pin_in, c.in_len + 32, hipMemcpyHostToDevice, p->sh)) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+      }
+      if (hipMemcpyAsync(s.d_meta, s.pin_meta, 2 * (nk + 1) * 8ull, hipMemcpyHostToDevice, p->sh) ||
           hipEventRecord(s.eh, p->sh) || hipStreamWaitEvent(p->sk, s.eh, 0) ||
           (k >= 2 && hipStreamWaitEvent(p->sk, s.ed, 0))) {
         rc = CPK_EDEVICE;
@@ -435,6 +494,13 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
         break;
       }
       memcpy(h_status + c.i0, s.pin_meta + 2 * (nk + 1), nk * 4ull);
+      if (one) {
+        // (its copy-out under its own D2H; the other slot's events are free)
+        if (d2h_pipelined(dst + 8 * h_swo[c.i0], s.pin_out, s.d_out, c.out_cap, p->sd, p->slot[1].eh,
+                          p->slot[1].ed))
+          rc = CPK_EDEVICE;
+        break;
+      }
       if ((c.out_cap && hipMemcpyAsync(s.pin_out, s.d_out, c.out_cap, hipMemcpyDeviceToHost, p->sd)) ||
           hipEventRecord(s.ed, p->sd)) {
         rc = CPK_EDEVICE;

@@ -703,3 +703,24 @@ def test_gate_edges_and_sparse_form(ctx, oracle, cfg, words):
     n = max(8, (1 << 22) // words)  # ~32 MiB per batch
     swo = _swo([words] * n)
     _check_batch(ctx, oracle, oracle.generate(oracle.preset(cfg), swo), swo)
+
+
+def test_decode_host_few_large_pieces(ctx, oracle):
+    """cpk_decode_host with a few large pieces (>= 8 MiB of words each on
+    average) decodes them as one stream in parallel and keeps that result
+    only when every piece ended exactly at its given packed boundary; a
+    piece with a trailing byte in its range (the reference's read() leaves
+    it unread: CPK_ETRAILING in the batch form) falls back to the batch
+    decoder, so the statuses are the batch form's."""
+    W = 3 << 19  # 1.5 Mi words = 12 MiB per piece
+    swo = _swo([W, W + 5, W - 7])
+    data = oracle.generate(oracle.preset(2), swo)
+    pk, off = _check_batch(ctx, oracle, data, swo)
+    # a trailing zero byte after piece 0's packed bytes, inside its range
+    pk2 = np.concatenate([pk[: off[1]], np.zeros(1, np.uint8), pk[off[1]:]])
+    off2 = off.copy()
+    off2[1:] += 1
+    dec, st = ctx.decode_host(pk2, off2, swo)
+    ost = oracle.unpack_batch(pk2, off2, swo, threads=8)[1]
+    assert list(st) == list(ost) and st[0] != 0 and (st[1:] == 0).all(), (st, ost)
+    assert np.array_equal(dec[8 * int(swo[1]):], data[8 * int(swo[1]):])
