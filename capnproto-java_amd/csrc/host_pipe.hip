@@ -573,7 +573,7 @@ std::vector<MsgChunk> enc_msg_chunks(const uint64_t *swo, const uint64_t *mso, u
 template <class Fill>
 int encode_messages_host_impl(cpk_ctx ctx, Fill fill, const uint64_t *h_swo, uint32_t nseg,
                               const uint64_t *h_msg_seg_off, uint32_t nm, void *h_out,
-                              uint64_t h_out_cap, uint64_t *h_out_off) {
+                              uint64_t h_out_cap, uint64_t *h_out_off, const uint8_t *contig = nullptr) {
   if (!ctx || !h_swo || !h_msg_seg_off || !h_out_off) return CPK_EINVAL;
   if (h_msg_seg_off[0] != 0 || h_msg_seg_off[nm] != nseg) return CPK_EINVAL;
   for (uint32_t m = 0; m < nm; ++m)
@@ -601,18 +601,31 @@ int encode_messages_host_impl(cpk_ctx ctx, Fill fill, const uint64_t *h_swo, uin
   uint8_t *dst = (uint8_t *)h_out;
   uint64_t base = 0;
   const size_t K = cs.size();
+  // one large chunk (e.g. one big message): its own transfers pipelined in
+  // 16 MiB sub-chunks (encode_host_impl likewise)
+  const bool one = K == 1 && cs[0].in_len >= 2 * kPipeChunk;
   for (size_t k = 0; k <= K + 1 && rc == CPK_OK; ++k) {
     if (k < K) {  // copy-in, H2D, kernels of chunk k
       const MsgChunk &c = cs[k];
       HostSlot &s = p->slot[k & 1];
       const uint32_t ns = (uint32_t)(c.s1 - c.s0), nmk = c.m1 - c.m0;
-      fill((uint8_t *)s.pin_in, c);
       uint64_t *m = s.pin_meta;
       for (uint32_t j = 0; j <= ns; ++j) m[j] = h_swo[c.s0 + j] - h_swo[c.s0];
       for (uint32_t j = 0; j <= nmk; ++j) m[ns + 1 + j] = h_msg_seg_off[c.m0 + j] - c.s0;
       uint64_t *dm = s.d_meta, *doff = dm + (ns + 1) + (nmk + 1);
-      if ((c.in_len && hipMemcpyAsync(s.d_in, s.pin_in, c.in_len, hipMemcpyHostToDevice, p->sh)) ||
-          hipMemcpyAsync(dm, m, ((ns + 1) + (nmk + 1)) * 8ull, hipMemcpyHostToDevice, p->sh) ||
+      if (one && contig) {
+        if (h2d_pipelined(s.d_in, s.pin_in, contig + c.in0, c.in_len, p->sh)) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+      } else {
+        fill((uint8_t *)s.pin_in, c);
+        if (c.in_len && hipMemcpyAsync(s.d_in, s.pin_in, c.in_len, hipMemcpyHostToDevice, p->sh)) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+      }
+      if (hipMemcpyAsync(dm, m, ((ns + 1) + (nmk + 1)) * 8ull, hipMemcpyHostToDevice, p->sh) ||
           hipEventRecord(s.eh, p->sh) || hipStreamWaitEvent(p->sk, s.eh, 0) ||
           (k >= 2 && hipStreamWaitEvent(p->sk, s.ed, 0))) {
         rc = CPK_EDEVICE;
@@ -647,6 +660,15 @@ int encode_messages_host_impl(cpk_ctx ctx, Fill fill, const uint64_t *h_swo, uin
       }
       // pieces in message order: chunk k-1's start at piece c.m0 + c.s0
       for (uint64_t j = 0; j <= np; ++j) h_out_off[c.m0 + c.s0 + j] = base + off[j];
+      if (one && P >= 2 * kPipeChunk) {
+        // (the one chunk's copy-out under its own D2H; the other slot's events are free)
+        if (d2h_pipelined(dst + base, s.pin_out, s.d_out, P, p->sd, p->slot[1].eh, p->slot[1].ed)) {
+          rc = CPK_EDEVICE;
+          break;
+        }
+        base += P;
+        break;
+      }
       if ((P && hipMemcpyAsync(s.pin_out, s.d_out, P, hipMemcpyDeviceToHost, p->sd)) ||
           hipEventRecord(s.ed, p->sd)) {
         rc = CPK_EDEVICE;
@@ -684,7 +706,7 @@ int cpk_encode_messages_host(cpk_ctx ctx, const void *h_in, const uint64_t *h_sw
   const uint8_t *src = (const uint8_t *)h_in + 8 * h_swo[0];
   return encode_messages_host_impl(
       ctx, [&](uint8_t *pin, const MsgChunk &c) { par_copy(pin, src + c.in0, c.in_len); }, h_swo, nseg,
-      h_msg_seg_off, nm, h_out, h_out_cap, h_out_off);
+      h_msg_seg_off, nm, h_out, h_out_cap, h_out_off, src);
 }
 
 int cpk_encode_messages_host_gather(cpk_ctx ctx, const void *const *h_segs, const uint64_t *h_swo,

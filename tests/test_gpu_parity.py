@@ -724,3 +724,13 @@ def test_decode_host_few_large_pieces(ctx, oracle):
     ost = oracle.unpack_batch(pk2, off2, swo, threads=8)[1]
     assert list(st) == list(ost) and st[0] != 0 and (st[1:] == 0).all(), (st, ost)
     assert np.array_equal(dec[8 * int(swo[1]):], data[8 * int(swo[1]):])
+
+
+def test_message_host_one_large_message(ctx, oracle):
+    """One message of one 40 MiB segment through cpk_encode_messages_host:
+    a single chunk, whose transfers are pipelined in 16 MiB sub-chunks;
+    the bytes equal the oracle's Serialize.write."""
+    swo = _swo([5 << 20])
+    seg = oracle.generate(oracle.preset(2), swo).tobytes()
+    pk, off = ctx.encode_messages_host([[seg]])
+    assert pk == oracle.write_message([seg])

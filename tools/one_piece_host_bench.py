@@ -52,3 +52,4 @@ for mib in sizes_mib:
         print(f"{mib:4d} MiB piece  {name:24s} encode_host {1e3 * np.median(te):7.2f} ms ({U / np.median(te):5.1f} GiB/s)"
               f"  decode_host {1e3 * np.median(td):7.2f} ms ({U / np.median(td):5.1f} GiB/s)  ok={ok} same={same}",
               flush=True)
+
