@@ -441,6 +441,20 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
 // per 131,072 config-4 pieces; the others to the block-map decoder (4.5
 // against 6.2 ms at config 2).  skip[0]: the block-map decoder's flag,
 // skip[1]: the record-index decoder's.
+// After a few large pieces were decoded as one stream (cpk_decode_batch):
+// when every piece ended exactly at its packed range's end and decoded, the
+// batch decoders are told to skip (both flags); else they run and give each
+// piece its batch-form status.  One block; n <= 32.
+__global__ void dec_stream_check_kernel(const uint64_t *__restrict__ found, const uint64_t *__restrict__ in_off,
+                                        const int32_t *__restrict__ st, uint32_t n, uint32_t *skip) {
+  const uint32_t i = threadIdx.x;
+  const bool ok = i > n || (found[i] == in_off[i] - in_off[0] && (i == n || st[i] == CPK_OK));
+  if (__syncthreads_and(ok) && i == 0) {
+    skip[0] = 1u;
+    skip[1] = 1u;
+  }
+}
+
 __global__ void dec_gate_kernel(const uint64_t *__restrict__ in_off, const uint64_t *__restrict__ swo, uint32_t n,
                                 uint32_t *skip) {
   if (threadIdx.x == 0) {

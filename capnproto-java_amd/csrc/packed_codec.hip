@@ -1381,6 +1381,7 @@ struct cpk_ctx_s {
   uint64_t *ss_buf;       // parallel stream decode scratch (stream_split.hip)
   uint64_t ss_cap;        //   u64 entries
   uint64_t *rm_buf;       // cpk_read_message: piece word offsets | piece ends | statuses (lazy)
+  uint64_t *fl_buf;       // cpk_decode_batch of a few large pieces: boundaries found [33] (lazy)
   uint64_t *sp_units;     // single pass, pieces over one chunk: unit counts | starts | block sums | unit table
   uint64_t sp_units_cap;  //   u64 entries
 };
@@ -1507,6 +1508,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->sp_desc) hipFree(ctx->sp_desc);
   if (ctx->ss_buf) hipFree(ctx->ss_buf);
   if (ctx->rm_buf) hipFree(ctx->rm_buf);
+  if (ctx->fl_buf) hipFree(ctx->fl_buf);
   if (ctx->sp_units) hipFree(ctx->sp_units);
   pipe_destroy(ctx->pipe);
   free(ctx);
@@ -1863,6 +1865,31 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   // one not chosen returns at its first instruction
   uint32_t *skip = ctx->tickets + cpk::kTkGate + 4;
   hipLaunchKernelGGL(cpk::dec_gate_kernel, dim3(1), dim3(64), 0, s, (const uint64_t *)d_in_off, d_swo, n, skip);
+  if (n <= 32) {
+    // A few pieces: read their extent back (one sync).  With >= 8 MiB of
+    // words each on average the batch decoders would give a piece one wave
+    // (one 64 MiB piece: ~100 ms), so decode them as one stream, 256-byte
+    // blocks in parallel, and let the batch decoders skip when every piece
+    // ended exactly at its packed range's end (dec_stream_check_kernel);
+    // otherwise they run after it and report the batch form's statuses.
+    uint64_t e[4];
+    if (hipMemcpyAsync(&e[0], d_in_off, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&e[1], d_in_off + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&e[2], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&e[3], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return CPK_EDEVICE;
+    if (e[3] - e[2] >= ((uint64_t)n << 20) && (e[0] & 15) == 0 && e[1] >= e[0]) {
+      if (!ctx->fl_buf && hipMalloc(&ctx->fl_buf, 33 * 8) != hipSuccess) return CPK_ENOMEM;
+      int rc = cpk_decode_stream(ctx, (const uint8_t *)d_packed + e[0], e[1] - e[0], d_swo, n, d_out, ctx->fl_buf,
+                                 d_status, s);
+      if (rc) return rc;
+      hipLaunchKernelGGL(cpk::dec_stream_check_kernel, dim3(1), dim3(64), 0, s, (const uint64_t *)ctx->fl_buf,
+                         (const uint64_t *)d_in_off, (const int32_t *)d_status, n, skip);
+      if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
+        return CPK_EDEVICE;
+    }
+  }
   dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, in_off, d_swo, n, (uint64_t *)d_out, d_status, 0,
              cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr, skip}, s, 1);
   dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, in_off, d_swo, n, (uint64_t *)d_out, d_status, 0,

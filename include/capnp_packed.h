@@ -144,7 +144,11 @@ int cpk_ctx_take_error(cpk_ctx ctx, void *stream);
  *   d_seg_word_off  : uint64[n+1], device; piece i's unpacked words.
  *   d_out           : 8-byte aligned; piece i -> words d_seg_word_off[i]...
  *   d_status        : int32[n], device, written per piece (CPK_* codes).
- * Returns CPK_OK if launched; per-piece results are in d_status. */
+ * Returns CPK_OK if launched; per-piece results are in d_status.  A batch of
+ * at most 32 pieces reads its extent back (one sync of `stream`): with
+ * >= 8 Mi words per piece on average it is decoded as one stream, 256-byte
+ * blocks in parallel, the batch decoders running after it only when some
+ * piece did not end exactly at its packed range's end. */
 int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off,
                      const uint64_t *d_seg_word_off, uint32_t n, void *d_out,
                      int32_t *d_status, void *stream);

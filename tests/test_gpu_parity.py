@@ -734,3 +734,37 @@ def test_message_host_one_large_message(ctx, oracle):
     seg = oracle.generate(oracle.preset(2), swo).tobytes()
     pk, off = ctx.encode_messages_host([[seg]])
     assert pk == oracle.write_message([seg])
+
+
+def test_decode_batch_few_large_pieces_device(ctx, oracle):
+    """Device-resident cpk_decode_batch of a few large pieces (>= 8 MiB of
+    words each on average; the default decoder choice): decoded as one
+    stream in parallel when every piece ends exactly at its packed range's
+    end; a trailing byte inside piece 0's range sends the batch to the batch
+    decoders, whose statuses are the batch form's (the oracle's)."""
+    import torch
+    W = 3 << 19
+    swo = _swo([W, W + 3, W - 9])
+    data = oracle.generate(oracle.preset(2), swo)
+    opk, ooff = oracle.pack_batch(data, swo, threads=8)
+    d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
+    for trailing in (False, True):
+        pk, off = opk, ooff.copy()
+        if trailing:
+            pk = np.concatenate([opk[: ooff[1]], np.zeros(1, np.uint8), opk[ooff[1]:]])
+            off[1:] += 1
+        d_pk = torch.zeros((pk.size + 64) // 16 * 16, dtype=torch.uint8, device="cuda")
+        d_pk[: pk.size] = torch.from_numpy(pk).cuda()
+        d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+        d_out = torch.zeros(int(swo[-1]), dtype=torch.int64, device="cuda")
+        d_st = torch.full((3,), -99, dtype=torch.int32, device="cuda")
+        ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
+        torch.cuda.synchronize()
+        st = d_st.cpu().numpy()
+        ost = oracle.unpack_batch(pk, off, swo, threads=8)[1]
+        assert list(st) == list(ost), (trailing, st, ost)
+        out = d_out.cpu().numpy().view(np.uint8)
+        if trailing:
+            assert st[0] != 0 and np.array_equal(out[8 * int(swo[1]):], data[8 * int(swo[1]):])
+        else:
+            assert (st == 0).all() and np.array_equal(out, data)
