@@ -1,8 +1,10 @@
 // sp_roles.hip -- the roles PackedOutputStream.write gives the words of one
 // 64-word step, as scalar mask algebra over the step's Z / D-or-L / D masks
-// and the run state entering it.  Included by encode_v4.hip (its size pass)
-// and, for the single pass's sparse form (a second namespace), again by
-// encode_sp.hip.
+// and the run state entering it (SpSt, sp_roles), and the lane helpers the
+// single pass uses with them (readfirstlane / readlane / writelane pairs,
+// v_ffbl, per-lane selects on an SGPR mask).  Included by encode_v4.hip
+// (its size pass's CPK_E4_MASKROLES form) and, for the single pass's sparse
+// form (a second namespace), again by encode_sp.hip.
 
 struct SpSt {
   uint32_t zl;   // zero run ending at the step start (0: none)
