@@ -6,4 +6,5 @@ tools/gpu_steps.sh \
  "200|r3Z_bench_config4|python bench.py --config 4 --steps 10 --warmup 2" \
  "300|r3Z_prof2|tools/profile.sh r3Z_c2 -- $B --config 2" \
  "300|r3Z_prof3|tools/profile.sh r3Z_c3 -- $B --config 3" \
- "300|r3Z_prof4|tools/profile.sh r3Z_c4 -- $B --config 4"
+ "300|r3Z_prof4|tools/profile.sh r3Z_c4 -- $B --config 4" \
+ "400|r3Z_gpu_tests|python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread"
