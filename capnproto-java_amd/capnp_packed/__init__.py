@@ -431,9 +431,11 @@ Context.read_message_host = _read_message_host
 
 
 def gen_params(cfg: int, z: float, lz: float, q: float) -> GenParams:
-    """Thresholds (out of 2^32) of the synthetic 2-state Markov generator."""
+    """Thresholds of the synthetic 2-state Markov generator, out of 2^31:
+    `FastRand.nextInt()` never returns a negative value (Common.java:31-38,
+    arithmetic `>>` clears bit 31), so a draw lies in [0, 2^31)."""
     def thr(p):
-        return int(min(max(p, 0.0), 1.0) * (1 << 32))
+        return int(min(max(p, 0.0), 1.0) * (1 << 31))
     a = 1.0 / lz
     b = 1.0 if z >= 1.0 else a * z / (1.0 - z)
     return GenParams(thr(z), thr(a), thr(b), thr(q), cfg, 0)

@@ -279,7 +279,8 @@ int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *
 /* ---- benchmark support (synthetic device-resident workloads) ---- */
 
 /* Device generator of the synthetic segments described in SURVEY.md 8d:
- * a 2-state Markov chain over words (thresholds out of 2^32), seeded per
+ * a 2-state Markov chain over words (thresholds out of 2^31: FastRand draws
+ * are never negative), seeded per
  * segment from (cfg, segment index).  Identical stream to the host copy in
  * oracle/packed_oracle.c:cpko_generate. */
 typedef struct {

@@ -52,11 +52,15 @@ class GenParams(ctypes.Structure):
 
 
 def _thr(p: float) -> int:
-    return int(min(max(p, 0.0), 1.0) * (1 << 32))
+    # FastRand.nextInt() is never negative: with Java's arithmetic `>>`
+    # (Common.java:36) bit 31 of `w ^ (w >> 19)` and of `tmp ^ (tmp >> 8)` is
+    # always clear, so every draw lies in [0, 2^31) and a probability p is the
+    # threshold p * 2^31 (round 3 used 2^32: every probability doubled).
+    return int(min(max(p, 0.0), 1.0) * (1 << 31))
 
 
 def gen_params(cfg: int, z: float, lz: float, q: float) -> GenParams:
-    """Integer thresholds (out of 2^32) of the 2-state Markov generator.
+    """Integer thresholds (out of 2^31: draws are non-negative) of the 2-state Markov generator.
     Stationary zero fraction z: P(z->n) = 1/Lz, P(n->z) = (1/Lz) z/(1-z)."""
     a = 1.0 / lz
     b = 1.0 if z >= 1.0 else a * z / (1.0 - z)

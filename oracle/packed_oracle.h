@@ -75,7 +75,8 @@ int cpko_read_message(const uint8_t *in, size_t in_len, size_t *consumed,
 /* Synthetic segment generator shared with the device generator in
  * capnproto-java_amd/csrc (bench + tests; not part of the reference).
  * PRNG core: benchmark/src/main/java/org/capnproto/benchmark/Common.java:25-38
- * (FastRand xorshift128, Java arithmetic >>).  Thresholds are out of 2^32. */
+ * (FastRand xorshift128, Java arithmetic >>).  Thresholds are out of 2^31:
+ * every draw is non-negative (bit 31 is cleared by the arithmetic shifts). */
 typedef struct {
   uint64_t t_zero0;  /* P(first word is in the zero state)   */
   uint64_t t_z2n;    /* P(zero -> nonzero) per word          */

@@ -133,6 +133,31 @@ def test_generator_presets(oracle):
         assert np.array_equal(one, d[2 * 65536:3 * 65536])
 
 
+def _run_lengths(z):
+    """Lengths of the maximal runs of True in a boolean vector."""
+    d = np.diff(np.concatenate([[0], z.astype(np.int8), [0]]))
+    return np.flatnonzero(d == -1) - np.flatnonzero(d == 1)
+
+
+def test_generator_matches_survey_workload(oracle):
+    """q (zero byte in a nonzero word) 0.25 / (1/256) / 0.25,
+    mean zero run Lz 4 / 1.5 / 64 for configs 2 / 3 / 4, on 64 pieces of
+    8192 words.  FastRand.nextInt() is never negative (Common.java:31-38),
+    so thresholds are out of 2^31 (round 3's 2^32 doubled every probability)."""
+    swo = np.arange(0, 8192 * 65, 8192, dtype=np.uint64)
+    spec = {2: (0.25, 0.01, 4.0), 3: (1 / 256, 0.001, 1.5), 4: (0.25, 0.01, 64.0)}
+    for cfg, (q, qtol, lz) in spec.items():
+        w = oracle.generate(oracle.preset(cfg), swo).view(np.uint64).reshape(64, 8192)
+        b = w.view(np.uint8).reshape(64, 8192, 8)
+        nzw = w != 0
+        qm = (b[nzw] == 0).mean()
+        assert abs(qm - q) <= qtol, (cfg, qm)
+        runs = np.concatenate([_run_lengths(~nzw[i]) for i in range(64)])
+        # runs cut by a piece's first or last word are shorter: keep interior runs
+        inner = np.concatenate([_run_lengths(~nzw[i][1:-1]) for i in range(64)])
+        assert runs.size and abs(inner.mean() - lz) <= 0.1 * lz, (cfg, inner.mean())
+
+
 def test_batch_threads_agree(oracle):
     swo = np.concatenate([[0], np.cumsum(np.array([0, 1, 3, 8192, 100, 7, 5000, 0, 2], np.uint64))]).astype(np.uint64)
     d = oracle.generate(oracle.preset(2), swo)
