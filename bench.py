@@ -24,9 +24,9 @@ Run:  python bench.py [--gpus N --steps K --warmup W --config C]
   itself (before any GPU call); under torchrun WORLD_SIZE must equal N.
   --stub: CPU-only rehearsal of the multi-rank path (gloo, the oracle as
   the "kernel"), used by tests/test_shard.py.
-  --same-device: every rank on cuda:0 with a gloo group (RCCL refuses two
-  ranks on one GPU): the real GPU rank path at N > 1 on a one-GPU box
-  (tests/test_gpu_bench_shapes.py); use a small --segments so the shards fit.
+  --same-device: every rank on cuda:0 (the real GPU rank path at N > 1 on a
+  one-GPU box, tests/test_gpu_bench_shapes.py); use a small --segments so
+  the shards fit.  Ranks talk over gloo in every mode: no RCCL anywhere.
 """
 from __future__ import annotations
 
@@ -138,10 +138,12 @@ def run_rank(args, rank, world, local):
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        if args.same_device:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # gloo in every mode: the data path has no collective (pieces are
+        # independent, Serialize.java:283-287); the group only carries the
+        # barrier around the timed region and the max / sum of a few host
+        # scalars, so an N-GPU run takes exactly the code the one-GPU
+        # --same-device rehearsal tests, but for the device each rank sets
+        dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     ctx = cp.Context(local)
 

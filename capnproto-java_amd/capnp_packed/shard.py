@@ -3,8 +3,9 @@
 Pieces are independent (PackedOutputStream.java:36-43 re-initialises run
 state per write(); Serialize.java:283-287 issues one write per segment), so a
 batch is split into contiguous piece ranges, one per rank, balanced by bytes,
-and no collective touches the data path.  torch.distributed is used only for
-the barrier around the timed region and the max-over-ranks of the timings.
+and no collective touches the data path.  torch.distributed (a gloo group,
+bench.py) is used only for the barrier around the timed region and the
+max-over-ranks of the timings.
 """
 from __future__ import annotations
 
@@ -27,7 +28,8 @@ def plan_shards(seg_word_off: np.ndarray, world: int) -> np.ndarray:
 
 def reduce_max_sum(values, group=None):
     """All-reduce a small vector of per-rank numbers: (max, sum) per entry.
-    Works with any torch.distributed backend (gloo in tests, RCCL on GPUs)."""
+    (bench.py's group is gloo in every mode; a device backend would reduce a
+    device copy)."""
     import torch
     import torch.distributed as dist
     dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"

@@ -1035,7 +1035,9 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
       w0 = swo[p];
       W64 = swo[p + 1] - w0;
     }
-    bool bad = W64 >= (1ull << 31) || (!utab && W64 > 64ull * kSpCS);
+    // (with a unit table, a piece over the hint is one empty unit: see
+    // sp_units_count_kernel)
+    bool bad = W64 >= (1ull << 31) || (!utab && W64 > 64ull * kSpCS) || (utab && hint && W64 > hint);
     if ((bad || (hint && W64 > hint)) && threadIdx.x == 0 && c == 0) atomicOr(err, 1u);
     const uint32_t W = bad ? 0u : (uint32_t)W64;  // (unsupported: sized 0, output undefined)
     const uint64_t *pw = base + w0;
@@ -1124,11 +1126,16 @@ __global__ void sp_msg_prep_kernel(const uint64_t *__restrict__ swo, const uint6
 // max(1, ceil(W / 8192)) units, one per chunk.  ucnt[p] = its unit count
 // (scanned into ustart by the e4 scan kernels), then utab[ustart[p] + k] =
 // p << 32 | k.
+// A piece the encoder cannot take (2^31 words or more, or over the caller's
+// hint) is one unit of no words, exactly as sp_encode_kernel sizes it: the
+// unit table then never outgrows the bound the host sized it by
+// (sp_unit_bound: ceil(hint / 8192) units per piece).
 __global__ void sp_units_count_kernel(const uint64_t *__restrict__ swo, const uint64_t *__restrict__ pdesc,
-                                      uint32_t n, uint64_t *__restrict__ ucnt) {
+                                      uint32_t n, uint64_t hint, uint64_t *__restrict__ ucnt) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  const uint64_t W = pdesc ? pdesc[2 * (uint64_t)p + 1] : swo[p + 1] - swo[p];
+  uint64_t W = pdesc ? pdesc[2 * (uint64_t)p + 1] : swo[p + 1] - swo[p];
+  if (W >= (1ull << 31) || (hint && W > hint)) W = 0;
   const uint64_t steps = (W + 63) >> 6;
   ucnt[p] = steps > (uint64_t)kSpCS ? (steps + kSpCS - 1) / kSpCS : 1;
 }

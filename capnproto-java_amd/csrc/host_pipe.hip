@@ -21,12 +21,12 @@ struct HostSlot {
   void *pin_in = nullptr, *pin_out = nullptr, *d_in = nullptr, *d_out = nullptr;
   uint64_t *pin_meta = nullptr, *d_meta = nullptr;
   hipEvent_t eh = nullptr, ek = nullptr, ed = nullptr;  // H2D done, kernels done, D2H done
+  uint64_t cap_in = 0, cap_out = 0, cap_meta = 0;       // bytes, bytes, u64 entries
 };
 
 struct HostPipe {
   hipStream_t sh = nullptr, sk = nullptr, sd = nullptr;
   HostSlot slot[2];
-  uint64_t cap_in = 0, cap_out = 0, cap_meta = 0;  // bytes, bytes, u64 entries
   bool ok = false;
 };
 
@@ -64,18 +64,20 @@ void par_copy(void *dst, const void *src, uint64_t bytes) {
   for (auto &t : ts) t.join();
 }
 
+void slot_free_buffers(HostSlot &s) {
+  if (s.pin_in) hipHostFree(s.pin_in);
+  if (s.pin_out) hipHostFree(s.pin_out);
+  if (s.pin_meta) hipHostFree(s.pin_meta);
+  if (s.d_in) hipFree(s.d_in);
+  if (s.d_out) hipFree(s.d_out);
+  if (s.d_meta) hipFree(s.d_meta);
+  s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
+  s.pin_meta = s.d_meta = nullptr;
+  s.cap_in = s.cap_out = s.cap_meta = 0;
+}
+
 void pipe_free_buffers(HostPipe *p) {
-  for (HostSlot &s : p->slot) {
-    if (s.pin_in) hipHostFree(s.pin_in);
-    if (s.pin_out) hipHostFree(s.pin_out);
-    if (s.pin_meta) hipHostFree(s.pin_meta);
-    if (s.d_in) hipFree(s.d_in);
-    if (s.d_out) hipFree(s.d_out);
-    if (s.d_meta) hipFree(s.d_meta);
-    s.pin_in = s.pin_out = s.d_in = s.d_out = nullptr;
-    s.pin_meta = s.d_meta = nullptr;
-  }
-  p->cap_in = p->cap_out = p->cap_meta = 0;
+  for (HostSlot &s : p->slot) slot_free_buffers(s);
 }
 
 void pipe_destroy(HostPipe *p) {
@@ -133,7 +135,10 @@ int d2h_pipelined(void *dst, void *pin, const void *dev, uint64_t bytes, hipStre
   return CPK_OK;
 }
 
-int pipe_get(cpk_ctx ctx, uint64_t in_bytes, uint64_t out_bytes, uint64_t meta, HostPipe **out) {
+// (nslots: the slots the caller stages through -- the single-slot forms, one
+// message or stream of unknown length, grow slot 0 alone, so a large one
+// does not also pin and allocate the same again in slot 1)
+int pipe_get(cpk_ctx ctx, uint64_t in_bytes, uint64_t out_bytes, uint64_t meta, HostPipe **out, int nslots = 2) {
   HostPipe *p = ctx->pipe;
   if (!p) {
     p = new HostPipe();
@@ -150,24 +155,24 @@ int pipe_get(cpk_ctx ctx, uint64_t in_bytes, uint64_t out_bytes, uint64_t meta, 
   if (!p->ok) return CPK_EDEVICE;
   in_bytes = (in_bytes + 64 + 4095) & ~4095ull;  // (+ the decoder's zero read slack)
   out_bytes = (out_bytes + 64 + 4095) & ~4095ull;
-  if (in_bytes > p->cap_in || out_bytes > p->cap_out || meta > p->cap_meta) {
-    const uint64_t ci = in_bytes > p->cap_in ? in_bytes : p->cap_in;
-    const uint64_t co = out_bytes > p->cap_out ? out_bytes : p->cap_out;
-    const uint64_t cm = meta > p->cap_meta ? meta : p->cap_meta;
-    pipe_free_buffers(p);
-    for (HostSlot &s : p->slot) {
-      if (hipHostMalloc(&s.pin_in, ci, hipHostMallocDefault) != hipSuccess ||
-          hipHostMalloc(&s.pin_out, co, hipHostMallocDefault) != hipSuccess ||
-          hipHostMalloc((void **)&s.pin_meta, cm * 8, hipHostMallocDefault) != hipSuccess ||
-          hipMalloc(&s.d_in, ci) != hipSuccess || hipMalloc(&s.d_out, co) != hipSuccess ||
-          hipMalloc((void **)&s.d_meta, cm * 8) != hipSuccess) {
-        pipe_free_buffers(p);
-        return CPK_ENOMEM;
-      }
+  for (int i = 0; i < nslots; ++i) {
+    HostSlot &s = p->slot[i];
+    if (in_bytes <= s.cap_in && out_bytes <= s.cap_out && meta <= s.cap_meta) continue;
+    const uint64_t ci = in_bytes > s.cap_in ? in_bytes : s.cap_in;
+    const uint64_t co = out_bytes > s.cap_out ? out_bytes : s.cap_out;
+    const uint64_t cm = meta > s.cap_meta ? meta : s.cap_meta;
+    slot_free_buffers(s);
+    if (hipHostMalloc(&s.pin_in, ci, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&s.pin_out, co, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&s.pin_meta, cm * 8, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&s.d_in, ci) != hipSuccess || hipMalloc(&s.d_out, co) != hipSuccess ||
+        hipMalloc((void **)&s.d_meta, cm * 8) != hipSuccess) {
+      pipe_free_buffers(p);
+      return CPK_ENOMEM;
     }
-    p->cap_in = ci;
-    p->cap_out = co;
-    p->cap_meta = cm;
+    s.cap_in = ci;
+    s.cap_out = co;
+    s.cap_meta = cm;
   }
   *out = p;
   return CPK_OK;
@@ -415,7 +420,10 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
     // and keep that when every piece ended exactly where its packed range
     // does -- then each read() consumed exactly its bytes, as the batch
     // decode requires; otherwise (an error, or a piece ending elsewhere) the
-    // batch decoder below gives each piece its own status.
+    // batch decoder below gives each piece its own status.  It stages the
+    // whole stream through slot 0 alone (pinned + device buffers of the
+    // packed bytes and the words, grown once and kept by the context: the
+    // same memory a batch chunk of these pieces would take in one slot).
     std::vector<uint64_t> sin(n + 1);
     std::vector<int32_t> sst(n);
     const uint8_t *sp = (const uint8_t *)h_packed + (h_packed ? h_in_off[0] : 0);
@@ -477,7 +485,7 @@ int cpk_decode_host(cpk_ctx ctx, const void *h_packed, const uint64_t *h_in_off,
         rc = CPK_EDEVICE;
         break;
       }
-      rc = cpk_decode_batch(ctx, s.d_in, s.d_meta + nk + 1, s.d_meta, nk, s.d_out, st, p->sk);
+      rc = decode_batch_impl(ctx, s.d_in, s.d_meta + nk + 1, s.d_meta, nk, s.d_out, st, p->sk, false);
       if (rc) break;
       if (hipMemcpyAsync(s.pin_meta + 2 * (nk + 1), st, nk * 4ull, hipMemcpyDeviceToHost, p->sk) ||
           hipEventRecord(s.ek, p->sk)) {
@@ -798,7 +806,7 @@ int cpk_decode_messages_host(cpk_ctx ctx, const void *h_packed, const uint64_t *
         break;
       }
       // room in the slot for the chunk's words and segments?
-      if (tot[0] * 8 + 64 > p->cap_out || meta_need(nmk, tot[1]) > p->cap_meta) {
+      if (tot[0] * 8 + 64 > s.cap_out || meta_need(nmk, tot[1]) > s.cap_meta) {
         if (attempt) {
           rc = CPK_EDEVICE;
           break;

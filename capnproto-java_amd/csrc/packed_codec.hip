@@ -1416,6 +1416,8 @@ int ensure_status(cpk_ctx ctx, uint64_t n) {
 }
 }  // namespace
 
+static int decode_batch_impl(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off, const uint64_t *d_swo,
+                             uint32_t n, void *d_out, int32_t *d_status, void *stream, bool probe);
 #include "host_pipe.hip"
 
 extern "C" {
@@ -1569,7 +1571,7 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
     }
     uint64_t *ucnt = ctx->sp_units, *ustart = ucnt + n, *bsum = ustart + (n + 1), *tab = bsum + nb + 1;
     const unsigned tb = 256, tg = (n + tb - 1) / tb;
-    hipLaunchKernelGGL(cpk::sp_units_count_kernel, dim3(tg), dim3(tb), 0, s, d_swo, pdesc, n, ucnt);
+    hipLaunchKernelGGL(cpk::sp_units_count_kernel, dim3(tg), dim3(tb), 0, s, d_swo, pdesc, n, hint, ucnt);
     hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s, (const uint64_t *)ucnt, n,
                        bsum);
     hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bsum, nb);
@@ -1844,9 +1846,26 @@ void dec_launch(cpk_ctx ctx, bool stream, unsigned want, const uint8_t *packed, 
 }
 }  // namespace
 
+// probe: a batch of <= 32 pieces may read its extent back (one sync) to
+// decode a few large pieces as one stream.  The host forms pass false: they
+// know the sizes and take that path themselves (cpk_decode_host), so their
+// two-slot pipeline never blocks on it; nor does a stream being captured.
+
 int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off,
                      const uint64_t *d_swo, uint32_t n, void *d_out, int32_t *d_status,
                      void *stream) {
+  bool probe = n <= 32;
+  if (probe && ctx) {
+    DeviceGuard g(ctx->device);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+      probe = false;
+  }
+  return decode_batch_impl(ctx, d_packed, d_in_off, d_swo, n, d_out, d_status, stream, probe);
+}
+
+static int decode_batch_impl(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off, const uint64_t *d_swo,
+                             uint32_t n, void *d_out, int32_t *d_status, void *stream, bool probe) {
   if (!ctx || (n && (!d_in_off || !d_swo || !d_status))) return CPK_EINVAL;
   if (((uintptr_t)d_packed & 15) || ((uintptr_t)d_out & 7)) return CPK_EINVAL;
   if (n == 0) return CPK_OK;
@@ -1865,7 +1884,7 @@ int cpk_decode_batch(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off
   // one not chosen returns at its first instruction
   uint32_t *skip = ctx->tickets + cpk::kTkGate + 4;
   hipLaunchKernelGGL(cpk::dec_gate_kernel, dim3(1), dim3(64), 0, s, (const uint64_t *)d_in_off, d_swo, n, skip);
-  if (n <= 32) {
+  if (probe && n <= 32) {
     // A few pieces: read their extent back (one sync).  With >= 8 MiB of
     // words each on average the batch decoders would give a piece one wave
     // (one 64 MiB piece: ~100 ms), so decode them as one stream, 256-byte
@@ -2134,7 +2153,7 @@ int cpk_decode_stream_host(cpk_ctx ctx, const void *h_packed, uint64_t avail,
   const uint64_t R = ss_reach(avail, words);
   HostPipe *p = nullptr;
   // meta: swo | in_off | status (int32)
-  int rc = pipe_get(ctx, R, words * 8, 2 * (n + 1ull) + n / 2 + 1, &p);
+  int rc = pipe_get(ctx, R, words * 8, 2 * (n + 1ull) + n / 2 + 1, &p, 1);
   if (rc) return rc;
   HostSlot &sl = p->slot[0];
   uint64_t *m = sl.pin_meta, *dm = sl.d_meta;
@@ -2173,7 +2192,7 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   // `avail` may be later messages)
   const uint64_t R = ss_reach(avail, out_cap_words + cpk::kRmHead);
   HostPipe *p = nullptr;
-  int rc = pipe_get(ctx, R, (out_cap_words + cpk::kRmHead) * 8, kRmInfo, &p);
+  int rc = pipe_get(ctx, R, (out_cap_words + cpk::kRmHead) * 8, kRmInfo, &p, 1);
   if (rc) return rc;
   HostSlot &sl = p->slot[0];
   uint64_t *info = sl.pin_meta;

@@ -37,6 +37,6 @@ public final class GpuPacked implements Compression {
         // ArrayInputStream; client / server: the wrapper's windows until the
         // message decodes), or the reference's PackedInputStream
         org.capnproto.MessageReader m = GpuDispatch.read(inputStream, ReaderOptions.DEFAULT_READER_OPTIONS);
-        return m != null ? m : SerializePacked.read(GpuDispatch.source(inputStream));
+        return m != null ? m : SerializePacked.read(inputStream);
     }
 }

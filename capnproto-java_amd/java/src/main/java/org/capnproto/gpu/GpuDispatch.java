@@ -17,15 +17,19 @@
 // from the message's segment table, peeked (not consumed) from the bytes the
 // stream has buffered.
 //
-// Streams: bytes a GPU read takes from a stream past its message (a
-// message's packed length is known only once it is decoded) stay in a
-// per-stream Source that every later SerializePacked call on that stream --
-// GPU or reference path -- reads first.  Such a stream must then only be read
-// through SerializePacked.  Channels (readFromUnbuffered) get one persistent
-// Source each, so, unlike the reference's per-call 8 KiB wrapper
-// (SerializePacked.java:92-96), no bytes past a message are dropped.  No lock
-// is held across a blocking read: the only shared state is the weak map of
-// Sources, locked for lookups.
+// Streams: a GPU read consumes exactly the bytes the reference's
+// PackedInputStream would -- up to the end of the record that completes the
+// message's last word (PackedInputStream.java:47-59, :84-88).  The message's
+// packed extent is found on the host by walking record headers only
+// (tag, count, literal-run skip; no bytes are expanded), buffer by buffer:
+// every upstream read buffer the message fills completely is taken, the last
+// one is advanced only by the bytes the message used, so the stream can go
+// on being read by anything (Serialize.read, a direct read, the GPU).
+// Channels (readFromUnbuffered) get one persistent Source each, so, unlike
+// the reference's per-call 8 KiB wrapper (SerializePacked.java:92-96), no
+// bytes past a message are dropped.  No lock is held across a blocking read:
+// the only shared state is the weak map of channel Sources, locked for
+// lookups.
 package org.capnproto.gpu;
 
 import java.io.IOException;
@@ -111,13 +115,6 @@ public final class GpuDispatch {
 
     private static final Map<Object, Source> SOURCES = Collections.synchronizedMap(new WeakHashMap<>());
 
-    /** The stream SerializePacked must read `input` through: its Source when
-     *  a GPU read left bytes there (or ever took bytes from it), else input. */
-    public static org.capnproto.BufferedInputStream source(org.capnproto.BufferedInputStream input) {
-        Source s = SOURCES.get(input);
-        return s != null ? s : input;
-    }
-
     /** The persistent buffered stream of a channel (readFromUnbuffered /
      *  tryReadFromUnbuffered read through it, GPU or reference path). */
     public static org.capnproto.BufferedInputStream stream(ReadableByteChannel channel) {
@@ -128,49 +125,38 @@ public final class GpuDispatch {
         }
     }
 
-    private static Source sourceFor(org.capnproto.BufferedInputStream input) {
-        if (input instanceof Source) return (Source) input;
-        synchronized (SOURCES) {
-            Source s = SOURCES.get(input);
-            if (s == null) SOURCES.put(input, s = new Source(input));
-            return s;
-        }
-    }
-
     /** SerializePacked.read(input, options): the message, read on the GPU;
      *  null when it is below MIN_BYTES (or its table is not yet buffered) --
-     *  nothing consumed, the caller runs the reference path over
-     *  source(input). */
+     *  nothing consumed, the caller runs the reference path over input. */
     public static org.capnproto.MessageReader read(org.capnproto.BufferedInputStream input,
                                                    org.capnproto.ReaderOptions options) throws IOException {
-        org.capnproto.BufferedInputStream in = source(input);
         // (getReadBuffer: DecodeException at the end of the stream, as the
         //  reference's first read throws)
-        ByteBuffer head = in.getReadBuffer();
+        ByteBuffer head = input.getReadBuffer();
         if (!head.hasRemaining()) throw new org.capnproto.DecodeException("premature EOF");
         long bytes = peekMessageBytes(head);
         if (bytes < 0 || bytes < MIN_BYTES) return null;
         long words = bytes / 8;
-        if (in instanceof org.capnproto.ArrayInputStream) {
+        if (input instanceof org.capnproto.ArrayInputStream) {
             // the whole array is the read buffer (ArrayInputStream.java:53-58)
             ByteBuffer[] segs = gpu().readMessage(head, options.traversalLimitInWords, words);
             if (segs == null) throw new org.capnproto.DecodeException("Premature EOF");
             return new org.capnproto.MessageReader(segs, options);
         }
-        return readFrom(sourceFor(input), options, words);
+        if (input instanceof Source) return readFrom((Source) input, options, words);
+        return readFromStream(input, options, words);
     }
 
     /** SerializePacked.tryRead(input, options): Optional.empty() when the
      *  stream ends before a message starts (the documented contract,
      *  SerializePacked.java:31-46); null when the message is below MIN_BYTES
-     *  (the caller then runs the reference path over source(input)). */
+     *  (the caller then runs the reference path over input). */
     public static Optional<org.capnproto.MessageReader> tryRead(org.capnproto.BufferedInputStream input,
                                                                 org.capnproto.ReaderOptions options)
             throws IOException {
-        org.capnproto.BufferedInputStream in = source(input);
         ByteBuffer head;
         try {
-            head = in.getReadBuffer();
+            head = input.getReadBuffer();
         } catch (org.capnproto.DecodeException eof) {
             return Optional.empty();
         }
@@ -179,13 +165,105 @@ public final class GpuDispatch {
         return m == null ? null : Optional.of(m);
     }
 
-    /** GPU read of one message from a Source: a try on the bytes buffered
-     *  so far; while they end inside the message, more are taken -- until
-     *  twice as many as at the last try are buffered, the upstream pauses
-     *  (a short read: waiting longer could wait on a peer that waits on us),
-     *  or the table's bound on the message's packed bytes is reached.  A
-     *  message of M bytes costs O(log M) tries plus one per pause, and the
-     *  buffer grows geometrically. */
+    /** GPU read of one message from a BufferedInputStream, consuming exactly
+     *  its packed bytes: each read buffer is copied (not consumed) behind the
+     *  message's earlier bytes and walked for the message's end (Extent);
+     *  a buffer the message runs past is then taken whole and the next one
+     *  fetched (getReadBuffer refills -- DecodeException at the end of the
+     *  stream, as the reference's read()), the one it ends in is advanced by
+     *  the bytes it used.  One library call per message.  A malformed
+     *  message (a run past its words) goes to the device as far as it was
+     *  walked, which throws the reference's DecodeException. */
+    private static org.capnproto.MessageReader readFromStream(org.capnproto.BufferedInputStream input,
+                                                              org.capnproto.ReaderOptions options,
+                                                              long words) throws IOException {
+        Extent ext = new Extent(words);
+        ByteBuffer carry = PackedGpu.directBuffer(1 << 16);
+        carry.limit(0);
+        for (;;) {
+            ByteBuffer cur = input.getReadBuffer();
+            if (!cur.hasRemaining()) throw new org.capnproto.DecodeException("premature EOF");
+            int base = carry.limit();
+            carry = append(carry, cur);
+            long end = ext.walk(carry);
+            if (end == Extent.MORE) {
+                cur.position(cur.limit());   // (all of it is the message's)
+                continue;
+            }
+            int take = end >= 0 ? (int) end : carry.limit();
+            ByteBuffer msg = carry.duplicate();
+            msg.position(0).limit(take);
+            ByteBuffer[] segs = gpu().readMessage(msg, options.traversalLimitInWords, words);
+            if (segs == null) throw new org.capnproto.DecodeException("premature EOF");
+            cur.position(cur.position() + (msg.position() - base));
+            return new org.capnproto.MessageReader(segs, options);
+        }
+    }
+
+    /** carry + src's remaining bytes (src not consumed), growing by doubling. */
+    private static ByteBuffer append(ByteBuffer carry, ByteBuffer src) {
+        int need = carry.limit() + src.remaining();
+        if (need > carry.capacity()) {
+            int cap = carry.capacity();
+            while (cap < need) cap = Math.multiplyExact(cap, 2);
+            ByteBuffer grown = PackedGpu.directBuffer(cap);
+            ByteBuffer old = carry.duplicate();
+            old.position(0);
+            grown.put(old);
+            carry = grown;
+        }
+        ByteBuffer w = carry.duplicate();
+        w.limit(need).position(carry.limit());
+        w.put(src.duplicate());
+        carry.limit(need).position(0);
+        return carry;
+    }
+
+    /** The packed extent of a message of `words` words, walked record by
+     *  record over bytes that arrive in pieces (PackedInputStream.java:
+     *  92-134's records: a tag, its nonzero bytes, then for 0x00 a zero-run
+     *  count, for 0xFF a count and that many verbatim words).  walk() resumes
+     *  at the first record it could not finish. */
+    static final class Extent {
+        static final long MORE = -1, MALFORMED = -2;
+        private long wordsLeft;
+        private int at;   // the next record's first byte
+
+        Extent(long words) { this.wordsLeft = words; }
+
+        /** The byte just past the message in b (absolute index), MORE when
+         *  b ends first, MALFORMED when a run passes the message's words. */
+        long walk(ByteBuffer b) {
+            final int end = b.limit();
+            while (wordsLeft > 0) {
+                int p = at;
+                if (p >= end) return MORE;
+                int tag = b.get(p) & 0xff;
+                p += 1 + Integer.bitCount(tag);
+                long w = 1;
+                if (tag == 0 || tag == 0xff) {
+                    if (p >= end) return MORE;
+                    int run = b.get(p) & 0xff;
+                    p += 1 + (tag == 0xff ? 8 * run : 0);
+                    w += run;
+                }
+                if (p > end) return MORE;
+                if (w > wordsLeft) return MALFORMED;
+                wordsLeft -= w;
+                at = p;
+            }
+            return at;
+        }
+    }
+
+    /** GPU read of one message from a channel's Source: a try on the bytes
+     *  buffered so far; while they end inside the message, more are taken --
+     *  until twice as many as at the last try are buffered, the upstream
+     *  pauses (a short read: waiting longer could wait on a peer that waits
+     *  on us), or the table's bound on the message's packed bytes is
+     *  reached.  A message of M bytes costs O(log M) tries plus one per
+     *  pause, and the buffer grows geometrically; bytes past the message
+     *  stay in the Source for the channel's next read. */
     private static org.capnproto.MessageReader readFrom(Source s, org.capnproto.ReaderOptions options,
                                                         long words) throws IOException {
         final long bound = 10 * (words + 1) + 16;   // packed bytes of the message, at most
@@ -271,38 +349,20 @@ public final class GpuDispatch {
 
     // ---------------------------------------------------------------- Source
 
-    /** A BufferedInputStream (BufferedInputStream.java:27-38) over a carry
-     *  buffer that an upstream stream or channel refills: what the GPU path
-     *  reads from, and what the reference path reads when bytes were carried.
-     *  Direct memory (passed to JNI zero-copy), grown by doubling. */
+    /** A channel's persistent BufferedInputStream (BufferedInputStream.java:
+     *  27-38): a carry buffer the channel refills, what the GPU path and the
+     *  reference path (readFromUnbuffered) both read.  Direct memory (passed
+     *  to JNI zero-copy), grown by doubling. */
     static final class Source implements org.capnproto.BufferedInputStream {
         // (weak: the map's value must not keep its key alive -- the entry
-        // goes when the caller drops the stream or channel)
-        private final WeakReference<org.capnproto.BufferedInputStream> upstreamRef;   // or
+        // goes when the caller drops the channel)
         private final WeakReference<ReadableByteChannel> channelRef;
-        private final boolean isChannel;
         ByteBuffer buf;   // [position, limit): bytes not yet consumed
 
-        Source(org.capnproto.BufferedInputStream upstream) {
-            this.upstreamRef = new WeakReference<>(upstream);
-            this.channelRef = null;
-            this.isChannel = false;
-            this.buf = PackedGpu.directBuffer(1 << 16);
-            this.buf.limit(0);
-        }
-
         Source(ReadableByteChannel channel) {
-            this.upstreamRef = null;
             this.channelRef = new WeakReference<>(channel);
-            this.isChannel = true;
             this.buf = PackedGpu.directBuffer(1 << 16);
             this.buf.limit(0);
-        }
-
-        private org.capnproto.BufferedInputStream upstream() throws IOException {
-            org.capnproto.BufferedInputStream u = upstreamRef.get();
-            if (u == null) throw new IOException("stream closed");
-            return u;
         }
 
         private ReadableByteChannel channel() throws IOException {
@@ -330,37 +390,24 @@ public final class GpuDispatch {
             buf = grown;
         }
 
-        /** One read from upstream appended to the buffer (blocking for >= 1
+        /** One read from the channel appended to the buffer (blocking for >= 1
          *  byte).  DecodeException("premature EOF") at the end of the stream
          *  (BufferedInputStreamWrapper.java:98-108).  True if the read filled
          *  all the room it was offered (more may be ready). */
         boolean fill() throws IOException {
-            if (isChannel) {
-                ReadableByteChannel channel = channel();
-                reserve(8192);
-                int lim = buf.limit();
-                ByteBuffer w = buf.duplicate();
-                w.position(lim).limit(buf.capacity());
-                int offered = w.remaining();
-                int n = 0;
-                while (n == 0) {
-                    n = channel.read(w);
-                    if (n < 0) throw new org.capnproto.DecodeException("premature EOF");
-                }
-                buf.limit(lim + n);
-                return n == offered;
-            }
-            ByteBuffer src = upstream().getReadBuffer();   // DecodeException at EOF
-            int n = src.remaining();
-            if (n == 0) throw new org.capnproto.DecodeException("premature EOF");
-            reserve(n);
+            ReadableByteChannel channel = channel();
+            reserve(8192);
             int lim = buf.limit();
             ByteBuffer w = buf.duplicate();
-            w.position(lim).limit(lim + n);
-            boolean full = n == src.capacity();
-            w.put(src);   // (src.position reaches its limit: the bytes are taken)
+            w.position(lim).limit(buf.capacity());
+            int offered = w.remaining();
+            int n = 0;
+            while (n == 0) {
+                n = channel.read(w);
+                if (n < 0) throw new org.capnproto.DecodeException("premature EOF");
+            }
             buf.limit(lim + n);
-            return full;
+            return n == offered;
         }
 
         @Override
@@ -386,15 +433,13 @@ public final class GpuDispatch {
 
         @Override
         public boolean isOpen() {
-            Object o = isChannel ? channelRef.get() : upstreamRef.get();
-            return o != null && (isChannel ? ((ReadableByteChannel) o).isOpen()
-                                           : ((org.capnproto.BufferedInputStream) o).isOpen());
+            ReadableByteChannel c = channelRef.get();
+            return c != null && c.isOpen();
         }
 
         @Override
         public void close() throws IOException {
-            if (isChannel) channel().close();
-            else upstream().close();
+            channel().close();
         }
     }
 }

@@ -298,6 +298,9 @@ public final class PackedGpu implements AutoCloseable {
             int st = nativeReadMessage(handle, pk, pk.position(), pk.limit(), traversalLimitInWords, out, info);
             if (st == CPK_ENOMEM && info[3] > cap) {   // (the table says how many words)
                 cap = info[3];
+                // a heap buffer's copy reaches only as far as the old hint's
+                // words can: copy it again for the table's count
+                if (pk != packed) pk = asDirect(packed, 10 * (cap + 257) + 16);
                 continue;
             }
             if (st == CPK_ETRUNC) return null;

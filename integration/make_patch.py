@@ -60,7 +60,6 @@ def main():
                  f"        if ({G}.enabled()) {{\n"
                  f"            {ret} m = {G}.{kind}(input, options);\n"
                  f"            if (m != null) return m;  // (null: below {G}.MIN_BYTES, the codec below)\n"
-                 f"            input = {G}.source(input);  // (bytes a GPU read carried past its message first)\n"
                  f"        }}\n")
         for tail, kind in (("        return Serialize.tryRead(packedInput, options);\n", "tryRead"),
                            ("        return Serialize.read(packedInput, options);\n", "read")):

@@ -143,10 +143,10 @@ def test_sparse_messages_multi_round(ctx, oracle):
 @pytest.mark.parametrize("config,segments", [(2, 4096), (3, 512)])
 def test_bench_two_ranks_same_device(config, segments):
     """bench.py's real GPU rank path at N = 2 (config 5 readiness) on a
-    one-GPU box: both ranks on cuda:0 with a gloo group (--same-device; RCCL
-    refuses two ranks on one GPU).  Shard planning, per-rank generation, the
-    barrier-bracketed timing and the max/sum reduction are the code the
-    8-GPU run takes; both shards must round-trip bit-exact and rank 0's
+    one-GPU box: both ranks on cuda:0 (--same-device).  Every mode uses the
+    same gloo group, so shard planning, per-rank generation, the
+    barrier-bracketed timing and the max/sum reduction are exactly the code
+    the 8-GPU run takes but for torch.cuda.set_device; both shards must round-trip bit-exact and rank 0's
     oracle sample must equal the device bytes."""
     import json
     import os

@@ -371,7 +371,9 @@ def test_wrong_size_hint_is_reported(ctx, oracle):
     """A piece larger than max_seg_words: no fault, reported by take_error."""
     import torch
     import capnp_packed as cp
-    for sizes, hint in (([9000, 10], 100), ([30000, 10], 9000)):
+    # (the last case: many pieces far over a hint above one chunk -- the
+    # unit table is sized from the hint, so no slack may hide an overrun)
+    for sizes, hint in (([9000, 10], 100), ([30000, 10], 9000), ([40000] * 1000, 9000)):
         swo = _swo(sizes)
         d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
         d_in = torch.ones(int(swo[-1]), dtype=torch.int64, device="cuda")

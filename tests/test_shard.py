@@ -1,5 +1,5 @@
 """N>1 path without GPUs: shard planning and the timing reduction over gloo
-(world size 2), the same calls bench.py makes over RCCL."""
+(world size 2), the same calls and backend bench.py uses on GPUs."""
 import os
 import socket
 
