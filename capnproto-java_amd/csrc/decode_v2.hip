@@ -24,45 +24,29 @@
 // its kD2NI-th record; the next window starts there.
 
 constexpr int kD2Threads = 256;  // 4 independent waves
-#ifndef CPK_D2_WPE
-#define CPK_D2_WPE 5  // workgroups per CU the register budget is sized for (LDS allows 5)
-#endif
-#ifndef CPK_D2_CHUNK
-#define CPK_D2_CHUNK 48
-#endif
-constexpr uint32_t kD2Chunk = CPK_D2_CHUNK;
+// workgroups per CU the register budget is sized for (LDS allows 5)
+constexpr int kD2Wpe = 5;
+constexpr uint32_t kD2Chunk = 48;
 constexpr uint32_t kD2Win = 64 * kD2Chunk;                           // packed bytes per window
 constexpr uint32_t kD2WinBuf = (kD2Win + 15 + 32 + 16 + 15) & ~15u;  // + pad, look-ahead, slack
-#ifndef CPK_D2_NI
-#define CPK_D2_NI 1024
-#endif
-constexpr uint32_t kD2NI = CPK_D2_NI;  // records indexed per window
-#ifndef CPK_D2_ROUND
-#define CPK_D2_ROUND 2048
-#endif
-constexpr uint32_t kD2Round = CPK_D2_ROUND;  // output words per expansion round
-#ifndef CPK_D2_UNROLL
-#define CPK_D2_UNROLL 4
-#endif
-constexpr int kD2Unroll = CPK_D2_UNROLL;  // 64-word groups expanded together
+constexpr uint32_t kD2NI = 1024;  // records indexed per window
+constexpr uint32_t kD2Round = 2048;  // output words per expansion round
+constexpr int kD2Unroll = 4;  // 64-word groups expanded together
 typedef std::conditional<(kD2Chunk <= 32), uint32_t, uint64_t>::type D2Vis;
 static_assert(kD2Chunk <= 64, "visited mask bits");
 constexpr uint32_t kD2Info = kD2NI * 4;
 static_assert(kD2Info >= 64 * sizeof(D2Vis) + 8, "visited masks live over the index");
-#ifndef CPK_D2_BYTEMAP
-#define CPK_D2_BYTEMAP 0
-#endif
 // record starts of a round: a byte per output word (plain byte stores, one
 // per record: consecutive records never contend for one LDS address as bits
 // OR-ed into a shared word would), or a bit per word with atomics
-constexpr uint32_t kD2Bits = CPK_D2_BYTEMAP ? kD2Round : kD2Round / 8;
+constexpr uint32_t kD2Bits = 0 ? kD2Round : kD2Round / 8;
 constexpr uint32_t kD2WaveLds = kD2WinBuf + kD2Info + kD2Bits;
 constexpr uint32_t kD2Lds = 2048 + 4 * kD2WaveLds;
 constexpr int kD2LinesPerLane = (int)((kD2Win + 47 + 15) / 16 + 63) / 64;
 static_assert(kD2Win <= 4095, "record positions are 12-bit");
 
 template <bool kStream>
-__global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
+__global__ __launch_bounds__(kD2Threads, kD2Wpe) void decode2_kernel(
     const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
     int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail, DecStreams sd) {
@@ -141,10 +125,8 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
     int ow = 0;      // output words produced
     if (W == 0) st = (P == 0 || kStream) ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
     while (W != 0) {
-#if CPK_DEC_UNI
       e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);  // (wave-uniform: SGPRs, scalar branches)
       ow = __builtin_amdgcn_readfirstlane(ow);
-#endif
       if (e >= P) {
         if (ow < W) st = CPK_ETRUNC;  // ArrayInputStream EOF -> DecodeException
         break;
@@ -165,11 +147,7 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
 #pragma unroll
         for (int j = 0; j < kD2LinesPerLane; ++j) {
           const uint32_t L = lane + 64 * j;
-#if CPK_DEC_NTLD
-          l[j] = L < lines ? ld_stream16(gsrc + L) : make_uint4(0u, 0u, 0u, 0u);
-#else
           l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
-#endif
         }
 #pragma unroll
         for (int j = 0; j < kD2LinesPerLane; ++j) {
@@ -352,10 +330,7 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
           const uint32_t i = ib + (uint32_t)lane;
           const uint32_t oi = i < (uint32_t)NRe ? (info[i] >> 12) : 0xffffffffu;
           const bool in = oi < rb + kD2Round;
-          if (in) {
-            if (CPK_D2_BYTEMAP) reinterpret_cast<uint8_t *>(bits)[oi - rb] = 1;
-            else atomicOr(&bits[(oi - rb) >> 5], 1u << ((oi - rb) & 31));
-          }
+          if (in) atomicOr(&bits[(oi - rb) >> 5], 1u << ((oi - rb) & 31));
           const uint64_t outm = __ballot(!in);
           if (outm) {
             ib += (uint32_t)__builtin_ctzll(outm);
@@ -372,12 +347,8 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
 #pragma unroll
           for (int u = 0; u < kD2Unroll; ++u) {
             const uint32_t g0 = gb + 64 * u;
-            if (CPK_D2_BYTEMAP) {
-              bm[u] = __ballot(g0 < re && reinterpret_cast<const uint8_t *>(bits)[g0 - rb + (uint32_t)lane] != 0);
-            } else {
-              const uint32_t gi = (g0 - rb) >> 5;  // (even; past the round: zero bits)
-              bm[u] = g0 < rb + kD2Round ? ((uint64_t)bits[gi] | ((uint64_t)bits[gi + 1] << 32)) : 0ull;
-            }
+            const uint32_t gi = (g0 - rb) >> 5;  // (even; past the round: zero bits)
+            bm[u] = g0 < rb + kD2Round ? ((uint64_t)bits[gi] | ((uint64_t)bits[gi + 1] << 32)) : 0ull;
           }
           const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1);
 #pragma unroll
@@ -397,11 +368,7 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
             const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
             const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
             const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
-#if CPK_DEC_NT
             if (wv < re) __builtin_nontemporal_store((uint64_t)x0 | ((uint64_t)x1 << 32), &dst_w[wv]);
-#else
-            if (wv < re) dst_w[wv] = (uint64_t)x0 | ((uint64_t)x1 << 32);
-#endif
           }
         }
         // the record covering the next round's first word
@@ -410,10 +377,8 @@ __global__ __launch_bounds__(kD2Threads, CPK_D2_WPE) void decode2_kernel(
         wave_lds_order();  // bits / info reused
       }
       };
-#if CPK_DEC_ALLIN
       if (eff_next + 12 <= lend) expand(std::true_type{});
       else
-#endif
         expand(std::false_type{});
       WPH(6)
       if (ow + (int)Teff >= W && fin) {  // the piece is full: next piece starts at fin

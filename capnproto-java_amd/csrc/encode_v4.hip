@@ -28,17 +28,7 @@ constexpr uint32_t kE4RingDw = kE4RingBytes / 4;
 
 // nonzero-byte tag of a word (PackedOutputStream.java:64-117): bit i set iff
 // byte i != 0.  SWAR: bit 7 of every byte of t = byte != 0, gathered by shifts.
-#ifndef CPK_E4_NTST
-#define CPK_E4_NTST 0  // nontemporal stores of the emit pass's packed lines
-#endif
-#ifndef CPK_E4_NTLD2
-#define CPK_E4_NTLD2 0  // nontemporal loads in the emit pass (the words' second and last read)
-#endif
-#if CPK_E4_NTLD2
-#define E4_LD2(p) ld_stream(p)
-#else
 #define E4_LD2(p) (*(p))
-#endif
 
 __device__ __forceinline__ uint32_t e4_tag(uint64_t v) {
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
@@ -76,25 +66,13 @@ __device__ __forceinline__ void e4_flush(uint8_t *out, uint32_t *ring, uint64_t 
       uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kE4RingLines - 1));
       const uint4 val = *rl;
       *rl = make_uint4(0u, 0u, 0u, 0u);
-#if CPK_E4_NTST
-      st_stream(val, out + L * 16);
-#else
       *reinterpret_cast<uint4 *>(out + L * 16) = val;
-#endif
     }
   }
   fl = upto;
 }
 
-#ifndef CPK_E4_WPE
-#define CPK_E4_WPE 8
-#endif
-#ifndef CPK_E4_MASKROLES
-#define CPK_E4_MASKROLES 0  // size pass: roles as scalar mask algebra per step (sp_roles), not per-lane selects (measured +12 %)
-#endif
-#ifndef CPK_E4_PF
-#define CPK_E4_PF 4  // steps of loads in flight ahead of the size pass's classification
-#endif
+constexpr int kE4Wpe = 8;
 
 // Run state entering a step (wave-uniform): g 0 zero run, 1 D/L stretch,
 // 2 none (piece start or after an M word); len: words of the run before the
@@ -227,7 +205,7 @@ __device__ __forceinline__ uint32_t e4_next_piece(uint32_t *ticket, int &xq, int
 }
 
 // ---- pass 1: packed size of every piece --------------------------------------
-__global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
+__global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     uint64_t *__restrict__ sizes, uint32_t *ticket, uint64_t hint, uint32_t *err,
     uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip) {
@@ -254,16 +232,13 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     E4St st = {2, 0, 0};
     int gl = 2;
     uint32_t acc = 0;
-#if CPK_E4_MASKROLES
-    SpSt mst = {0u, 0u, 0u};  // (a fresh piece: no run enters it)
-    uint64_t sb = 0;          // wave-uniform bytes beyond the nonzero bytes
-#endif
     // (32-bit step / word indices: a piece is at most 2^31 words, Serialize
     // limits segments to 2^29 - 1, Serialize.java:45-53)
     const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;
-    // software pipeline: the next CPK_E4_PF steps' loads are in flight while
+    // software pipeline: the next kE4Pf steps' loads are in flight while
     // these are classified
-    constexpr int PF = CPK_E4_PF;
+    // steps of loads in flight ahead of the size pass's classification
+constexpr int PF = 4;
     uint64_t v[PF], vn[PF];
     // loads clamped to the piece's last word, not predicated (no exec-mask
     // branches around them); words past the end are masked by `valid`
@@ -279,37 +254,10 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
         const uint32_t k = ((s0 + j) << 6) + lane;
         const bool valid = k < W32;
         if (s0 + j < nsteps) {
-#if CPK_E4_MASKROLES
-          // per word only the tag, its popcount and three ballots; the
-          // roles of the step's words follow from the masks and the state
-          // carried in SGPRs (sp_roles, as the single pass's sequential
-          // form), its bytes from popcounts: tag + nonzero bytes of every
-          // word but zero-run members, a count after each head, 8 verbatim
-          // bytes per literal-run member (PackedOutputStream.java:64-193)
-          const uint32_t m = valid ? e4_tag(v[j]) : 0u;
-          const uint32_t pc = (uint32_t)__builtin_popcount(m);
-          acc += pc;
-          const uint64_t Z = __ballot(valid && m == 0), DL = __ballot(pc >= 7), D = __ballot(m == 0xffu);
-          const uint32_t vr = W32 - ((s0 + j) << 6);
-          const uint64_t Vm = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
-          // the emit pass's run boundaries (as e4_classify's BV): past the
-          // end, every M word, and a Z / D-or-L word whose predecessor is
-          // of another group (gl: the group of the word before the step)
-          const uint64_t Zp = (Z << 1) | (gl == 0 ? 1ull : 0ull), DLp = (DL << 1) | (gl == 1 ? 1ull : 0ull);
-          const uint64_t BV = ~Vm | (Vm & ~Z & ~DL) | (Z & ~Zp) | (DL & ~DLp);
-          gl = (Z >> 63) ? 0 : ((DL >> 63) ? 1 : 2);
-          uint64_t Zh, Mem;
-          sp_roles(Z, DL, D, mst, Zh, Mem);
-          const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~Vm;
-          sb += (uint64_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
-                           __builtin_popcountll(HC));
-          x = lane == j ? BV : x;
-#else
           const E4Cls c = e4_classify(v[j], valid, gl);
           const E4Role r = e4_roles(e4_tag(v[j]), valid, c, st, lane, lem);
           acc += r.nb;
           x = lane == j ? c.BV : x;
-#endif
         }
       }
       // the group's boundary rows for the emit pass: lanes 0..PF-1, one store
@@ -320,11 +268,7 @@ __global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_size_kernel(
     // wave sum in two 16-bit halves (a piece's packed size may pass 2^31)
     const uint32_t thi = (uint32_t)wave_incl_add((int)(acc >> 16));
     const uint32_t tlo = (uint32_t)wave_incl_add((int)(acc & 0xffffu));
-#if CPK_E4_MASKROLES
-    if (lane == 63) sizes[seg] = ((uint64_t)thi << 16) + tlo + sb;
-#else
     if (lane == 63) sizes[seg] = ((uint64_t)thi << 16) + tlo;
-#endif
   }
 }
 
@@ -493,7 +437,7 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
   }
 }
 
-__global__ __launch_bounds__(kE4Threads, CPK_E4_WPE) void e4_emit_kernel(
+__global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint32_t *ticket,
     const uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip) {

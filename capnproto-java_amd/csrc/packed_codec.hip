@@ -308,33 +308,23 @@ __device__ uint64_t lb_resolve_wide(uint64_t *status, uint32_t tile, uint64_t ag
 //      gather-expand the blocks (PackedInputStream.java:82-134 per word).
 // No barriers: up to 28 pieces in flight per CU.
 constexpr int kDecThreads = 256;               // 4 independent waves
-#ifndef CPK_DEC_WPE
-#define CPK_DEC_WPE 7  // workgroups per CU the register budget is sized for (= the LDS limit:
-                       // 72 VGPRs; at 8 the stream form spilled, messages decode +10 %)
-#endif
-#ifndef CPK_DEC_CHUNK
-#define CPK_DEC_CHUNK 56
-#endif
+// workgroups per CU the register budget is sized for (= the LDS limit:
+// 72 VGPRs; at 8 the stream form spilled, messages decode +10 %)
+constexpr int kDecWpe = 7;
 // Lane chunks C of 56 bytes (3.5 KiB windows, 7 workgroups per CU by LDS):
 // measured against 40 / 48 / 60 / 64 at 131,072 pieces with the max-map
 // block map, 56 is fastest on configs 2-4 (against 48: 4.29 -> 4.13 ms,
 // 6.80 -> 6.51, 2.84 -> 2.80)
-constexpr uint32_t kDecChunk = CPK_DEC_CHUNK;
+constexpr uint32_t kDecChunk = 56;
 constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per window
-#ifndef CPK_DEC_LOOK
-#define CPK_DEC_LOOK 240  // bytes loaded past the window (a literal run reaching past them is read from memory;
-                         // 240: config 3 decode -4.5 % against 32, config 2 neutral; 368 costs occupancy)
-#endif
-constexpr uint32_t kDecLook = CPK_DEC_LOOK;
+// bytes loaded past the window (a literal run reaching past them is read from memory;
+// 240: config 3 decode -4.5 % against 32, config 2 neutral; 368 costs occupancy)
+constexpr uint32_t kDecLook = 240;
 constexpr uint32_t kWinBuf = (kWin + 15 + kDecLook + 16 + 15) & ~15u;  // + pad, look-ahead, slack
-#ifndef CPK_DEC_ROUND
-#define CPK_DEC_ROUND 1280  // (8 workgroups per CU with 48-byte chunks; larger rounds cost occupancy)
-#endif
-constexpr int kRound = CPK_DEC_ROUND;  // output words expanded per round
-#ifndef CPK_DEC_BLK
-#define CPK_DEC_BLK 4  // (4: 64 lanes cover a window's blocks in fewer, fuller passes; measured faster than 8)
-#endif
-constexpr int kBlk = CPK_DEC_BLK;  // output words per expansion block
+// (8 workgroups per CU with 48-byte chunks; larger rounds cost occupancy)
+constexpr int kRound = 1280;  // output words expanded per round
+// (4: 64 lanes cover a window's blocks in fewer, fuller passes; measured faster than 8)
+constexpr int kBlk = 4;  // output words per expansion block
 // a lane's visited positions: one bit per chunk byte
 typedef std::conditional<(kDecChunk <= 32), uint32_t, uint64_t>::type VisMask;
 static_assert(kDecChunk <= 64, "visited mask bits");
@@ -342,49 +332,14 @@ static_assert(kDecChunk <= 64, "visited mask bits");
 constexpr uint32_t kDecWaveLds = kWinBuf + (4 * (kRound / kBlk) > 64 * sizeof(VisMask)
                                                 ? 4 * (kRound / kBlk)
                                                 : 64 * sizeof(VisMask));
-#ifndef CPK_DEC_MAXMAP
-#define CPK_DEC_MAXMAP 1
-#endif
-#ifndef CPK_DEC_LEANMAP
-#define CPK_DEC_LEANMAP 1  // a check-free block-map walk for windows no record of which can fail
-#endif
-static_assert(!CPK_DEC_LEANMAP || CPK_DEC_MAXMAP, "CPK_DEC_LEANMAP needs CPK_DEC_MAXMAP");
-#ifndef CPK_DEC_TRACKCHK
-#define CPK_DEC_TRACKCHK 1  // windows near the piece's end check only the two records that can fail
-#endif
-static_assert(!CPK_DEC_TRACKCHK || CPK_DEC_LEANMAP, "CPK_DEC_TRACKCHK needs CPK_DEC_LEANMAP");
-// CPK_DEC_MAXMAP: a record marks only the block whose span ends at or after
+// The block map: a record marks only the block whose span ends at or after
 // its first word (ds_max of an entry ordered by output position), and a
 // prefix max over the blocks hands every block the last record starting at
 // or before its first word: one LDS op per record, no per-block loop
 constexpr int kMapPer = kRound / kBlk / 64;  // map entries per lane in the fill
-static_assert(!CPK_DEC_MAXMAP || (kRound / kBlk == 64 * kMapPer && kWin <= 4096 && kRound + 256 < (1 << 19)),
+static_assert((kRound / kBlk == 64 * kMapPer && kWin <= 4096 && kRound + 256 < (1 << 19)),
               "max-map entry: 12-bit window position, 19-bit output position");
-#ifndef CPK_DEC_UNI
-#define CPK_DEC_UNI 1
-#endif
-#ifndef CPK_DEC_MAP0
-#define CPK_DEC_MAP0 1  // a check-free round-0 map walk (no past-the-round-start test)
-#endif
-#ifndef CPK_DEC_ALLIN
-#define CPK_DEC_ALLIN 1  // an expansion without bound checks for windows whose records are all loaded
-#endif
-#ifndef CPK_DEC_NTLD
-#define CPK_DEC_NTLD 0  // nontemporal loads of the window lines
-#endif
-#ifndef CPK_DEC_NT
-#define CPK_DEC_NT 1  // nontemporal stores of the expanded words (config 2 decode -9 %, config 4 -5 %)
-#endif
-#ifndef CPK_DEC_ABL
-#define CPK_DEC_ABL 0  // ablations for timing only (wrong output): 1 no word stores, 2 no expansion, 4 no block-map walk
-#endif
-#ifndef CPK_DEC_HOIST_CNT
-#define CPK_DEC_HOIST_CNT 0
-#endif
-#ifndef CPK_DEC_CHK_REACH
-#define CPK_DEC_CHK_REACH (kWin + 2064)
-#endif
-constexpr uint32_t kDecChkReach = CPK_DEC_CHK_REACH;
+constexpr uint32_t kDecChkReach = (kWin + 2064);
 static_assert(kDecChkReach >= kWin + 2050, "a window's last record must fall inside the checked reach");
 constexpr int kWinLinesPerLane = (int)((kWin + 15 + kDecLook + 15) / 16 + 63) / 64;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;  // 21,760 at 56-byte chunks
@@ -466,7 +421,7 @@ struct DecStreams {
   const uint32_t *skip;  // (batch form: nonzero = the other decoder took the batch)
 };
 template <bool kStream>
-__global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
+__global__ __launch_bounds__(kDecThreads, kDecWpe) void decode_kernel(
     const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
     int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail, DecStreams sd) {
@@ -544,13 +499,11 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
     int ow = 0;      // output words produced
     if (W == 0) st = (P == 0 || kStream) ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
     while (W != 0) {
-#if CPK_DEC_UNI
       // the window's start and the words so far are wave-uniform: say so
       // (the loop's exits made the compiler keep them in VGPRs and run the
       // window's uniform branches under exec masks)
       e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
       ow = __builtin_amdgcn_readfirstlane(ow);
-#endif
       if (e >= P) {
         if (ow < W) st = CPK_ETRUNC;  // ArrayInputStream EOF -> DecodeException
         break;
@@ -571,11 +524,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
 #pragma unroll
         for (int j = 0; j < kWinLinesPerLane; ++j) {
           const uint32_t L = lane + 64 * j;
-#if CPK_DEC_NTLD
-          l[j] = L < lines ? ld_stream16(gsrc + L) : make_uint4(0u, 0u, 0u, 0u);
-#else
           l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
-#endif
         }
 #pragma unroll
         for (int j = 0; j < kWinLinesPerLane; ++j) {
@@ -679,21 +628,17 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
       const bool chk = (ow + T >= W) || (P - e < kDecChkReach);
       for (int rb = 0; rb < T; rb += kRound) {
         int err = 0x7fffffff;
-#if CPK_DEC_MAXMAP
         wave_lds_order();  // (the visited masks / last round's map reads are done)
 #pragma unroll
         for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = 0u;
         wave_lds_order();
-#endif
         // after the first round only the lanes whose output meets this round
-#if CPK_DEC_LEANMAP
         if (!(chk && rb == 0)) {
           // no record here can fail or fill the piece: the map alone
-#if CPK_DEC_MAP0
           if (rb == 0) {
             // round 0 (usually the window's only one): every record's output
             // is at or past the round's start, so it always marks a block
-            if (on && !(CPK_DEC_ABL & 4)) {
+            if (on) {
               uint32_t rel = (uint32_t)o0;
               for (uint32_t q = entry; q < S && rel <= (uint32_t)(kRound - kBlk);) {
                 const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
@@ -704,7 +649,6 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
               }
             }
           } else
-#endif
           if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
             int rel = o0 - rb;  // round-relative output of the record (> -256 when live)
             // (records past the round's last block start mark nothing, nor
@@ -720,8 +664,6 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
             }
           }
         } else
-#endif
-#if CPK_DEC_TRACKCHK
         {
           // round 0 of a window near the piece's end.  Only two records can
           // fail or fill the piece: the one whose words reach word W (when the
@@ -778,50 +720,6 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
             if (oo + nw == W) fin = q + adv;
           }
         }
-        if (false)
-#endif
-        if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
-          int o = o0;
-          for (uint32_t q = entry; q < S;) {
-            const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
-            const uint32_t ntag = 1 + __builtin_popcount(tag);
-            const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
-            const int nw = 1 + (int)((zm & c1) + (fm & c9));
-            const uint32_t adv = ntag + (zm & 1u) + (fm & (8u * c9 + 1u));
-            const int oo = ow + o;
-            if (chk && rb == 0 && oo < W && err == 0x7fffffff) {
-              // PackedInputStream.java:53-138: truncated tag bytes / count /
-              // literal run -> EOF DecodeException; run past the piece ->
-              // DecodeException / BufferOverflowException
-              int code = 0;
-              if (q + ntag > P) code = 2;
-              else if (tag == 0 || tag == 0xffu) {
-                if (q + (tag ? 10u : 2u) > P) code = 2;
-                else if (oo + nw > W) code = 3;
-                else if (q + adv > P) code = 2;
-              }
-              if (!kStream && !code && oo + nw == W && q + adv < P) code = 4;
-              if (code) err = (int)(((q - e) << 3) | (uint32_t)code);  // window-relative
-              if (oo + nw == W) fin = q + adv;
-            }
-#if CPK_DEC_MAXMAP
-            {
-              const int rel = o - rb;  // round-relative output of the record (> -256 when live)
-              const int idx = (max(rel, 0) + kBlk - 1) / kBlk;
-              if (rel + nw > 0 && idx < kRound / kBlk)
-                atomicMax(&blk[idx], ((uint32_t)(rel + 256) << 12) | (q - e));
-            }
-#else
-            // blocks of this round whose first word this record covers
-            const int lo = max(o, rb), hi = min(o + nw, rb + kRound);
-            // window-relative record position (< 2 KiB) | offset in the run
-            for (int bb = (lo + kBlk - 1) & ~(kBlk - 1); bb < hi; bb += kBlk)
-              blk[(bb - rb) / kBlk] = (q - e) | ((uint32_t)(bb - o) << 16);
-#endif
-            o += nw;
-            q += adv;
-          }
-        }
         if (rb == 0) {
           err = __builtin_amdgcn_readfirstlane(wave_min(err));
           if (err != 0x7fffffff) {
@@ -832,7 +730,6 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
           fin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u(fin));
         }
         wave_lds_order();
-#if CPK_DEC_MAXMAP
         {
           // prefix max: lane l holds blocks [kMapPer * l, kMapPer * (l + 1))
           uint32_t m[kMapPer];
@@ -847,7 +744,6 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
           for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = max(m[i], pre);
         }
         wave_lds_order();
-#endif
         WPH(5)
         const int nb = (min(min(kRound, T - rb), W - ow - rb) + kBlk - 1) / kBlk;
         // two copies of the expansion: one for windows whose records all lie
@@ -857,13 +753,8 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
         constexpr bool kAllIn = decltype(allin)::value;
         for (int b = lane; b < nb; b += 64) {
           const uint32_t v = blk[b];
-#if CPK_DEC_MAXMAP
           uint32_t q = e + (v & 0xfffu);
           int ofs = kBlk * b + 256 - (int)(v >> 12);
-#else
-          uint32_t q = e + (v & 0xffffu);
-          int ofs = (int)(v >> 16);
-#endif
           const int wbase = ow + rb + kBlk * b;  // piece word of the block's first word
           const int wleft = ow + T - wbase - 1;   // words of the window after the block's first
           uint64_t words[kBlk];
@@ -873,11 +764,6 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
             // run (tag word, then the counted words), or a tagged word
             // (the count bytes are read with the tag: one LDS round trip)
             uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
-#if CPK_DEC_HOIST_CNT
-            // the count bytes with the tag (one LDS round trip), not sunk
-            // into the zero / 0xFF branches
-            asm volatile("" : "+v"(tag), "+v"(c1), "+v"(c9));
-#endif
             uint64_t x;
             int nw;
             uint32_t adv;
@@ -917,13 +803,7 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
               v4.y = (uint32_t)(words[i] >> 32);
               v4.z = (uint32_t)words[i + 1];
               v4.w = (uint32_t)(words[i + 1] >> 32);
-#if CPK_DEC_ABL & 1
-              asm volatile("" ::"v"(v4.x), "v"(v4.y), "v"(v4.z), "v"(v4.w));
-#elif CPK_DEC_NT
               st_stream(v4, d + i);
-#else
-              *reinterpret_cast<uint4 *>(d + i) = v4;
-#endif
             }
           } else {
 #pragma unroll
@@ -932,13 +812,8 @@ __global__ __launch_bounds__(kDecThreads, CPK_DEC_WPE) void decode_kernel(
           }
         }
         };
-#if CPK_DEC_ABL & 2
-        if (false)
-#endif
-#if CPK_DEC_ALLIN
         if (enext + 12 <= lend) expand(std::true_type{});
         else
-#endif
           expand(std::false_type{});
         wave_lds_order();  // blk reused by the next round
         WPH(6)

@@ -3,7 +3,7 @@
 // and the run state entering it (SpSt, sp_roles), and the lane helpers the
 // single pass uses with them (readfirstlane / readlane / writelane pairs,
 // v_ffbl, per-lane selects on an SGPR mask).  Included by encode_v4.hip
-// (its size pass's CPK_E4_MASKROLES form) and, for the single pass's sparse
+// (in namespace cpk, for the single pass) and, for the single pass's sparse
 // form (a second namespace), again by encode_sp.hip.
 
 struct SpSt {

@@ -543,10 +543,7 @@ __global__ __launch_bounds__(64) void ss_bound_kernel(const uint8_t *__restrict_
 // the blocks, kSsSub at a time, as batch pieces, clamped to the last piece's
 // end (a few large pieces keep the batch decoder's waves busy; one per block
 // would spend them on per-piece setup)
-#ifndef CPK_SS_SUB
-#define CPK_SS_SUB 32
-#endif
-constexpr uint32_t kSsSub = CPK_SS_SUB;
+constexpr uint32_t kSsSub = 32;
 __global__ __launch_bounds__(256) void ss_sub_kernel(const uint64_t *__restrict__ swo, uint32_t n, uint64_t nbmax,
                                                      const uint64_t *__restrict__ in_off, SsBufs B) {
   const uint64_t R = B.lim[0];
