@@ -178,6 +178,41 @@ int pipe_get(cpk_ctx ctx, uint64_t in_bytes, uint64_t out_bytes, uint64_t meta, 
   return CPK_OK;
 }
 
+// Small batches (<= cpk::kSpSmallWords words, pieces and tables): ONE
+// kernel launch (cpk::sp_small_kernel, one workgroup) reads the words from
+// the pinned slot and writes the packed bytes and offsets into pinned memory
+// in place, then one sync -- no DMA, no second kernel, no second sync.
+// lay(pin_words, desc) puts the pieces' words into the slot and their
+// (first word, words) pairs, in output order, into desc.
+template <class Lay>
+int small_encode(cpk_ctx ctx, uint64_t np, uint64_t words, Lay lay, void *h_out, uint64_t h_out_cap,
+                 uint64_t *h_out_off, uint64_t off_base) {
+  HostPipe *p = nullptr;
+  const uint64_t ocap = 9 * words + np + 16;
+  // meta: desc [2 np] | out_off [np + 1]
+  int rc = pipe_get(ctx, 8 * words + 64, ocap + 64, 3 * np + 1, &p, 1);
+  if (rc) return rc;
+  HostSlot &s = p->slot[0];
+  uint64_t *desc = s.pin_meta, *off = desc + 2 * np;
+  lay((uint64_t *)s.pin_in, desc);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void *)cpk::sp_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)cpk::kSp3Lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(cpk::sp_small_kernel, dim3(1), dim3(cpk::kSpThreads), cpk::kSp3Lds, p->sk,
+                     (const uint64_t *)s.pin_in, (const uint64_t *)desc, (uint32_t)np, (uint8_t *)s.pin_out, off,
+                     ocap, ctx->tickets + cpk::kTkErr);
+  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p->sk) != hipSuccess) return CPK_EDEVICE;
+  const uint64_t P = off[np];
+  if (P > ocap) return CPK_EDEVICE;
+  if (P > h_out_cap) return CPK_ENOMEM;
+  memcpy(h_out, s.pin_out, P);
+  for (uint64_t j = 0; j <= np; ++j) h_out_off[j] = off_base + off[j];
+  return CPK_OK;
+}
+
 struct HostChunk {
   uint32_t i0, i1;       // pieces [i0, i1)
   uint64_t in0, in_len;  // input bytes (encode: words * 8; decode: packed range)
@@ -275,6 +310,19 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
   for (uint32_t i = 0; i < n; ++i)
     if (h_swo[i + 1] < h_swo[i]) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
+  if (h_swo[n] - h_swo[0] <= cpk::kSpSmallWords && n <= 4096 && !getenv("CPK_NO_SMALL")) {
+    const HostChunk all{0, n, 0, 8 * (h_swo[n] - h_swo[0]), 0, 0};
+    return small_encode(
+        ctx, n, h_swo[n] - h_swo[0],
+        [&](uint64_t *pin, uint64_t *desc) {
+          copy_in((uint8_t *)pin, all);
+          for (uint32_t i = 0; i < n; ++i) {
+            desc[2 * i] = h_swo[i] - h_swo[0];
+            desc[2 * i + 1] = h_swo[i + 1] - h_swo[i];
+          }
+        },
+        h_out, h_out_cap, h_out_off, 0);
+  }
   const std::vector<HostChunk> cs = host_chunks(h_swo, nullptr, n, host_chunk_bytes());
   uint64_t mi = 0, mo = 0, mm = 0;
   for (const HostChunk &c : cs) {
@@ -593,6 +641,43 @@ int encode_messages_host_impl(cpk_ctx ctx, Fill fill, const uint64_t *h_swo, uin
     return CPK_OK;
   }
   DeviceGuard g(ctx->device);
+  {
+    // a small batch: tables (Serialize.java:256-267, laid out after the
+    // segments) and segments, in message order, through one kernel
+    const uint64_t sw = h_swo[nseg] - h_swo[0];
+    uint64_t tw = 0;
+    for (uint32_t m = 0; m < nm; ++m) tw += ((h_msg_seg_off[m + 1] - h_msg_seg_off[m] + 2) & ~1ull) / 2;
+    const uint64_t np = (uint64_t)nm + nseg;
+    if (sw + tw <= cpk::kSpSmallWords && np <= 4096 && !getenv("CPK_NO_SMALL"))
+      return small_encode(
+          ctx, np, sw + tw,
+          [&](uint64_t *pin, uint64_t *desc) {
+            if (sw) fill((uint8_t *)pin, MsgChunk{0, nm, 0, nseg, 0, 8 * sw, 0, 0});
+            uint64_t t = sw, q = 0;
+            for (uint32_t m = 0; m < nm; ++m) {
+              const uint64_t a = h_msg_seg_off[m], b = h_msg_seg_off[m + 1];
+              const uint32_t count = (uint32_t)(b - a);
+              const uint64_t ntw = ((uint64_t)count + 2) / 2;
+              for (uint64_t k = 0; k < ntw; ++k) {
+                uint32_t v[2];
+                for (int h = 0; h < 2; ++h) {
+                  const uint64_t j = 2 * k + h;
+                  v[h] = j == 0 ? count - 1 : (j <= count ? (uint32_t)(h_swo[a + j] - h_swo[a + j - 1]) : 0u);
+                }
+                pin[t + k] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+              }
+              desc[2 * q] = t;
+              desc[2 * q + 1] = ntw;
+              ++q;
+              t += ntw;
+              for (uint64_t i = a; i < b; ++i, ++q) {
+                desc[2 * q] = h_swo[i] - h_swo[0];
+                desc[2 * q + 1] = h_swo[i + 1] - h_swo[i];
+              }
+            }
+          },
+          h_out, h_out_cap, h_out_off, 0);
+  }
   const std::vector<MsgChunk> cs = enc_msg_chunks(h_swo, h_msg_seg_off, nm, host_chunk_bytes());
   uint64_t mi = 0, mo = 0, mm = 0;
   for (const MsgChunk &c : cs) {

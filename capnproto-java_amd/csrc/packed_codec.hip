@@ -987,14 +987,27 @@ constexpr uint32_t kRmInfo = 4 + 513;          // status, consumed, count, words
 // stream): [0] its first byte, [1] its end, [2..3] its pieces (the table's
 // two and the segments only: the padding is the parallel path's); [5] the
 // parallel path's piece count
+// (dec_tk: the batch decoder's ticket counters, zeroed here for the one-wave
+// decode launched next -- one command fewer than a memset)
 __global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit,
                                 uint64_t cap_words, uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
-                                uint64_t *__restrict__ sdesc) {
+                                uint64_t *__restrict__ sdesc, uint32_t *__restrict__ dec_tk) {
+  if (dec_tk)
+    for (uint32_t i = threadIdx.x; i < 8 * kTkStride; i += blockDim.x) dec_tk[i] = 0;
+  // the bytes a table can reach (257 words: 2,570 packed bytes) staged in
+  // LDS by whole 16-byte lines (readable up to round_up(avail, 16)), so the
+  // byte-serial parse below makes no dependent memory round trips -- the
+  // packed bytes may be pinned host memory
+  __shared__ __attribute__((aligned(16))) uint8_t tb[2576];
+  const uint64_t nt = min(avail, (uint64_t)sizeof tb);
+  for (uint32_t i = threadIdx.x; i < (uint32_t)((nt + 15) / 16); i += blockDim.x)
+    reinterpret_cast<uint4 *>(tb)[i] = reinterpret_cast<const uint4 *>(packed)[i];
+  __syncthreads();
   if (threadIdx.x != 0) return;
   uint64_t ip = 0, total = 0;
   uint32_t count = 0;
   // sizes parked in the info row (offsets written over them below)
-  int st = read_table(packed, avail, limit, ip, count, total,
+  int st = read_table(tb, nt, limit, ip, count, total,
                       [&](uint32_t i, uint32_t sz) { info[5 + i] = sz; });
   if (st == CPK_OK && total > cap_words) st = CPK_ENOMEM;
   info[0] = (uint64_t)(int64_t)st;
@@ -1026,12 +1039,19 @@ __global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t ava
 // the message's status: its table's, else the stream's (a failed piece
 // stops the stream: the last piece carries it); the bytes consumed
 // (end: where the stream's pieces ended; npieces: how many were decoded)
+// (mirror: a host-visible copy of the finished row, or null)
 __global__ void rm_final_kernel(const uint64_t *__restrict__ end, const int32_t *__restrict__ pstatus,
-                                const uint64_t *__restrict__ npieces, uint64_t *__restrict__ info) {
-  if (threadIdx.x != 0 || (int64_t)info[0] != CPK_OK) return;
-  const int32_t st = pstatus[*npieces - 1];
-  info[0] = (uint64_t)(int64_t)st;
-  info[1] = st == CPK_OK ? *end : 0;
+                                const uint64_t *__restrict__ npieces, uint64_t *__restrict__ info,
+                                uint64_t *__restrict__ mirror) {
+  if (threadIdx.x == 0 && (int64_t)info[0] == CPK_OK) {
+    const int32_t st = pstatus[*npieces - 1];
+    info[0] = (uint64_t)(int64_t)st;
+    info[1] = st == CPK_OK ? *end : 0;
+  }
+  if (!mirror) return;
+  __syncthreads();
+  const uint32_t rows = 4 + (uint32_t)min(info[2], (uint64_t)512) + 1;  // (status, consumed, count, words, offsets)
+  for (uint32_t i = threadIdx.x; i < rows; i += blockDim.x) mirror[i] = info[i];
 }
 
 // ---- message write: Serialize.write = table piece + segment pieces --------
@@ -1193,6 +1213,7 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 
 #include "encode_v4.hip"
 #include "encode_sp.hip"
+#include "encode_sp3.hip"
 #include "decode_v2.hip"
 #include "stream_split.hip"
 
@@ -1244,6 +1265,7 @@ struct cpk_ctx_s {
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
   int encoder;            // 0: single pass (encode_sp.hip); 4: size + emit passes; 5: by piece size
   int sp_form;            // the single pass's form: 0 by density, 1 dense, 2 sparse (CPK_SP_FORM)
+  int sp_kernel;          // the dense form: 3 pipelined (encode_sp3.hip), 2 per unit (CPK_SP_KERNEL)
   int decoder;            // 2: record index (decode_v2.hip); 1: block map (decode_kernel); 3: by density
   uint64_t *sp_status;    // single pass: look-back word per piece
   uint64_t sp_cap;        //   entries
@@ -1354,6 +1376,8 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     // gate picks the single pass (A/B of the density threshold)
     const char *f = getenv("CPK_SP_FORM");
     c->sp_form = (f && f[0] == 'd') ? 1 : (f && f[0] == 's') ? 2 : 0;
+    const char *k = getenv("CPK_SP_KERNEL");
+    c->sp_kernel = (k && k[0] == '2') ? 2 : 3;
     // CPK_DECODER=1 selects the block-map decoder, 2 the record-index one
     const char *d = getenv("CPK_DECODER");
     c->decoder = (d && d[0] == '2') ? 2 : (d && d[0] == '1') ? 1 : 3;
@@ -1469,11 +1493,35 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
       attr = true;
     }
   }
-  unsigned grid = (unsigned)(cpk::kSpWpe * ctx->cus);
-  if (grid > ucap) grid = (unsigned)ucap;
   // (gated: both forms enqueued, the one the gate did not pick returns at once)
   const uint32_t *pick = gated ? ctx->tickets + cpk::kTkGate + 6 : nullptr;
-  if (pdesc)
+  if (ctx->sp_kernel == 3) {
+    static bool attr3 = false;
+    if (!attr3) {
+      hipFuncSetAttribute((const void *)cpk::sp3_encode_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)cpk::kSp3Lds);
+      hipFuncSetAttribute((const void *)cpk::sp3_encode_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)cpk::kSp3Lds);
+      attr3 = true;
+    }
+    unsigned g3 = (unsigned)(cpk::kSp3Wpe * ctx->cus);
+    if (g3 > ucap) g3 = (unsigned)ucap;
+    if (pdesc)
+      hipLaunchKernelGGL(cpk::sp3_encode_kernel<true>, dim3(g3), dim3(cpk::kSpThreads), cpk::kSp3Lds, s,
+                         (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
+                         ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
+                         ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr, pick, 0u);
+    else
+      hipLaunchKernelGGL(cpk::sp3_encode_kernel<false>, dim3(g3), dim3(cpk::kSpThreads), cpk::kSp3Lds, s,
+                         (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
+                         ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
+                         ctx->tickets + cpk::kTkErr, (const uint64_t *)nullptr, pick, 0u);
+  }
+  unsigned grid = (unsigned)(cpk::kSpWpe * ctx->cus);
+  if (grid > ucap) grid = (unsigned)ucap;
+  if (ctx->sp_kernel == 3) {
+    // (launched above)
+  } else if (pdesc)
     hipLaunchKernelGGL(cpk::sp_encode_kernel<true>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
                        ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
@@ -1911,36 +1959,54 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
   return hip_ok(hipGetLastError());
 }
 
+}  // extern "C"
+static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t traversal_limit_words,
+                             void *d_out, uint64_t out_cap_words, uint64_t *d_info, void *stream,
+                             uint64_t *info_mirror);
+extern "C" {
 int cpk_read_message(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t traversal_limit_words,
                      void *d_out, uint64_t out_cap_words, uint64_t *d_info, void *stream) {
+  return read_message_impl(ctx, d_packed, avail, traversal_limit_words, d_out, out_cap_words, d_info, stream,
+                           nullptr);
+}
+}  // extern "C"
+
+// (info_mirror: where rm_final_kernel also copies the info row, e.g. pinned
+// host memory read after one sync; d_info null: a device row in rm_buf)
+static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t traversal_limit_words,
+                             void *d_out, uint64_t out_cap_words, uint64_t *d_info, void *stream,
+                             uint64_t *info_mirror) {
   using cpk::kRmPieces;
-  if (!ctx || !d_info || (avail && !d_packed) || !d_out) return CPK_EINVAL;
+  if (!ctx || (!d_info && !info_mirror) || (avail && !d_packed) || !d_out) return CPK_EINVAL;
   if (((uintptr_t)d_packed & 15) || ((uintptr_t)d_out & 7)) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   // swo [515] | in_off [515] | statuses [514 x i32] | stream descriptor [4] | stream end [1] | pieces [1]
-  if (!ctx->rm_buf && hipMalloc(&ctx->rm_buf, (2 * (kRmPieces + 1) + kRmPieces / 2 + 8) * 8ull) != hipSuccess)
+  // | spare [2] | info row [517]
+  if (!ctx->rm_buf &&
+      hipMalloc(&ctx->rm_buf, (2 * (kRmPieces + 1) + kRmPieces / 2 + 8 + cpk::kRmInfo) * 8ull) != hipSuccess)
     return CPK_ENOMEM;
+  if (!d_info) d_info = ctx->rm_buf + 2 * (kRmPieces + 1) + kRmPieces / 2 + 8;
   uint64_t *swo = ctx->rm_buf, *in_off = swo + kRmPieces + 1;
   int32_t *pst = (int32_t *)(in_off + kRmPieces + 1);
   uint64_t *sdesc = in_off + kRmPieces + 1 + kRmPieces / 2, *send_out = sdesc + 4, *npad = sdesc + 5;
-  hipLaunchKernelGGL(cpk::rm_table_kernel, dim3(1), dim3(64), 0, s, (const uint8_t *)d_packed, avail,
-                     traversal_limit_words, out_cap_words, swo, d_info, sdesc);
   // the pieces' sizes are on the device only: the stream decoder is sized by
   // the bytes the caller's capacity can reach (10 per word at most)
   const uint64_t reach = ss_reach(avail, out_cap_words + cpk::kRmHead);
-  int rc;
   // (a lower bar than cpk_decode_stream's: a message's one-wave decode is
   //  ~0.5 GB/s, the parallel path ~250 us of fixed cost: even at 64 KiB)
   const bool par = reach >= kRmSsMin && !getenv("CPK_STREAM_ONE_WAVE");
+  hipLaunchKernelGGL(cpk::rm_table_kernel, dim3(1), dim3(64), 0, s, (const uint8_t *)d_packed, avail,
+                     traversal_limit_words, out_cap_words, swo, d_info, sdesc,
+                     par ? (uint32_t *)nullptr : ctx->tickets + cpk::kTkDec);
+  int rc;
   if (par) {
     // every piece, the padding included, gets a status; the last carries the stream's
     rc = ss_decode(ctx, (const uint8_t *)d_packed, avail, reach, swo, kRmPieces, (uint64_t *)d_out, in_off, pst, s);
   } else {
     // one wave over the table's pieces and the segments (the piece count is
-    // on the device: a one-stream descriptor), none of the padding
-    if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
-      return CPK_EDEVICE;
+    // on the device: a one-stream descriptor), none of the padding; its
+    // tickets were zeroed by rm_table_kernel
     dec_launch(ctx, true, 1, (const uint8_t *)d_packed, in_off, swo, kRmPieces, (uint64_t *)d_out, pst, avail,
                cpk::DecStreams{sdesc, sdesc + 1, sdesc + 2, 1, send_out}, s);
     rc = hip_ok(hipGetLastError());
@@ -1948,9 +2014,11 @@ int cpk_read_message(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t
   if (rc) return rc;
   hipLaunchKernelGGL(cpk::rm_final_kernel, dim3(1), dim3(64), 0, s, par ? (const uint64_t *)(in_off + kRmPieces)
                                                                         : (const uint64_t *)send_out,
-                     (const int32_t *)pst, par ? (const uint64_t *)npad : (const uint64_t *)(sdesc + 3), d_info);
+                     (const int32_t *)pst, par ? (const uint64_t *)npad : (const uint64_t *)(sdesc + 3), d_info,
+                     info_mirror);
   return hip_ok(hipGetLastError());
 }
+extern "C" {
 
 int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg_off, uint32_t nm,
                         uint64_t traversal_limit_words, void *d_out, uint64_t out_cap_words,
@@ -2071,6 +2139,28 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   if (rc) return rc;
   HostSlot &sl = p->slot[0];
   uint64_t *info = sl.pin_meta;
+  if (R < kRmSsMin && !getenv("CPK_NO_SMALL")) {
+    // the one-wave range: the kernels read the packed bytes from the pinned
+    // slot and write the words and the info row into pinned memory in place
+    // -- no DMA either way, one sync
+    memcpy(sl.pin_in, h_packed, R);
+    memset((uint8_t *)sl.pin_in + R, 0, 64);
+    rc = read_message_impl(ctx, sl.pin_in, R, traversal_limit_words, sl.pin_out, out_cap_words, nullptr, p->sk,
+                           info);
+    if (rc) {
+      pipe_drain(p);
+      return rc;
+    }
+    if (hipStreamSynchronize(p->sk)) return CPK_EDEVICE;
+    const int st = (int)(int64_t)info[0];
+    const uint32_t count = (uint32_t)info[2];
+    for (int i = 0; i < 4; ++i) h_info[i] = info[i];
+    if (st != CPK_OK) return st;
+    const uint64_t w0 = info[4], words = info[4 + count] - w0;
+    for (uint32_t i = 0; i <= count; ++i) h_info[4 + i] = info[4 + i] - w0;
+    if (words) memcpy(h_out, (const uint64_t *)sl.pin_out + w0, words * 8);
+    return CPK_OK;
+  }
   // (the bytes chunk by chunk, DMA under the host copy; then the decoder's
   // 64 bytes of read slack)
   memset((uint8_t *)sl.pin_in + R, 0, 64);

@@ -6,7 +6,7 @@ out=$1; lim=$2; shift 2
 for i in $(seq 1 40); do
   /usr/local/graft/bin/gpurun --timeout "$lim" -- "$@" > "$out" 2>&1
   rc=$?
-  [ $rc -ne 3 ] && ! grep -q "no free box right now" "$out" && exit $rc
+  [ $rc -ne 3 ] && ! grep -q "no free box right now\|backing off\|status=transient" "$out" && exit $rc
   sleep 90
 done
 exit $rc
