@@ -8,17 +8,21 @@
 // JVM's).  Messages: one segment of config-2-like words (half zero words,
 // the rest a quarter zero bytes).
 //
-//   g++ -O2 -std=c++17 -pthread -Iinclude tools/threshold_probe.cpp oracle/packed_oracle.c
+// Test infrastructure (the oracle is the checker and the CPU leg): built and
+// run by tests/test_gpu_threshold.py, or by hand:
+//   g++ -O2 -std=c++17 -pthread -Iinclude tests/cpp/threshold_probe.cpp oracle/packed_oracle.c
 //       -Lcapnproto-java_amd/lib -lcapnp_packed_hip -Wl,-rpath,$PWD/capnproto-java_amd/lib -o /tmp/probe
+//   /tmp/probe [max KiB]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
-#include "../include/capnp_packed.h"
+#include "../../include/capnp_packed.h"
 extern "C" {
-#include "../oracle/packed_oracle.h"
+#include "../../oracle/packed_oracle.h"
 }
 
 static double now() {
@@ -37,13 +41,14 @@ static double median_time(F f, int reps) {
   return t[t.size() / 2];
 }
 
-int main() {
+int main(int argc, char **argv) {
+  const size_t max_kib = argc > 1 ? (size_t)atol(argv[1]) : 16384;
   cpk_ctx ctx = nullptr;
   if (cpk_ctx_create(0, &ctx) != CPK_OK) return 1;
   uint32_t rs = 99;
   auto rnd = [&]() { return rs = rs * 1103515245u + 12345u, rs >> 8; };
   std::printf("# bytes  gpu_write_us  gpu_read_us  cpu_write_us  cpu_read_us  gpu_rt_us  cpu_rt_us\n");
-  for (size_t kib = 1; kib <= 16384; kib *= 2) {
+  for (size_t kib = 1; kib <= max_kib; kib *= 2) {
     const size_t W = kib * 128;  // words
     std::vector<uint8_t> seg(8 * W + 8, 0);
     for (size_t w = 0; w < W; ++w)
