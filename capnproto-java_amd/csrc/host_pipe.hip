@@ -184,6 +184,11 @@ int pipe_get(cpk_ctx ctx, uint64_t in_bytes, uint64_t out_bytes, uint64_t meta, 
 // in place, then one sync -- no DMA, no second kernel, no second sync.
 // lay(pin_words, desc) puts the pieces' words into the slot and their
 // (first word, words) pairs, in output order, into desc.
+// (CPK_HOST_CHUNK_KB, the tests' small chunks, keeps batches on the pipeline)
+bool small_ok(uint64_t words, uint64_t np) {
+  return words <= cpk::kSpSmallWords && np <= 4096 && !getenv("CPK_NO_SMALL") && !getenv("CPK_HOST_CHUNK_KB");
+}
+
 template <class Lay>
 int small_encode(cpk_ctx ctx, uint64_t np, uint64_t words, Lay lay, void *h_out, uint64_t h_out_cap,
                  uint64_t *h_out_off, uint64_t off_base) {
@@ -310,7 +315,7 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
   for (uint32_t i = 0; i < n; ++i)
     if (h_swo[i + 1] < h_swo[i]) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
-  if (h_swo[n] - h_swo[0] <= cpk::kSpSmallWords && n <= 4096 && !getenv("CPK_NO_SMALL")) {
+  if (small_ok(h_swo[n] - h_swo[0], n)) {
     const HostChunk all{0, n, 0, 8 * (h_swo[n] - h_swo[0]), 0, 0};
     return small_encode(
         ctx, n, h_swo[n] - h_swo[0],
@@ -648,7 +653,7 @@ int encode_messages_host_impl(cpk_ctx ctx, Fill fill, const uint64_t *h_swo, uin
     uint64_t tw = 0;
     for (uint32_t m = 0; m < nm; ++m) tw += ((h_msg_seg_off[m + 1] - h_msg_seg_off[m] + 2) & ~1ull) / 2;
     const uint64_t np = (uint64_t)nm + nseg;
-    if (sw + tw <= cpk::kSpSmallWords && np <= 4096 && !getenv("CPK_NO_SMALL"))
+    if (small_ok(sw + tw, np))
       return small_encode(
           ctx, np, sw + tw,
           [&](uint64_t *pin, uint64_t *desc) {
