@@ -590,6 +590,8 @@ __global__ __launch_bounds__(kSpThreads, 2) void sp3_encode_kernel(
 // run state a chunk leaves for the piece's next chunk passes through two LDS
 // words.  out_off[0..n] written.
 constexpr uint64_t kSpSmallWords = 32768;  // (256 KiB: four chunks, ~10 us each)
+constexpr uint32_t kSpSmallPieces = 512;   // piece descriptors staged in LDS (8 KiB)
+constexpr uint32_t kSpSmallLds = kSp3Lds + 16 * kSpSmallPieces;
 
 __device__ __forceinline__ Sp3Unit sp3_unit_at(const uint64_t *pw, uint32_t W, uint32_t p, uint32_t c, int w) {
   Sp3Unit u;
@@ -621,8 +623,12 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
   uint64_t *msk = reinterpret_cast<uint64_t *>(smem + kSp3oMsk);
   uint64_t *scr = reinterpret_cast<uint64_t *>(smem + kSp3oScr);
   uint32_t *stage = reinterpret_cast<uint32_t *>(smem + kSp3oStage);
+  uint64_t *ldesc = reinterpret_cast<uint64_t *>(smem + kSp3Lds);
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  // the descriptors in LDS at once (they may be host memory: one round
+  // trip, not two dependent ones per piece)
+  for (uint32_t i = threadIdx.x; i < 2 * n; i += kSpThreads) ldesc[i] = desc[i];
   fill_luts(lut, false);
   for (uint32_t i = threadIdx.x; i < kSp3Stage / 16; i += kSpThreads)
     reinterpret_cast<uint4 *>(stage)[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -633,8 +639,8 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
   __syncthreads();
   uint64_t g = 0;
   for (uint32_t p = 0; p < n; ++p) {
-    const uint64_t w0 = desc[2 * (uint64_t)p];
-    const uint32_t W = (uint32_t)desc[2 * (uint64_t)p + 1];
+    const uint64_t w0 = sp_ld(&ldesc[2 * p]);
+    const uint32_t W = (uint32_t)sp_ld(&ldesc[2 * p + 1]);
     const uint32_t nch = max((((W + 63) >> 6) + kSpCS - 1) / kSpCS, 1u);
     if (threadIdx.x == 0) out_off[p] = g;
     for (uint32_t c = 0; c < nch; ++c) {

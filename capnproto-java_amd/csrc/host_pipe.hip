@@ -186,7 +186,8 @@ int pipe_get(cpk_ctx ctx, uint64_t in_bytes, uint64_t out_bytes, uint64_t meta, 
 // (first word, words) pairs, in output order, into desc.
 // (CPK_HOST_CHUNK_KB, the tests' small chunks, keeps batches on the pipeline)
 bool small_ok(uint64_t words, uint64_t np) {
-  return words <= cpk::kSpSmallWords && np <= 4096 && !getenv("CPK_NO_SMALL") && !getenv("CPK_HOST_CHUNK_KB");
+  return words <= cpk::kSpSmallWords && np <= cpk::kSpSmallPieces && !getenv("CPK_NO_SMALL") &&
+         !getenv("CPK_HOST_CHUNK_KB");
 }
 
 template <class Lay>
@@ -203,10 +204,10 @@ int small_encode(cpk_ctx ctx, uint64_t np, uint64_t words, Lay lay, void *h_out,
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void *)cpk::sp_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)cpk::kSp3Lds);
+                        (int)cpk::kSpSmallLds);
     attr = true;
   }
-  hipLaunchKernelGGL(cpk::sp_small_kernel, dim3(1), dim3(cpk::kSpThreads), cpk::kSp3Lds, p->sk,
+  hipLaunchKernelGGL(cpk::sp_small_kernel, dim3(1), dim3(cpk::kSpThreads), cpk::kSpSmallLds, p->sk,
                      (const uint64_t *)s.pin_in, (const uint64_t *)desc, (uint32_t)np, (uint8_t *)s.pin_out, off,
                      ocap, ctx->tickets + cpk::kTkErr);
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p->sk) != hipSuccess) return CPK_EDEVICE;
