@@ -28,10 +28,7 @@
 // chunk to chunk (the state a chunk leaves is published for the next);
 // every unit is read once: traffic U + P for any mix of piece sizes.
 
-#ifndef CPK_SP_WAVES
-#define CPK_SP_WAVES 4
-#endif
-constexpr int kSpWaves = CPK_SP_WAVES;
+constexpr int kSpWaves = 4;
 constexpr int kSpThreads = 64 * kSpWaves;
 constexpr int kSpWS = 128 / kSpWaves;          // steps per wave
 constexpr int kSpCS = kSpWaves * kSpWS;        // steps per chunk (8192 words)
@@ -56,38 +53,7 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 // (+ 1) whose offset [5] holds
 // Steps are scheduled one at a time: hoisting later steps' LUT reads and
 // lane reads ahead would keep them all live at once (VGPR spills).
-#ifndef CPK_SP_FENCE
-#define CPK_SP_FENCE 1
-#endif
-#if CPK_SP_FENCE
 #define CPK_SP_STEP_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define CPK_SP_STEP_FENCE()
-#endif
-#ifndef CPK_SP_PUT_PERM
-#define CPK_SP_PUT_PERM 1
-#endif
-#ifndef CPK_SP_UNI_BASE
-#define CPK_SP_UNI_BASE 1
-#endif
-#ifndef CPK_SP_FLUSH_UNCOND
-#define CPK_SP_FLUSH_UNCOND 1
-#endif
-#ifndef CPK_SP_A1FULL
-#define CPK_SP_A1FULL 1
-#endif
-#ifndef CPK_SP_HCBR
-#define CPK_SP_HCBR 1  // head counts only in steps with heads (a branch per step: -2 % encode)
-#endif
-#ifndef CPK_SP_NTLD
-#define CPK_SP_NTLD 1  // nontemporal loads of the words (A1; config 3 encode -1.5 %)
-#endif
-#ifndef CPK_SP_NTST
-#define CPK_SP_NTST 1  // nontemporal stores of the packed lines (flush; config 3 encode -1 %)
-#endif
-#ifndef CPK_SP_PRIO_A1
-#define CPK_SP_PRIO_A1 1  // raised wave priority while A1 issues its loads (configs 3 / 4 encode -1 %)
-#endif
 #ifndef CPK_SP_WPE
 #define CPK_SP_WPE 3  // waves per SIMD the registers must allow (3 workgroups per CU)
 #endif
@@ -194,12 +160,6 @@ __device__ uint32_t sp_cont(const uint64_t *msk, int s, int cs, int cls, uint32_
   return min(r, 256u);
 }
 
-#ifndef CPK_SP_ABL
-#define CPK_SP_ABL 0  // ablations for timing only (wrong output): 1 no ring ORs, 2 no head counts, 4 no LUT read, 8 no line stores
-#endif
-#ifndef CPK_SP_EVEN
-#define CPK_SP_EVEN 1  // a short chunk's steps spread over all waves (4 Ki-word pieces: encode -15 %)
-#endif
 #ifndef CPK_SP_A1G
 #define CPK_SP_A1G 8  // (reload form) steps whose loads A1 keeps in flight per group
 #endif
@@ -273,20 +233,12 @@ __device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict_
                                           int cnt, int lane) {
   // loads clamped to the piece, not predicated: step j's lanes read
   // min(lane, last valid lane of the step) (one lane register for all steps)
-#if CPK_SP_PRIO_A1
   __builtin_amdgcn_s_setprio(1);  // (the loads out first)
-#endif
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j)
     if (kFull || j < cnt)
-#if CPK_SP_NTLD
       R.v[j] = ld_stream(&(src + j * 64)[kFull ? (uint32_t)lane : min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))]);
-#else
-      R.v[j] = (src + j * 64)[kFull ? (uint32_t)lane : min((uint32_t)lane, min(wrem - 1 - 64u * j, 63u))];
-#endif
-#if CPK_SP_PRIO_A1
   __builtin_amdgcn_s_setprio(0);
-#endif
   uint32_t acc = 0;
 #pragma unroll
   for (int j = 0; j < kSpWS; ++j) {
@@ -530,23 +482,13 @@ __device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t 
   }
   for (uint32_t t0 = ft; t0 < upto; t0 += 64) {
     const uint32_t t = t0 + (uint32_t)lane;
-#if CPK_SP_FLUSH_UNCOND
     // every lane builds a line (ring indices wrap: lanes past upto read
     // harmless lines): the shift's switch on the uniform k stays a scalar
     // branch instead of an exec-masked one inside the lane condition
     const uint4 v = sp_gline(ring, t, k);
-#else
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (t < upto) v = sp_gline(ring, t, k);
-#endif
     wave_lds_order();
     if (t < upto) {
-#if CPK_SP_NTST
-      if (!(CPK_SP_ABL & 8) && (L0 + t) * 16 + 16 <= ocap) st_stream(v, out + (L0 + t) * 16);
-      if (CPK_SP_ABL & 8) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-#else
-      if ((L0 + t) * 16 + 16 <= ocap) *reinterpret_cast<uint4 *>(out + (L0 + t) * 16) = v;
-#endif
+      if ((L0 + t) * 16 + 16 <= ocap) st_stream(v, out + (L0 + t) * 16);
       if (t) sp_ring_clear(ring, t - 1);
     }
     wave_lds_order();
@@ -558,27 +500,18 @@ __device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t 
 // offset is given (known) or fetched once kSpDefer steps are in the ring
 // (getbase: wave 0 runs the piece's look-back meanwhile -- the other waves
 // have had that many steps of work before they wait for it).
-#ifndef CPK_SP_DEFER
-#define CPK_SP_DEFER (((int)(kSpRing - 16) / 640) & ~1)  // steps laid out before the offset is needed (12 at 8 KiB)
-#endif
-#ifndef CPK_SP_BPF
-#define CPK_SP_BPF 2  // (reload form) step pairs whose words B has in flight ahead
-#endif
-constexpr int kSpDefer = CPK_SP_DEFER;
-// which waves may lay out all their steps before fetching the offset when
-// their output fits the ring (0: none; 1: waves 1-3; 2: all -- measured
-// best: the look-back then runs last, when the pieces before have published)
-#ifndef CPK_SP_FITS
-#define CPK_SP_FITS 2
-#endif
-#define CPK_SP_FITS_WAVES(w) (CPK_SP_FITS == 2 || (CPK_SP_FITS == 1 && (w) != 0))
+// steps laid out before the offset is needed (12 at 8 KiB)
+constexpr int kSpDefer = (((int)(kSpRing - 16) / 640) & ~1);
+// (every wave whose output fits its ring lays out all its steps before
+// fetching the offset: the look-back then runs last, when the pieces before
+// have published -- measured best)
 static_assert(kSpDefer * 640 + 16 <= (int)kSpRing && kSpDefer % 2 == 0, "deferred steps must fit the ring");
 template <class GetBase>
 __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, uint32_t *ring, uint8_t *out,
                                      bool known, bool fits, uint64_t g0, int lane, uint64_t ocap,
                                      const uint64_t *__restrict__ src, uint32_t wrem, GetBase getbase) {
 #if CPK_SP_RELOAD
-  // the words again (read by A1 moments ago: L2), CPK_SP_BPF pairs ahead
+  // the words again (read by A1 moments ago: L2), 2 pairs ahead
   uint64_t pv[kSpWS];
   // only the lanes whose word is nonzero load it (a zero word's string
   // needs no bytes): a line of zero words is not fetched again at all
@@ -589,15 +522,13 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     }
   };
 #pragma unroll
-  for (int j = 0; j < 2 * CPK_SP_BPF; ++j) ldw(j);
+  for (int j = 0; j < 2 * 2; ++j) ldw(j);
 #endif
   uint32_t rel = 0, ft = 0;
-#if CPK_SP_UNI_BASE
   // the output offset is wave-uniform: say so (readfirstlane), or the flush
   // condition and the line shift's switch on g0 & 15 compile to exec-masked
   // branches
   g0 = sp_uni(g0);
-#endif
   const uint32_t l64 = 64u - (uint32_t)lane;
   // step j's string per lane (s0..s2, nb bytes)
   auto strings = [&](const int j, uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &nb)
@@ -610,20 +541,12 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
 #else
     const uint32_t lo = (uint32_t)R.v[j], hi = (uint32_t)(R.v[j] >> 32);
 #endif
-#if CPK_SP_ABL & 4
-    const uint64_t sel = 0x0706050403020100ull + m;  // (ablation: no LUT read)
-#else
     const uint64_t sel = lut[m];
-#endif
     const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
     const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
     const bool zw = m == 0;
     uint32_t cz = 0, cd = 0;
-#if CPK_SP_ABL & 2
-    if (false)
-#elif CPK_SP_HCBR
     if (HC)
-#endif
     {
       // a head's count: words to its run's end, at most 255 (:119-131, :143-164)
       const uint32_t X = (uint32_t)__builtin_amdgcn_readlane((int)R.ox, j);
@@ -656,23 +579,14 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
   };
   // a string OR-ed into the ring at relative byte p
   auto put = [&](uint32_t p, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t nb) __attribute__((always_inline)) {
-#if CPK_SP_PUT_PERM
     // the string shifted left by p & 3 bytes over four dwords: one v_perm
     // each, selector bytes [4 - b, 8 - b) of (s_k : s_k-1)
     const uint32_t b = p & 3;
     const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, b, 0u);  // (b in every byte)
     const uint32_t d0 = __builtin_amdgcn_perm(s0, 0u, sel), d1 = __builtin_amdgcn_perm(s1, s0, sel);
     const uint32_t d2 = __builtin_amdgcn_perm(s2, s1, sel), d3 = __builtin_amdgcn_perm(0u, s2, sel);
-#else
-    const uint32_t sh = (p & 3) * 8;
-    const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
-    const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
-    const uint32_t d0 = (uint32_t)a01, d1 = (uint32_t)(a01 >> 32), d2 = (uint32_t)(a12 >> 32);
-    const uint32_t d3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
-#endif
     uint32_t *rp = ring + ((p >> 2) & (kSpRing / 4 - 1));
-    if (CPK_SP_ABL & 1) asm volatile("" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3), "v"(rp));
-    else if (nb) {  // (zero-length strings would all hit one address)
+    if (nb) {  // (zero-length strings would all hit one address)
       atomicOr(rp, d0);
       atomicOr(rp + 1, d1);
       atomicOr(rp + 2, d2);
@@ -683,8 +597,8 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
   // (16-bit halves: a step's strings total at most 640 bytes)
   auto step = [&](const int j) __attribute__((always_inline)) {
 #if CPK_SP_RELOAD
-    ldw(j + 2 * CPK_SP_BPF);
-    ldw(j + 2 * CPK_SP_BPF + 1);
+    ldw(j + 2 * 2);
+    ldw(j + 2 * 2 + 1);
 #endif
     {
       uint32_t a0, a1, a2, na, b0 = 0, b1 = 0, b2 = 0, nb2 = 0;
@@ -716,18 +630,14 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     if (j < cnt) step(j);
   if (!known && !fits && cnt > kSpDefer) {
     g0 = getbase();
-#if CPK_SP_UNI_BASE
     g0 = sp_uni(g0);
-#endif
     known = true;
   }
 #pragma unroll
   for (int j = kSpDefer; j < kSpWS; j += 2)
     if (j < cnt) step(j);
   if (!known) g0 = getbase();
-#if CPK_SP_UNI_BASE
   g0 = sp_uni(g0);
-#endif
   wave_lds_order();
   const uint32_t k = (uint32_t)(g0 & 15);
   const uint32_t done = (k + rel) >> 4;
@@ -862,26 +772,19 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   const uint32_t ns = (W + 63) >> 6;
   const uint32_t cs0 = c * kSpCS;
   const int cs = (int)min((uint32_t)kSpCS, ns - cs0);  // steps in this chunk
-#if CPK_SP_EVEN
   // a chunk's steps spread over all waves (a short piece keeps every wave
   // busy, not wave 0 alone): per wave ceil(cs / waves), rounded up to a pair
   const int per = min(kSpWS, ((cs + kSpWaves - 1) / kSpWaves + 1) & ~1);
   const int sa = w * per;
   cnt = max(0, min(per, cs - sa));
-#else
-  const int sa = w * kSpWS;
-  cnt = max(0, min(kSpWS, cs - sa));
-#endif
   const uint32_t wfirst = (cs0 + (uint32_t)sa) * 64;  // the wave's first word
   const uint32_t wrem = cnt ? W - wfirst : 0;
   wsrc = pw + wfirst;
   wrem_o = wrem;
   uint32_t acc = 0;
   if (cnt) {
-#if CPK_SP_A1FULL
     if (cnt == kSpWS && wrem >= 64u * kSpWS) acc = sp_a1<true>(R, pw + wfirst, wrem, cnt, lane);
     else
-#endif
       acc = sp_a1<false>(R, pw + wfirst, wrem, cnt, lane);
     sp_put_masks(R, msk, sa, cnt, lane);
   }
@@ -1083,7 +986,7 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
         WPH(6)
         return sp_ld(&scr[5]) + wbefore;
       };
-      sp_b(R, cnt, lut, ring, out, false, CPK_SP_FITS_WAVES(w) && wmine + 16 <= kSpRing, wbefore, lane, ocap,
+      sp_b(R, cnt, lut, ring, out, false, wmine + 16 <= kSpRing, wbefore, lane, ocap,
            wsrc, wrem, getbase);
     } else if (w == 0) {
       getoff();  // wave 0 runs the look-back even without steps (an empty piece)
