@@ -776,35 +776,6 @@ __global__ __launch_bounds__(kDecThreads, kDecWpe) void decode_kernel(
           const int wbase = ow + rb + kBlk * b;  // piece word of the block's first word
           const int wleft = ow + T - wbase - 1;   // words of the window after the block's first
           uint64_t words[kBlk];
-          // a block whose words all lie inside one run: a zero run's words,
-          // or the counted words of a 0xFF run, copied from the window as
-          // 36 bytes (9 LDS dwords for 4 words; no per-word record reads) --
-          // the usual block of dense (literal-run) and sparse data
-          bool run = false;
-          {
-            const uint32_t t0 = pkw[q], c10 = pkw[q + 1], c90 = pkw[q + 9];
-            const uint32_t nw0 = 1u + (t0 == 0 ? c10 : 0u) + (t0 == 0xffu ? c90 : 0u);
-            if (t0 == 0 && (uint32_t)ofs + kBlk <= nw0) {
-#pragma unroll
-              for (int i = 0; i < kBlk; ++i) words[i] = 0;
-              run = true;
-            } else if (t0 == 0xffu && ofs >= 1 && (uint32_t)ofs + kBlk <= nw0) {
-              const uint32_t x = q + 2 + 8u * (uint32_t)ofs;  // the block's first word (PackedInputStream.java:106-134)
-              if (x + 8 * kBlk + 4 <= lend) {
-                const uint32_t sh = (x + ph) & 3;
-                const uint32_t *pl = reinterpret_cast<const uint32_t *>(pkw + ((int64_t)x - sh));
-                uint32_t dw[2 * kBlk + 1];
-#pragma unroll
-                for (int k = 0; k < 2 * kBlk + 1; ++k) dw[k] = pl[k];
-#pragma unroll
-                for (int i = 0; i < kBlk; ++i)
-                  words[i] = (uint64_t)__builtin_amdgcn_alignbyte(dw[2 * i + 1], dw[2 * i], sh) |
-                             ((uint64_t)__builtin_amdgcn_alignbyte(dw[2 * i + 2], dw[2 * i + 1], sh) << 32);
-                run = true;
-              }
-            }
-          }
-          if (!run)
 #pragma unroll
           for (int i = 0; i < kBlk; ++i) {
             // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
