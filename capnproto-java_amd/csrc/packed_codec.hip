@@ -441,11 +441,6 @@ __global__ __launch_bounds__(kDecThreads, kDecWpe) void decode_kernel(
   uint64_t slim = avail;  //   end of the stream's bytes
   int sfail = CPK_OK;     //   a failed piece stops the stream
   uint32_t snext = 0, sende = 0, sj = 0;  // next piece, end of the stream's pieces, stream
-  // batch form: the next piece's ticket is taken as a piece starts and read
-  // when it ends (its atomic's latency under the piece's decode)
-  uint32_t pre = 0;
-  int prex = 0;
-  bool havep = false;
 
   for (uint32_t sidx = 0;; ++sidx) {
     // every branch below is on wave-uniform (SGPR) values: the compiler
@@ -455,23 +450,10 @@ __global__ __launch_bounds__(kDecThreads, kDecWpe) void decode_kernel(
     // divergent loop re-running piece 0.  Tickets count in units of 64.
     uint32_t seg = sidx;
     if (!kStream) {
-      bool got = false;
-      if (havep) {
-        seg = (((uint32_t)__builtin_amdgcn_readlane((int)pre, 0) >> 6) << 3) | (uint32_t)prex;
-        havep = false;
-        got = seg < n;
-      }
-      if (!got) {
-        for (;;) {
-          seg = take_ticket(ticket, xq);
-          if (seg < n || ++dry >= 8) break;
-          xq = (xq + 1) & 7;  // this counter ran dry: help the next one
-        }
-      }
-      if (seg < n) {
-        pre = atomicAdd(&ticket[xq * kTkStride], 1u);
-        prex = xq;
-        havep = true;
+      for (;;) {
+        seg = take_ticket(ticket, xq);
+        if (seg < n || ++dry >= 8) break;
+        xq = (xq + 1) & 7;  // this counter ran dry: help the next one
       }
     } else {
       // the next stream with pieces (empty streams end where they begin)
