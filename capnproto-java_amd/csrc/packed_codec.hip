@@ -421,11 +421,10 @@ struct DecStreams {
   const uint32_t *skip;  // (batch form: nonzero = the other decoder took the batch)
 };
 template <bool kStream>
-__global__ __launch_bounds__(kDecThreads, kDecWpe) void decode_kernel(
-    const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
-    const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
-    int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail, DecStreams sd) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+__device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__restrict__ packed,
+                                            uint64_t *__restrict__ in_off, const uint64_t *__restrict__ swo,
+                                            uint32_t n, uint64_t *__restrict__ out, int32_t *__restrict__ status,
+                                            uint32_t *ticket, uint64_t avail, DecStreams sd) {
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem);
   const int lane = lane_id(), w = wave_id();
   uint8_t *wl = smem + 2048 + w * kDecWaveLds;
@@ -837,6 +836,14 @@ __global__ __launch_bounds__(kDecThreads, kDecWpe) void decode_kernel(
   }
   WPH_FLUSH(16)
 }
+template <bool kStream>
+__global__ __launch_bounds__(kDecThreads, kDecWpe) void decode_kernel(
+    const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
+    const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
+    int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail, DecStreams sd) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  decode_body<kStream>(smem, packed, in_off, swo, n, out, status, ticket, avail, sd);
+}
 
 // ------------------------------------------------------------ messages
 // Serialize.read over PackedInputStream for a batch of packed messages whose
@@ -989,21 +996,37 @@ constexpr uint32_t kRmInfo = 4 + 513;          // status, consumed, count, words
 // parallel path's piece count
 // (dec_tk: the batch decoder's ticket counters, zeroed here for the one-wave
 // decode launched next -- one command fewer than a memset)
-__global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit,
-                                uint64_t cap_words, uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
-                                uint64_t *__restrict__ sdesc, uint32_t *__restrict__ dec_tk) {
+constexpr uint32_t kRmTableBytes = 2576;  // a table's packed bytes at most (257 words: 2,570)
+__device__ void rm_table_parse(const uint8_t *tb, uint64_t nt, uint64_t avail, uint64_t limit, uint64_t cap_words,
+                               uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
+                               uint64_t *__restrict__ sdesc);
+__device__ __forceinline__ void rm_table_body(const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit,
+                                              uint64_t cap_words, uint64_t *__restrict__ swo,
+                                              uint64_t *__restrict__ info, uint64_t *__restrict__ sdesc,
+                                              uint32_t *__restrict__ dec_tk, uint8_t *tb) {
   if (dec_tk)
     for (uint32_t i = threadIdx.x; i < 8 * kTkStride; i += blockDim.x) dec_tk[i] = 0;
-  // the bytes a table can reach (257 words: 2,570 packed bytes) staged in
-  // LDS by whole 16-byte lines (readable up to round_up(avail, 16)), so the
-  // byte-serial parse below makes no dependent memory round trips -- the
-  // packed bytes may be pinned host memory
-  __shared__ __attribute__((aligned(16))) uint8_t tb[2576];
-  const uint64_t nt = min(avail, (uint64_t)sizeof tb);
+  // the bytes a table can reach staged in LDS (tb) by whole 16-byte lines
+  // (readable up to round_up(avail, 16)), so the byte-serial parse below
+  // makes no dependent memory round trips -- the packed bytes may be pinned
+  // host memory
+  const uint64_t nt = min(avail, (uint64_t)kRmTableBytes);
   for (uint32_t i = threadIdx.x; i < (uint32_t)((nt + 15) / 16); i += blockDim.x)
     reinterpret_cast<uint4 *>(tb)[i] = reinterpret_cast<const uint4 *>(packed)[i];
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x == 0) rm_table_parse(tb, nt, avail, limit, cap_words, swo, info, sdesc);
+}
+__global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit,
+                                uint64_t cap_words, uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
+                                uint64_t *__restrict__ sdesc, uint32_t *__restrict__ dec_tk) {
+  __shared__ __attribute__((aligned(16))) uint8_t tb[kRmTableBytes];
+  rm_table_body(packed, avail, limit, cap_words, swo, info, sdesc, dec_tk, tb);
+}
+// (one thread) the table read and checked as doRead does, the message laid
+// out as the stream's pieces
+__device__ void rm_table_parse(const uint8_t *tb, uint64_t nt, uint64_t avail, uint64_t limit, uint64_t cap_words,
+                               uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
+                               uint64_t *__restrict__ sdesc) {
   uint64_t ip = 0, total = 0;
   uint32_t count = 0;
   // sizes parked in the info row (offsets written over them below)
@@ -1040,9 +1063,17 @@ __global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t ava
 // stops the stream: the last piece carries it); the bytes consumed
 // (end: where the stream's pieces ended; npieces: how many were decoded)
 // (mirror: a host-visible copy of the finished row, or null)
+__device__ __forceinline__ void rm_final_body(const uint64_t *__restrict__ end, const int32_t *__restrict__ pstatus,
+                                              const uint64_t *__restrict__ npieces, uint64_t *__restrict__ info,
+                                              uint64_t *__restrict__ mirror);
 __global__ void rm_final_kernel(const uint64_t *__restrict__ end, const int32_t *__restrict__ pstatus,
                                 const uint64_t *__restrict__ npieces, uint64_t *__restrict__ info,
                                 uint64_t *__restrict__ mirror) {
+  rm_final_body(end, pstatus, npieces, info, mirror);
+}
+__device__ __forceinline__ void rm_final_body(const uint64_t *__restrict__ end, const int32_t *__restrict__ pstatus,
+                                              const uint64_t *__restrict__ npieces, uint64_t *__restrict__ info,
+                                              uint64_t *__restrict__ mirror) {
   if (threadIdx.x == 0 && (int64_t)info[0] == CPK_OK) {
     const int32_t st = pstatus[*npieces - 1];
     info[0] = (uint64_t)(int64_t)st;
@@ -1052,6 +1083,25 @@ __global__ void rm_final_kernel(const uint64_t *__restrict__ end, const int32_t 
   __syncthreads();
   const uint32_t rows = 4 + (uint32_t)min(info[2], (uint64_t)512) + 1;  // (status, consumed, count, words, offsets)
   for (uint32_t i = threadIdx.x; i < rows; i += blockDim.x) mirror[i] = info[i];
+}
+
+// cpk_read_message whole in ONE launch when the one-wave decoder takes the
+// message: the table (rm_table_body), the stream of its pieces
+// (decode_body<true>: one of the four waves finds the stream's ticket) and
+// the info row (rm_final_body), separated by workgroup barriers -- three
+// launches' dispatch latency saved on the small-message path
+__global__ __launch_bounds__(kDecThreads, 1) void rm_small_kernel(
+    const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit, uint64_t cap_words,
+    uint64_t *__restrict__ swo, uint64_t *__restrict__ info, uint64_t *__restrict__ sdesc, uint32_t *tk,
+    uint64_t *__restrict__ out, uint64_t *__restrict__ in_off, int32_t *__restrict__ pst,
+    uint64_t *__restrict__ send_out, uint64_t *__restrict__ mirror) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  rm_table_body(packed, avail, limit, cap_words, swo, info, sdesc, tk, smem);
+  __syncthreads();  // (the layout and the zeroed tickets before the decode)
+  decode_body<true>(smem, packed, in_off, swo, kRmPieces, out, pst, tk, avail,
+                    DecStreams{sdesc, sdesc + 1, sdesc + 2, 1, send_out, nullptr});
+  __syncthreads();  // (the stream's end and statuses before the fold)
+  rm_final_body(send_out, pst, sdesc + 3, info, mirror);
 }
 
 // ---- message write: Serialize.write = table piece + segment pieces --------
@@ -1996,6 +2046,12 @@ static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, 
   // (a lower bar than cpk_decode_stream's: a message's one-wave decode is
   //  ~0.5 GB/s, the parallel path ~250 us of fixed cost: even at 64 KiB)
   const bool par = reach >= kRmSsMin && !getenv("CPK_STREAM_ONE_WAVE");
+  if (!par && !dec_v2(ctx)) {
+    hipLaunchKernelGGL(cpk::rm_small_kernel, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds, s,
+                       (const uint8_t *)d_packed, avail, traversal_limit_words, out_cap_words, swo, d_info, sdesc,
+                       ctx->tickets + cpk::kTkDec, (uint64_t *)d_out, in_off, pst, send_out, info_mirror);
+    return hip_ok(hipGetLastError());
+  }
   hipLaunchKernelGGL(cpk::rm_table_kernel, dim3(1), dim3(64), 0, s, (const uint8_t *)d_packed, avail,
                      traversal_limit_words, out_cap_words, swo, d_info, sdesc,
                      par ? (uint32_t *)nullptr : ctx->tickets + cpk::kTkDec);
