@@ -40,6 +40,12 @@ constexpr int kSpCS = kSpWaves * kSpWS;        // steps per chunk (8192 words)
 #endif
 constexpr uint32_t kSpRing = CPK_SP_RING;      // output ring per wave (bytes)
 constexpr uint32_t kSpRingLines = kSpRing / 16;
+constexpr uint32_t kSpRing4 = kSpRing / 4;       // (dwords)
+static_assert(kSpRing % 16 == 0, "whole lines");
+// ring line of relative line i (the dense form's 11 KiB ring is no power of two)
+__device__ __forceinline__ uint32_t sp_rline(uint32_t i) {
+  return (kSpRingLines & (kSpRingLines - 1)) == 0 ? (i & (kSpRingLines - 1)) : (i % kSpRingLines);
+}
 constexpr uint32_t kSpRingStride = kSpRing + 16;  // + one overhang line (line 0's spill)
 constexpr uint32_t kSpoLut = 0;                                      // u64[256]
 constexpr uint32_t kSpoMsk = 2048;                                   // u64[kSpCS][3]
@@ -413,8 +419,9 @@ __device__ __forceinline__ void sp_xs(SpRegs &R, int cnt, uint32_t Xlast, int la
 // i.e. the last k bytes of relative line t - 1 and the first 16 - k of line t.
 __device__ __forceinline__ uint4 sp_ring_line(const uint32_t *ring, uint32_t i) {
   const uint4 *rl = reinterpret_cast<const uint4 *>(ring);
-  uint4 v = rl[i & (kSpRingLines - 1)];
-  if ((i & (kSpRingLines - 1)) == 0) {
+  const uint32_t r = sp_rline(i);
+  uint4 v = rl[r];
+  if (r == 0) {
     const uint4 o = rl[kSpRingLines];
     v.x |= o.x;
     v.y |= o.y;
@@ -425,8 +432,9 @@ __device__ __forceinline__ uint4 sp_ring_line(const uint32_t *ring, uint32_t i) 
 }
 __device__ __forceinline__ void sp_ring_clear(uint32_t *ring, uint32_t i) {
   uint4 *rl = reinterpret_cast<uint4 *>(ring);
-  rl[i & (kSpRingLines - 1)] = make_uint4(0u, 0u, 0u, 0u);
-  if ((i & (kSpRingLines - 1)) == 0) rl[kSpRingLines] = make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t r = sp_rline(i);
+  rl[r] = make_uint4(0u, 0u, 0u, 0u);
+  if (r == 0) rl[kSpRingLines] = make_uint4(0u, 0u, 0u, 0u);
 }
 // global line (g0 >> 4) + t from relative lines t - 1 and t
 __device__ __forceinline__ uint4 sp_gline(const uint32_t *ring, uint32_t t, uint32_t k) {
@@ -577,15 +585,20 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     // ZO mask, without its two lane reads
     nb = sp_sel(zw ? 0u : nb, nb, HC);
   };
-  // a string OR-ed into the ring at relative byte p
-  auto put = [&](uint32_t p, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t nb) __attribute__((always_inline)) {
+  // a string OR-ed into the ring at relative byte p (r4 / relq: the ring
+  // dword of the step's first byte rel and rel >> 2, wave-uniform -- the
+  // ring position without a per-lane modulo: p - rel < 1,284)
+  auto put = [&](uint32_t p, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t nb, uint32_t r4, uint32_t relq)
+      __attribute__((always_inline)) {
     // the string shifted left by p & 3 bytes over four dwords: one v_perm
     // each, selector bytes [4 - b, 8 - b) of (s_k : s_k-1)
     const uint32_t b = p & 3;
     const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, b, 0u);  // (b in every byte)
     const uint32_t d0 = __builtin_amdgcn_perm(s0, 0u, sel), d1 = __builtin_amdgcn_perm(s1, s0, sel);
     const uint32_t d2 = __builtin_amdgcn_perm(s2, s1, sel), d3 = __builtin_amdgcn_perm(0u, s2, sel);
-    uint32_t *rp = ring + ((p >> 2) & (kSpRing / 4 - 1));
+    uint32_t q = r4 + ((p >> 2) - relq);
+    q = q >= kSpRing4 ? q - kSpRing4 : q;
+    uint32_t *rp = ring + q;
     if (nb) {  // (zero-length strings would all hit one address)
       atomicOr(rp, d0);
       atomicOr(rp + 1, d1);
@@ -609,8 +622,9 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
       const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       if (stot) {
         const uint32_t ta = stot & 0xffffu;
-        put(rel + (incl & 0xffffu) - na, a0, a1, a2, na);
-        put(rel + ta + (incl >> 16) - nb2, b0, b1, b2, nb2);
+        const uint32_t relq = rel >> 2, r4 = relq % kSpRing4;
+        put(rel + (incl & 0xffffu) - na, a0, a1, a2, na, r4, relq);
+        put(rel + ta + (incl >> 16) - nb2, b0, b1, b2, nb2, r4, relq);
         rel += ta + (stot >> 16);
         // complete lines leave 64 at a time (one full-wave store)
         if (known) {

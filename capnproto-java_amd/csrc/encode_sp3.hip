@@ -1,28 +1,15 @@
-// encode_sp3.hip -- the single-pass encoder, pipelined across units.
-// Included from packed_codec.hip after encode_sp.hip (namespace cpk); reuses
-// its per-unit algebra (A1 tags / ballots, A2 roles, B strings) and its
-// decoupled look-back, PackedOutputStream.java:35-205 restated per unit.
+// encode_sp3.hip -- one workgroup encoding a small batch in order: the
+// one-launch kernel behind the host path for small messages
+// (cpk_encode_messages_host / cpk_encode_host, host_pipe.hip).  Included from
+// packed_codec.hip after encode_sp.hip (namespace cpk); reuses the single
+// pass's per-unit algebra (A1 tags / ballots, A2 roles, B strings),
+// PackedOutputStream.java:35-205 restated per 8192-word chunk, with the
+// chunk's packed bytes staged whole in LDS and the output offset running.
 //
-// sp_encode_kernel (encode_sp.hip) runs each unit as load -> A -> offset ->
-// B in one workgroup, so every unit exposes its load latency once, and a
-// wave whose output outgrows its 8 KiB ring waits for the offset while its
-// predecessors may not have published yet.  Here each workgroup keeps two
-// units in flight and staggers them:
-//
-//   iteration i   loads of unit i+1 issued (words into a second register
-//                 set; the ticket of unit i+2 taken)
-//                 A(i)  tags, roles, size published (the words of unit i
-//                       arrived during iteration i-1)
-//                 offset of unit i-1 from the look-back (its status polls
-//                       were issued before A(i)), unit i-1's packed bytes
-//                       flushed from the LDS stage to the output
-//                 B(i)  unit i's strings into the LDS stage (the whole unit:
-//                       73,728 bytes at most), no offset needed
-//
-// so no load latency is exposed after the first unit, and a unit's offset
-// is asked for one whole iteration after its size was published -- the
-// units before it (earlier tickets, same stagger) have published by then.
-// 2 workgroups per CU (LDS stage), 2 waves per SIMD (two word sets: 128 VGPRs).
+// (Round 4 also ran a pipelined batch encoder on these pieces -- each
+// workgroup with the next unit's words in flight and a whole-unit LDS stage,
+// its look-back one iteration late: 2 workgroups per CU, config 2 encode
+// +7 % against the per-unit kernel with 11 KiB rings, docs/tuning_log.md.)
 
 constexpr uint32_t kSp3Stage = 9 * 64 * kSpCS + 32;  // a unit's packed bytes (<= 9 per word) + put spill
 constexpr uint32_t kSp3oLut = 0;
@@ -30,8 +17,6 @@ constexpr uint32_t kSp3oMsk = 2048;
 constexpr uint32_t kSp3oScr = kSp3oMsk + kSpCS * 24;
 constexpr uint32_t kSp3oStage = kSp3oScr + 32 * 8;
 constexpr uint32_t kSp3Lds = kSp3oStage + kSp3Stage;  // 79,136 B
-constexpr int kSp3Wpe = 2;                              // workgroups per CU
-static_assert(kSp3Lds * kSp3Wpe <= 160 * 1024, "two workgroups per CU");
 static_assert(kSp3oStage % 16 == 0, "LDS alignment");
 
 // One unit as a wave sees it: the piece, the chunk and this wave's steps.
@@ -48,55 +33,7 @@ struct Sp3Unit {
   uint32_t wrem;       // piece words from wfirst on (0: no steps)
 };
 
-template <bool kMsg>
-__device__ __forceinline__ Sp3Unit sp3_unit(uint32_t t, uint32_t nu, const uint64_t *__restrict__ in,
-                                            const uint64_t *__restrict__ swo, const uint64_t *__restrict__ pdesc,
-                                            const uint64_t *__restrict__ tin, const uint64_t *__restrict__ utab,
-                                            uint64_t hint, int w) {
-  Sp3Unit u;
-  u.pw = in;
-  u.W = 0;
-  u.p = u.c = 0;
-  u.lastc = true;
-  u.bad = u.over = false;
-  u.cs = u.sa = u.cnt = 0;
-  u.wfirst = u.wrem = 0;
-  if (t >= nu) return u;
-  const uint64_t ud = utab ? utab[t] : (uint64_t)t << 32;
-  u.p = (uint32_t)(ud >> 32);
-  u.c = (uint32_t)ud;
-  uint64_t w0, W64;
-  const uint64_t *base = in;
-  if (kMsg) {
-    w0 = pdesc[2 * (uint64_t)u.p];
-    W64 = pdesc[2 * (uint64_t)u.p + 1];
-    if (w0 >> 63) base = tin;
-    w0 &= ~(1ull << 63);
-  } else {
-    w0 = swo[u.p];
-    W64 = swo[u.p + 1] - w0;
-  }
-  // (a unit table exists when pieces may exceed a chunk: a piece over the
-  // hint is then one empty unit, sp_units_count_kernel)
-  u.bad = W64 >= (1ull << 31) || (!utab && W64 > 64ull * kSpCS) || (utab && hint && W64 > hint);
-  u.over = hint && W64 > hint;
-  u.W = u.bad ? 0u : (uint32_t)W64;
-  u.pw = base + w0;
-  const uint32_t ns = (u.W + 63) >> 6;
-  const uint32_t nch = max((ns + kSpCS - 1) / kSpCS, 1u);
-  u.lastc = u.c + 1 >= nch;
-  const uint32_t cs0 = u.c * kSpCS;
-  u.cs = ns > cs0 ? (int)min((uint32_t)kSpCS, ns - cs0) : 0;
-  // a chunk's steps spread over all waves, rounded up to a pair
-  const int per = min(kSpWS, ((u.cs + kSpWaves - 1) / kSpWaves + 1) & ~1);
-  u.sa = w * per;
-  u.cnt = max(0, min(per, u.cs - u.sa));
-  u.wfirst = (cs0 + (uint32_t)u.sa) * 64;
-  u.wrem = u.cnt ? u.W - u.wfirst : 0;
-  return u;
-}
-
-// The wave's words of a unit, every load issued (none waited for): step j
+// The wave's words of a chunk, every load issued (none waited for): step j
 // of lane l reads word min(64 j + l, last) -- a partial step or wave reads
 // its last word again, a wave without steps a valid dummy word.
 __device__ __forceinline__ void sp3_load(uint64_t (&V)[kSpWS], const Sp3Unit &u, const uint64_t *dummy, int lane) {
@@ -401,182 +338,6 @@ __device__ __forceinline__ void sp3_flush(uint8_t *out, uint32_t *stage, uint64_
   const uint32_t used = (uint32_t)((ct + 15) >> 4) + 1;
   for (uint32_t i = threadIdx.x; i < used; i += kSpThreads) cl[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
-}
-
-// the decoupled look-back in two halves (wave 0): the nearest 256
-// predecessors' status words loaded ahead (issue), then evaluated and, if
-// some of them had not published, polled again (finish; sp_lookback's loop)
-struct Sp3Lb {
-  uint64_t v[4];
-};
-__device__ __forceinline__ void sp3_lb_issue(Sp3Lb &L, uint64_t *status, uint32_t p, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t idx = (int64_t)p - 1 - 4 * lane - i;
-    L.v[i] = ld_status(&status[idx >= 0 ? idx : 0]);
-  }
-}
-__device__ uint64_t sp3_lb_finish(const Sp3Lb &L, uint64_t *status, uint32_t p, uint64_t agg, uint32_t ep,
-                                  uint32_t *err, int lane) {
-  if (p == 0) {
-    return 0;
-  }
-  uint64_t excl = 0;
-  int64_t top = (int64_t)p - 1;
-  uint32_t spins = 0;
-  bool first = true;
-  for (;;) {
-    uint64_t v[4];
-    int fi = 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t idx = top - 4 * lane - i;
-      v[i] = idx < 0 ? sp_word(ep, 2u, 0) : first ? L.v[i] : ld_status(&status[idx]);
-    }
-    first = false;
-#pragma unroll
-    for (int i = 3; i >= 0; --i)
-      if (sp_flag(v[i], ep) == 2) fi = i;
-    const uint64_t has = __ballot(fi < 4);
-    const int fln = has ? __builtin_ctzll(has) : 64;
-    const int firstPos = fln < 64 ? 4 * fln + __builtin_amdgcn_readlane(fi, fln) : 256;
-    bool z = false;
-    uint64_t sum = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (4 * lane + i <= firstPos) {
-        z = z || sp_flag(v[i], ep) == 0;
-        sum += v[i] & kSpValMask;
-      }
-    }
-    if (__ballot(z)) {
-      if (++spins > (1u << 22)) {  // cannot happen: every predecessor is held by a running workgroup
-        if (lane == 0) atomicOr(err, 4u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
-    excl += sum;
-    if (firstPos < 256) break;
-    top -= 256;
-  }
-  if (lane == 0) st_status(&status[p], sp_word(ep, 2u, excl + agg));
-  return excl;
-}
-
-template <bool kMsg>
-__global__ __launch_bounds__(kSpThreads, 2) void sp3_encode_kernel(
-    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo,
-    const uint64_t *__restrict__ pdesc, const uint64_t *__restrict__ tin, uint32_t n,
-    uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status, uint32_t ep,
-    uint32_t *ticket, const uint64_t *__restrict__ utab, const uint64_t *__restrict__ nunits,
-    uint64_t *ustate, uint64_t hint, uint32_t *err, const uint64_t *ocapp, const uint32_t *pick, uint32_t mine) {
-  if (pick && (uint32_t)__builtin_amdgcn_readfirstlane((int)*pick) != mine) return;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint64_t ocap = kMsg ? *ocapp : 9 * (swo[n] - swo[0]) + n + 16;
-  uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kSp3oLut);
-  uint64_t *msk = reinterpret_cast<uint64_t *>(smem + kSp3oMsk);
-  uint64_t *scr = reinterpret_cast<uint64_t *>(smem + kSp3oScr);
-  uint32_t *stage = reinterpret_cast<uint32_t *>(smem + kSp3oStage);
-  const int lane0 = lane_id();
-  const int w = __builtin_amdgcn_readfirstlane(wave_id());
-  fill_luts(lut, false);
-  for (uint32_t i = threadIdx.x; i < kSp3Stage / 16; i += kSpThreads)
-    reinterpret_cast<uint4 *>(stage)[i] = make_uint4(0u, 0u, 0u, 0u);
-  SpRegs R;
-  R.zl = R.zh = R.dll = R.dlh = R.dl_ = R.dh_ = 0;
-  R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = 0;
-  const uint32_t nu = utab ? (uint32_t)*nunits : n;
-  const uint64_t *dummy = kMsg ? pdesc : swo;  // (a valid word for loads that are not used)
-  if (threadIdx.x == 0) {
-    scr[0] = atomicAdd(ticket, 1u);
-    scr[1] = atomicAdd(ticket, 1u);
-  }
-  __syncthreads();
-  uint32_t t = (uint32_t)sp_ld(&scr[0]), tn = (uint32_t)sp_ld(&scr[1]);
-  uint64_t V[kSpWS], N[kSpWS];
-  Sp3Unit cu = sp3_unit<kMsg>(t, nu, in, swo, pdesc, tin, utab, hint, w);
-  sp3_load(V, cu, dummy, lane0);
-  // the staged unit: its bytes are in the stage, its offset not yet known
-  bool sv = false;
-  uint32_t s_t = 0, s_p = 0;
-  bool s_first = false, s_end = false;
-  uint64_t s_ct = 0;
-  for (;;) {
-    if (t >= nu) break;
-    // an opaque copy of the lane id: nothing lane-dependent is hoisted out
-    // of the unit loop into registers that stay live across it
-    int lane = lane0;
-    asm volatile("" : "+v"(lane));
-    // ---- issued first, waited for in the order used: the ticket of the
-    // unit after next, the first probe of the entering state, the
-    // look-ahead words, the staged unit's look-back polls, the next unit's
-    // words (the in-order vmcnt lets each wait skip the loads behind it)
-    uint32_t tk = 0;
-    if (threadIdx.x == 0) tk = atomicAdd(ticket, 1u);
-    uint64_t pst = 0;
-    if (threadIdx.x == 0 && cu.c) pst = ld_status(ustate + (t - 1));
-    uint64_t LA[4];
-    sp3_la_load(LA, cu, dummy, lane);
-    Sp3Lb lb;
-    if (sv && w == 0) sp3_lb_issue(lb, status, s_t, lane);
-    const Sp3Unit nx = sp3_unit<kMsg>(tn, nu, in, swo, pdesc, tin, utab, hint, w);
-    sp3_load(N, nx, dummy, lane);
-    // ---- A of unit t
-    if ((cu.bad || cu.over) && threadIdx.x == 0 && cu.c == 0) atomicOr(err, 1u);
-    uint32_t Xlast = 0;
-    uint64_t wbefore = 0;
-    const uint64_t ct = sp3_chunk(R, V, LA, cu, msk, scr, pst, cu.c ? ustate + (t - 1) : nullptr,
-                                  cu.lastc ? nullptr : ustate + t, ep, err, w, lane, Xlast, wbefore);
-    if (w == 0 && lane == 0) st_status(&status[t], sp_word(ep, t == 0 ? 2u : 1u, ct));
-    // ---- the staged unit's offset, then its bytes out
-    if (sv) {
-      if (w == 0) {
-        const uint64_t excl = sp3_lb_finish(lb, status, s_t, s_ct, ep, err, lane);
-        if (lane == 0) {
-          scr[5] = excl;
-          if (s_first) out_off[s_p] = excl;
-          if (s_end) out_off[n] = excl + s_ct;
-        }
-      }
-      if (threadIdx.x == 0) scr[2] = tk;
-      __syncthreads();
-      sp3_flush(out, stage, sp_ld(&scr[5]), s_ct, ocap);
-    } else {
-      if (threadIdx.x == 0) scr[2] = tk;
-      __syncthreads();
-    }
-    // ---- B of unit t into the stage
-    if (cu.cnt) sp3_b(R, V, cu.cnt, lut, stage, (uint32_t)wbefore, lane);
-    sv = true;
-    s_t = t;
-    s_p = cu.p;
-    s_first = cu.c == 0;
-    s_end = cu.p + 1 == n && cu.lastc;
-    s_ct = ct;
-    t = tn;
-    tn = (uint32_t)sp_ld(&scr[2]);
-    cu = nx;
-#pragma unroll
-    for (int j = 0; j < kSpWS; ++j) V[j] = N[j];
-    __syncthreads();  // (the stage complete before the next flush; scr[2] read before it is rewritten)
-  }
-  if (sv) {
-    if (w == 0) {
-      Sp3Lb lb;
-      sp3_lb_issue(lb, status, s_t, lane0);
-      const uint64_t excl = sp3_lb_finish(lb, status, s_t, s_ct, ep, err, lane0);
-      if (lane0 == 0) {
-        scr[5] = excl;
-        if (s_first) out_off[s_p] = excl;
-        if (s_end) out_off[n] = excl + s_ct;
-      }
-    }
-    __syncthreads();
-    sp3_flush(out, stage, sp_ld(&scr[5]), s_ct, ocap);
-  }
 }
 
 // ------------------------------------------------------------ one workgroup

@@ -1262,7 +1262,13 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 }
 
 #include "encode_v4.hip"
+// the dense form's ring: 11 KiB per wave, the most three workgroups per CU
+// leave room for (round 4: config 2's ~7.7 KiB of output per wave overflowed
+// 8 KiB rings often enough that waves waited for their offset a third of
+// the time; 11 KiB: encode -11 %)
+#define CPK_SP_RING 11264
 #include "encode_sp.hip"
+#undef CPK_SP_RING
 #include "encode_sp3.hip"
 #include "decode_v2.hip"
 #include "stream_split.hip"
@@ -1315,7 +1321,6 @@ struct cpk_ctx_s {
   uint32_t *tickets;      // cpk::kTkWords words: per-XCD counters, plan ticket, error bits
   int encoder;            // 0: single pass (encode_sp.hip); 4: size + emit passes; 5: by piece size
   int sp_form;            // the single pass's form: 0 by density, 1 dense, 2 sparse (CPK_SP_FORM)
-  int sp_kernel;          // the dense form: 3 pipelined (encode_sp3.hip), 2 per unit (CPK_SP_KERNEL)
   int decoder;            // 2: record index (decode_v2.hip); 1: block map (decode_kernel); 3: by density
   uint64_t *sp_status;    // single pass: look-back word per piece
   uint64_t sp_cap;        //   entries
@@ -1426,8 +1431,6 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     // gate picks the single pass (A/B of the density threshold)
     const char *f = getenv("CPK_SP_FORM");
     c->sp_form = (f && f[0] == 'd') ? 1 : (f && f[0] == 's') ? 2 : 0;
-    const char *k = getenv("CPK_SP_KERNEL");
-    c->sp_kernel = (k && k[0] == '2') ? 2 : 3;
     // CPK_DECODER=1 selects the block-map decoder, 2 the record-index one
     const char *d = getenv("CPK_DECODER");
     c->decoder = (d && d[0] == '2') ? 2 : (d && d[0] == '1') ? 1 : 3;
@@ -1545,33 +1548,9 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
   }
   // (gated: both forms enqueued, the one the gate did not pick returns at once)
   const uint32_t *pick = gated ? ctx->tickets + cpk::kTkGate + 6 : nullptr;
-  if (ctx->sp_kernel == 3) {
-    static bool attr3 = false;
-    if (!attr3) {
-      hipFuncSetAttribute((const void *)cpk::sp3_encode_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)cpk::kSp3Lds);
-      hipFuncSetAttribute((const void *)cpk::sp3_encode_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)cpk::kSp3Lds);
-      attr3 = true;
-    }
-    unsigned g3 = (unsigned)(cpk::kSp3Wpe * ctx->cus);
-    if (g3 > ucap) g3 = (unsigned)ucap;
-    if (pdesc)
-      hipLaunchKernelGGL(cpk::sp3_encode_kernel<true>, dim3(g3), dim3(cpk::kSpThreads), cpk::kSp3Lds, s,
-                         (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
-                         ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
-                         ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr, pick, 0u);
-    else
-      hipLaunchKernelGGL(cpk::sp3_encode_kernel<false>, dim3(g3), dim3(cpk::kSpThreads), cpk::kSp3Lds, s,
-                         (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
-                         ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
-                         ctx->tickets + cpk::kTkErr, (const uint64_t *)nullptr, pick, 0u);
-  }
   unsigned grid = (unsigned)(cpk::kSpWpe * ctx->cus);
   if (grid > ucap) grid = (unsigned)ucap;
-  if (ctx->sp_kernel == 3) {
-    // (launched above)
-  } else if (pdesc)
+  if (pdesc)
     hipLaunchKernelGGL(cpk::sp_encode_kernel<true>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
                        ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
