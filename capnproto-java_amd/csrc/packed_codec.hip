@@ -434,7 +434,10 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
   if (sd.skip && __builtin_amdgcn_readfirstlane(*sd.skip)) return;
   fill_luts(lut, true);
   __syncthreads();  // the only block-wide barrier: LUT ready
-  int xq = xcc_id(), dry = 0;
+  // (one stream: its one ticket is item 0 of counter 0 -- start there, and
+  // a wave that does not get it leaves at once instead of trying the other
+  // seven counters one dependent atomic after another)
+  int xq = (kStream && sd.ns == 1) ? 0 : xcc_id(), dry = 0;
   WPH_INIT
   uint64_t scur = 0;      // stream mode: start of the next piece
   uint64_t slim = avail;  //   end of the stream's bytes
@@ -461,7 +464,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
         uint32_t j;
         for (;;) {
           j = take_ticket(ticket, xq);
-          if (j < sd.ns || ++dry >= 8) break;
+          if (j < sd.ns || ++dry >= 8 || sd.ns == 1) break;
           xq = (xq + 1) & 7;
         }
         if (j >= sd.ns) {
