@@ -876,7 +876,7 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
   }
   if (lane == 0) scr[16 + w] = bytes;
   __syncthreads();  // wave bytes in LDS
-  uint64_t tot = 0, wmax = 0;
+  uint64_t tot = 0;
   wbefore = 0;
   wmine = 0;
 #pragma unroll
@@ -884,13 +884,8 @@ __device__ __forceinline__ uint64_t sp_chunk(SpRegs &R, const uint64_t *__restri
     const uint64_t b = sp_ld(&scr[16 + q]);
     if (q < w) wbefore += b;
     if (q == w) wmine = b;
-    wmax = b > wmax ? b : wmax;
     tot += b;
   }
-  // wave 0 runs the unit's look-back: when any wave's output outgrows its
-  // ring, wave 0 asks for the offset early too (after kSpDefer steps), not
-  // after laying out all its own steps -- the overflowing wave waits on it
-  if (w == 0) wmine = wmax;
   return tot;
 }
 
