@@ -1093,12 +1093,22 @@ __device__ __forceinline__ void rm_final_body(const uint64_t *__restrict__ end, 
 // (decode_body<true>: one of the four waves finds the stream's ticket) and
 // the info row (rm_final_body), separated by workgroup barriers -- three
 // launches' dispatch latency saved on the small-message path
+// (dcopy, when set: the packed bytes -- pinned host memory -- are first
+// copied there by all threads at once, one PCIe round trip instead of one
+// per window of the one-wave walk; round_up(avail, 16) + 64 bytes)
 __global__ __launch_bounds__(kDecThreads, 1) void rm_small_kernel(
     const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit, uint64_t cap_words,
     uint64_t *__restrict__ swo, uint64_t *__restrict__ info, uint64_t *__restrict__ sdesc, uint32_t *tk,
     uint64_t *__restrict__ out, uint64_t *__restrict__ in_off, int32_t *__restrict__ pst,
-    uint64_t *__restrict__ send_out, uint64_t *__restrict__ mirror) {
+    uint64_t *__restrict__ send_out, uint64_t *__restrict__ mirror, uint8_t *__restrict__ dcopy) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  if (dcopy) {
+    const uint32_t lines = (uint32_t)((avail + 15) / 16) + 4;
+    for (uint32_t i = threadIdx.x; i < lines; i += blockDim.x)
+      reinterpret_cast<uint4 *>(dcopy)[i] = reinterpret_cast<const uint4 *>(packed)[i];
+    __syncthreads();
+    packed = dcopy;
+  }
   rm_table_body(packed, avail, limit, cap_words, swo, info, sdesc, tk, smem);
   __syncthreads();  // (the layout and the zeroed tickets before the decode)
   decode_body<true>(smem, packed, in_off, swo, kRmPieces, out, pst, tk, avail,
@@ -1337,6 +1347,7 @@ struct cpk_ctx_s {
   uint64_t ss_cap;        //   u64 entries
   uint64_t *rm_buf;       // cpk_read_message: piece word offsets | piece ends | statuses (lazy)
   uint64_t *fl_buf;       // cpk_decode_batch of a few large pieces: boundaries found [33] (lazy)
+  uint8_t *rm_copy;       // cpk_read_message_host, one-wave path: the packed bytes on the device (lazy)
   uint64_t *sp_units;     // single pass, pieces over one chunk: unit counts | starts | block sums | unit table
   uint64_t sp_units_cap;  //   u64 entries
 };
@@ -1466,6 +1477,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->ss_buf) hipFree(ctx->ss_buf);
   if (ctx->rm_buf) hipFree(ctx->rm_buf);
   if (ctx->fl_buf) hipFree(ctx->fl_buf);
+  if (ctx->rm_copy) hipFree(ctx->rm_copy);
   if (ctx->sp_units) hipFree(ctx->sp_units);
   pipe_destroy(ctx->pipe);
   free(ctx);
@@ -2029,9 +2041,16 @@ static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, 
   //  ~0.5 GB/s, the parallel path ~250 us of fixed cost: even at 64 KiB)
   const bool par = reach >= kRmSsMin && !getenv("CPK_STREAM_ONE_WAVE");
   if (!par && !dec_v2(ctx)) {
+    // (the host path's packed bytes are pinned host memory: copied to the
+    // device once, in the kernel)
+    uint8_t *dcopy = nullptr;
+    if (info_mirror && reach + 96 <= kRmSsMin + 128) {
+      if (!ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmSsMin + 128) != hipSuccess) return CPK_ENOMEM;
+      dcopy = ctx->rm_copy;
+    }
     hipLaunchKernelGGL(cpk::rm_small_kernel, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds, s,
                        (const uint8_t *)d_packed, avail, traversal_limit_words, out_cap_words, swo, d_info, sdesc,
-                       ctx->tickets + cpk::kTkDec, (uint64_t *)d_out, in_off, pst, send_out, info_mirror);
+                       ctx->tickets + cpk::kTkDec, (uint64_t *)d_out, in_off, pst, send_out, info_mirror, dcopy);
     return hip_ok(hipGetLastError());
   }
   hipLaunchKernelGGL(cpk::rm_table_kernel, dim3(1), dim3(64), 0, s, (const uint8_t *)d_packed, avail,
