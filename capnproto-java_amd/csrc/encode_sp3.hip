@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
                                                                  const uint64_t *__restrict__ desc, uint32_t n,
                                                                  uint8_t *__restrict__ out,
                                                                  uint64_t *__restrict__ out_off, uint64_t ocap,
-                                                                 uint32_t *err) {
+                                                                 uint32_t *err, uint64_t *flag, uint64_t seq) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kSp3oLut);
   uint64_t *msk = reinterpret_cast<uint64_t *>(smem + kSp3oMsk);
@@ -387,6 +387,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
   uint64_t *ldesc = reinterpret_cast<uint64_t *>(smem + kSp3Lds);
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  if (flag) small_begin();
   // the descriptors in LDS at once (they may be host memory: one round
   // trip, not two dependent ones per piece)
   for (uint32_t i = threadIdx.x; i < 2 * n; i += kSpThreads) ldesc[i] = desc[i];
@@ -422,4 +423,5 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
     }
   }
   if (threadIdx.x == 0) out_off[n] = g;
+  if (flag) small_done(flag, seq);
 }

@@ -195,12 +195,13 @@ int small_encode(cpk_ctx ctx, uint64_t np, uint64_t words, Lay lay, void *h_out,
                  uint64_t *h_out_off, uint64_t off_base) {
   HostPipe *p = nullptr;
   const uint64_t ocap = 9 * words + np + 16;
-  // meta: desc [2 np] | out_off [np + 1]
-  int rc = pipe_get(ctx, 8 * words + 64, ocap + 64, 3 * np + 1, &p, 1);
+  // meta: desc [2 np] | out_off [np + 1] | completion flag
+  int rc = pipe_get(ctx, 8 * words + 64, ocap + 64, 3 * np + 2, &p, 1);
   if (rc) return rc;
   HostSlot &s = p->slot[0];
   uint64_t *desc = s.pin_meta, *off = desc + 2 * np;
   lay((uint64_t *)s.pin_in, desc);
+  const uint64_t seq = small_arm(ctx, off + np + 1);
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void *)cpk::sp_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -209,8 +210,8 @@ int small_encode(cpk_ctx ctx, uint64_t np, uint64_t words, Lay lay, void *h_out,
   }
   hipLaunchKernelGGL(cpk::sp_small_kernel, dim3(1), dim3(cpk::kSpThreads), cpk::kSpSmallLds, p->sk,
                      (const uint64_t *)s.pin_in, (const uint64_t *)desc, (uint32_t)np, (uint8_t *)s.pin_out, off,
-                     ocap, ctx->tickets + cpk::kTkErr);
-  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p->sk) != hipSuccess) return CPK_EDEVICE;
+                     ocap, ctx->tickets + cpk::kTkErr, off + np + 1, seq);
+  if (hipGetLastError() != hipSuccess || small_wait(p->sk, off + np + 1, seq)) return CPK_EDEVICE;
   const uint64_t P = off[np];
   if (P > ocap) return CPK_EDEVICE;
   if (P > h_out_cap) return CPK_ENOMEM;

@@ -31,6 +31,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -894,11 +895,18 @@ __device__ int serial_read(const uint8_t *p, uint64_t n, uint64_t &ip, uint32_t 
 
 // the table of message m: status, segment count, total words; on OK the
 // packed position after the table.  emit(i, size) per segment.
-template <class F>
+struct NoWords {
+  __device__ void operator()(uint32_t, uint64_t) const {}
+};
+// (word(i, w): the table's words as read, i = 0 the first)
+template <class F, class G = NoWords>
 __device__ int read_table(const uint8_t *p, uint64_t n, uint64_t limit, uint64_t &ip,
-                          uint32_t &count, uint64_t &total, F emit) {
+                          uint32_t &count, uint64_t &total, F emit, G word = G()) {
   uint64_t first = 0;
-  int st = serial_read(p, n, ip, 1, [&](uint32_t, uint64_t w) { first = w; });
+  int st = serial_read(p, n, ip, 1, [&](uint32_t, uint64_t w) {
+    first = w;
+    word(0u, w);
+  });
   if (st) return st;
   const int32_t raw = (int32_t)(uint32_t)first;
   if (raw < 0 || raw > 511) return CPK_EFRAME;  // Serialize.java:128-131
@@ -911,6 +919,7 @@ __device__ int read_table(const uint8_t *p, uint64_t n, uint64_t limit, uint64_t
   if (count > 1) {  // :144-157
     const uint32_t c = count;
     st = serial_read(p, n, ip, (count & ~1u) / 2, [&](uint32_t i, uint64_t w) {
+      word(1u + i, w);
       for (uint32_t h = 0; h < 2; ++h) {
         const uint32_t k = 2 * i + h;  // moreSizes[k] = segment k + 1
         if (k + 1 < c) {
@@ -981,6 +990,20 @@ __global__ void msg_final_kernel(const uint64_t *__restrict__ moff, uint32_t nm,
   mstatus[m] = st != CPK_OK ? st : (mend[m] != moff[m + 1] ? CPK_ETRAILING : CPK_OK);
 }
 
+// The one-launch small paths' completion flag: once every wave's writes
+// (pinned host memory included) are complete at system scope, seq goes to
+// *flag -- host memory the caller spins on instead of a stream
+// synchronisation (small_wait)
+__device__ __forceinline__ void small_done(uint64_t *flag, uint64_t seq) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// ... and its start: with no stream synchronisation between two calls the
+// launch's own acquire may stop at device scope, so lines of the pinned
+// input an earlier call read could still sit in L2: dropped here
+__device__ __forceinline__ void small_begin() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+
 // ---- one message from the front of a stream (cpk_read_message) -------------
 // Serialize.read over PackedInputStream (Serialize.java:119-178) when the
 // message's packed length is unknown: the table is read here, laid out as the
@@ -999,14 +1022,24 @@ constexpr uint32_t kRmInfo = 4 + 513;          // status, consumed, count, words
 // parallel path's piece count
 // (dec_tk: the batch decoder's ticket counters, zeroed here for the one-wave
 // decode launched next -- one command fewer than a memset)
+// (out, when set -- the one-launch path: the parse's own table words are
+// written there and the stream descriptor starts at the first segment, so
+// the decoder walks the segments only; otherwise the swo of the padding
+// pieces is filled by all threads)
 constexpr uint32_t kRmTableBytes = 2576;  // a table's packed bytes at most (257 words: 2,570)
+struct RmScratch {
+  uint32_t size[512];  // the segments' sizes as the parse reads them
+  uint64_t fill[2];    // swo padding: first index, value
+};
+static_assert(kRmTableBytes % 16 == 0 && kRmTableBytes + sizeof(RmScratch) <= kDecLds, "rm_small_kernel LDS");
 __device__ void rm_table_parse(const uint8_t *tb, uint64_t nt, uint64_t avail, uint64_t limit, uint64_t cap_words,
                                uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
-                               uint64_t *__restrict__ sdesc);
+                               uint64_t *__restrict__ sdesc, uint64_t *__restrict__ out, RmScratch &rs);
 __device__ __forceinline__ void rm_table_body(const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit,
                                               uint64_t cap_words, uint64_t *__restrict__ swo,
                                               uint64_t *__restrict__ info, uint64_t *__restrict__ sdesc,
-                                              uint32_t *__restrict__ dec_tk, uint8_t *tb) {
+                                              uint32_t *__restrict__ dec_tk, uint8_t *tb, RmScratch &rs,
+                                              uint64_t *__restrict__ out) {
   if (dec_tk)
     for (uint32_t i = threadIdx.x; i < 8 * kTkStride; i += blockDim.x) dec_tk[i] = 0;
   // the bytes a table can reach staged in LDS (tb) by whole 16-byte lines
@@ -1017,24 +1050,32 @@ __device__ __forceinline__ void rm_table_body(const uint8_t *__restrict__ packed
   for (uint32_t i = threadIdx.x; i < (uint32_t)((nt + 15) / 16); i += blockDim.x)
     reinterpret_cast<uint4 *>(tb)[i] = reinterpret_cast<const uint4 *>(packed)[i];
   __syncthreads();
-  if (threadIdx.x == 0) rm_table_parse(tb, nt, avail, limit, cap_words, swo, info, sdesc);
+  if (threadIdx.x == 0) rm_table_parse(tb, nt, avail, limit, cap_words, swo, info, sdesc, out, rs);
+  if (out) return;
+  __syncthreads();
+  const uint32_t f0 = (uint32_t)rs.fill[0];
+  const uint64_t fv = rs.fill[1];
+  for (uint32_t i = f0 + threadIdx.x; i <= kRmPieces; i += blockDim.x) swo[i] = fv;
 }
 __global__ void rm_table_kernel(const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit,
                                 uint64_t cap_words, uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
                                 uint64_t *__restrict__ sdesc, uint32_t *__restrict__ dec_tk) {
   __shared__ __attribute__((aligned(16))) uint8_t tb[kRmTableBytes];
-  rm_table_body(packed, avail, limit, cap_words, swo, info, sdesc, dec_tk, tb);
+  __shared__ RmScratch rs;
+  rm_table_body(packed, avail, limit, cap_words, swo, info, sdesc, dec_tk, tb, rs, nullptr);
 }
 // (one thread) the table read and checked as doRead does, the message laid
 // out as the stream's pieces
 __device__ void rm_table_parse(const uint8_t *tb, uint64_t nt, uint64_t avail, uint64_t limit, uint64_t cap_words,
                                uint64_t *__restrict__ swo, uint64_t *__restrict__ info,
-                               uint64_t *__restrict__ sdesc) {
+                               uint64_t *__restrict__ sdesc, uint64_t *__restrict__ out, RmScratch &rs) {
   uint64_t ip = 0, total = 0;
   uint32_t count = 0;
-  // sizes parked in the info row (offsets written over them below)
-  int st = read_table(tb, nt, limit, ip, count, total,
-                      [&](uint32_t i, uint32_t sz) { info[5 + i] = sz; });
+  int st = read_table(
+      tb, nt, limit, ip, count, total, [&](uint32_t i, uint32_t sz) { rs.size[i] = sz; },
+      [&](uint32_t i, uint64_t w) {
+        if (out) out[i] = w;
+      });
   if (st == CPK_OK && total > cap_words) st = CPK_ENOMEM;
   info[0] = (uint64_t)(int64_t)st;
   info[1] = 0;
@@ -1046,19 +1087,21 @@ __device__ void rm_table_parse(const uint8_t *tb, uint64_t nt, uint64_t avail, u
     swo[1] = w = 1;
     swo[2] = w += (count & ~1u) / 2;
     for (uint32_t i = 0; i < count; ++i) {
-      const uint64_t sz = info[5 + i];
       info[4 + i] = w;
-      swo[3 + i] = w += sz;
+      swo[3 + i] = w += rs.size[i];
     }
     info[4 + count] = w;
   } else {
     swo[1] = swo[2] = 0;
   }
-  for (uint32_t i = (st == CPK_OK ? count : 0) + 3; i <= kRmPieces; ++i) swo[i] = w;
-  sdesc[0] = 0;
+  rs.fill[0] = (st == CPK_OK ? count : 0) + 3;
+  rs.fill[1] = w;
+  const bool go = st == CPK_OK;
+  // (out: the segments' stream starts where the table's bytes end)
+  sdesc[0] = out && go ? ip : 0;
   sdesc[1] = avail;
-  sdesc[2] = 0;
-  sdesc[3] = st == CPK_OK ? count + 2 : 0;
+  sdesc[2] = out && go ? 2 : 0;
+  sdesc[3] = go ? count + 2 : 0;
   sdesc[5] = kRmPieces;  // (the parallel path decodes every piece)
 }
 
@@ -1089,7 +1132,8 @@ __device__ __forceinline__ void rm_final_body(const uint64_t *__restrict__ end, 
 }
 
 // cpk_read_message whole in ONE launch when the one-wave decoder takes the
-// message: the table (rm_table_body), the stream of its pieces
+// message: the table (rm_table_body, which also writes the table's words),
+// the stream of its segments from where the table's bytes end
 // (decode_body<true>: one of the four waves finds the stream's ticket) and
 // the info row (rm_final_body), separated by workgroup barriers -- three
 // launches' dispatch latency saved on the small-message path
@@ -1100,8 +1144,9 @@ __global__ __launch_bounds__(kDecThreads, 1) void rm_small_kernel(
     const uint8_t *__restrict__ packed, uint64_t avail, uint64_t limit, uint64_t cap_words,
     uint64_t *__restrict__ swo, uint64_t *__restrict__ info, uint64_t *__restrict__ sdesc, uint32_t *tk,
     uint64_t *__restrict__ out, uint64_t *__restrict__ in_off, int32_t *__restrict__ pst,
-    uint64_t *__restrict__ send_out, uint64_t *__restrict__ mirror, uint8_t *__restrict__ dcopy) {
+    uint64_t *__restrict__ send_out, uint64_t *__restrict__ mirror, uint8_t *__restrict__ dcopy, uint64_t seq) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  if (mirror) small_begin();
   if (dcopy) {
     const uint32_t lines = (uint32_t)((avail + 15) / 16) + 4;
     for (uint32_t i = threadIdx.x; i < lines; i += blockDim.x)
@@ -1109,12 +1154,14 @@ __global__ __launch_bounds__(kDecThreads, 1) void rm_small_kernel(
     __syncthreads();
     packed = dcopy;
   }
-  rm_table_body(packed, avail, limit, cap_words, swo, info, sdesc, tk, smem);
+  rm_table_body(packed, avail, limit, cap_words, swo, info, sdesc, tk, smem,
+                *reinterpret_cast<RmScratch *>(smem + kRmTableBytes), out);
   __syncthreads();  // (the layout and the zeroed tickets before the decode)
   decode_body<true>(smem, packed, in_off, swo, kRmPieces, out, pst, tk, avail,
                     DecStreams{sdesc, sdesc + 1, sdesc + 2, 1, send_out, nullptr});
   __syncthreads();  // (the stream's end and statuses before the fold)
   rm_final_body(send_out, pst, sdesc + 3, info, mirror);
+  if (mirror) small_done(mirror + kRmInfo, seq);
 }
 
 // ---- message write: Serialize.write = table piece + segment pieces --------
@@ -1348,6 +1395,7 @@ struct cpk_ctx_s {
   uint64_t *rm_buf;       // cpk_read_message: piece word offsets | piece ends | statuses (lazy)
   uint64_t *fl_buf;       // cpk_decode_batch of a few large pieces: boundaries found [33] (lazy)
   uint8_t *rm_copy;       // cpk_read_message_host, one-wave path: the packed bytes on the device (lazy)
+  uint64_t small_seq;     // the one-launch host paths' completion flag values (small_wait)
   uint64_t *sp_units;     // single pass, pieces over one chunk: unit counts | starts | block sums | unit table
   uint64_t sp_units_cap;  //   u64 entries
 };
@@ -1384,6 +1432,31 @@ int ensure_status(cpk_ctx ctx, uint64_t n) {
 
 static int decode_batch_impl(cpk_ctx ctx, const void *d_packed, const uint64_t *d_in_off, const uint64_t *d_swo,
                              uint32_t n, void *d_out, int32_t *d_status, void *stream, bool probe);
+
+// The end of a one-launch small path (rm_small_kernel, sp_small_kernel):
+// its kernel writes seq to *flag (pinned host memory) after all its other
+// writes, so the host reads its results once the flag turns -- without the
+// stream synchronisation's wait for the kernel's completion signal.  Past a
+// bound (the kernel is slow or faulted) the stream synchronisation decides.
+// Returns 0 or nonzero like hipStreamSynchronize.
+// The flag word is cleared by small_arm before the launch (it is pinned
+// memory other calls use for other data) and its values carry a tag no
+// offset or size the slot held can equal.
+constexpr uint64_t kSmallTag = 0x5ea1ull << 48;
+static uint64_t small_arm(cpk_ctx ctx, uint64_t *flag) {
+  __atomic_store_n(flag, 0ull, __ATOMIC_RELEASE);
+  return kSmallTag | (++ctx->small_seq & ((1ull << 48) - 1));
+}
+static int small_wait(hipStream_t s, const uint64_t *flag, uint64_t seq) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1;; ++i) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
+    __builtin_ia32_pause();
+    if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return 1;
+  return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
+}
 #include "host_pipe.hip"
 
 extern "C" {
@@ -2006,7 +2079,7 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
 }  // extern "C"
 static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t traversal_limit_words,
                              void *d_out, uint64_t out_cap_words, uint64_t *d_info, void *stream,
-                             uint64_t *info_mirror);
+                             uint64_t *info_mirror, uint64_t seq = 0, bool *flagged = nullptr);
 extern "C" {
 int cpk_read_message(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t traversal_limit_words,
                      void *d_out, uint64_t out_cap_words, uint64_t *d_info, void *stream) {
@@ -2016,10 +2089,13 @@ int cpk_read_message(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t
 }  // extern "C"
 
 // (info_mirror: where rm_final_kernel also copies the info row, e.g. pinned
-// host memory read after one sync; d_info null: a device row in rm_buf)
+// host memory read after one sync; d_info null: a device row in rm_buf;
+// *flagged set: the one-launch kernel took it and writes seq to
+// info_mirror[kRmInfo] when done)
 static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, uint64_t traversal_limit_words,
                              void *d_out, uint64_t out_cap_words, uint64_t *d_info, void *stream,
-                             uint64_t *info_mirror) {
+                             uint64_t *info_mirror, uint64_t seq, bool *flagged) {
+  if (flagged) *flagged = false;
   using cpk::kRmPieces;
   if (!ctx || (!d_info && !info_mirror) || (avail && !d_packed) || !d_out) return CPK_EINVAL;
   if (((uintptr_t)d_packed & 15) || ((uintptr_t)d_out & 7)) return CPK_EINVAL;
@@ -2050,7 +2126,9 @@ static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, 
     }
     hipLaunchKernelGGL(cpk::rm_small_kernel, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds, s,
                        (const uint8_t *)d_packed, avail, traversal_limit_words, out_cap_words, swo, d_info, sdesc,
-                       ctx->tickets + cpk::kTkDec, (uint64_t *)d_out, in_off, pst, send_out, info_mirror, dcopy);
+                       ctx->tickets + cpk::kTkDec, (uint64_t *)d_out, in_off, pst, send_out, info_mirror, dcopy,
+                       seq);
+    if (flagged) *flagged = info_mirror != nullptr;
     return hip_ok(hipGetLastError());
   }
   hipLaunchKernelGGL(cpk::rm_table_kernel, dim3(1), dim3(64), 0, s, (const uint8_t *)d_packed, avail,
@@ -2192,7 +2270,7 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   // `avail` may be later messages)
   const uint64_t R = ss_reach(avail, out_cap_words + cpk::kRmHead);
   HostPipe *p = nullptr;
-  int rc = pipe_get(ctx, R, (out_cap_words + cpk::kRmHead) * 8, kRmInfo, &p, 1);
+  int rc = pipe_get(ctx, R, (out_cap_words + cpk::kRmHead) * 8, kRmInfo + 1, &p, 1);
   if (rc) return rc;
   HostSlot &sl = p->slot[0];
   uint64_t *info = sl.pin_meta;
@@ -2202,13 +2280,15 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
     // -- no DMA either way, one sync
     memcpy(sl.pin_in, h_packed, R);
     memset((uint8_t *)sl.pin_in + R, 0, 64);
+    const uint64_t seq = small_arm(ctx, info + kRmInfo);
+    bool flagged = false;
     rc = read_message_impl(ctx, sl.pin_in, R, traversal_limit_words, sl.pin_out, out_cap_words, nullptr, p->sk,
-                           info);
+                           info, seq, &flagged);
     if (rc) {
       pipe_drain(p);
       return rc;
     }
-    if (hipStreamSynchronize(p->sk)) return CPK_EDEVICE;
+    if (flagged ? small_wait(p->sk, info + kRmInfo, seq) : hipStreamSynchronize(p->sk)) return CPK_EDEVICE;
     const int st = (int)(int64_t)info[0];
     const uint32_t count = (uint32_t)info[2];
     for (int i = 0; i < 4; ++i) h_info[i] = info[i];

@@ -170,3 +170,20 @@ def test_read_message_device_form(ctx, oracle):
     out = d_out.cpu().numpy().view(np.uint8)
     got = [out[8 * int(info[4 + i]): 8 * int(info[5 + i])].tobytes() for i in range(4)]
     assert got == segs
+
+
+def test_small_host_paths_back_to_back(ctx, oracle):
+    """The one-launch host paths (read and write under 64 KiB) return once
+    their kernel's completion flag turns, with no stream synchronisation:
+    back-to-back calls whose pinned input changes every time must each see
+    their own bytes (a kernel must not read lines an earlier call left in
+    L2) and hand back their own results."""
+    rng = np.random.default_rng(13)
+    msgs = [_msg(rng, oracle, [int(x) for x in rng.integers(1, 600, size=int(rng.integers(1, 4)))])
+            for _ in range(6)]
+    for k in range(300):
+        segs, pk = msgs[k % len(msgs)]
+        st, got, used, _ = _rd(ctx, pk)
+        assert st == 0 and got == segs and used == len(pk), k
+        packed, _ = ctx.encode_messages_host([segs])
+        assert bytes(packed) == pk, k
