@@ -406,6 +406,297 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
+// (stats build: the window phases' clock sums live in the caller)
+#ifdef CPK_PHASE_STATS
+#define DEC_PH_PARAMS , unsigned long long &wph_last, unsigned long long *wph_acc
+#define DEC_PH_ARGS , wph_last, wph_acc
+#else
+#define DEC_PH_PARAMS
+#define DEC_PH_ARGS
+#endif
+// ---- 1-3 of a window [e, wend) (decode_body; decode_piece_mw): lane l
+// walks its chunk [cb, cb + kDecChunk) from cb as if a tag stood there (the
+// visited positions into visa[l], its words wt, its exit X), then on until it
+// lands on a position some lane visited -- from there the two walks coincide,
+// the chain being a function of the position -- (S, its words lw); R: the
+// lanes reachable from l under "lane -> owner of its landing point" (always a
+// later lane), by pointer doubling (6 rounds cover a chain of 64).  Nothing
+// here depends on where the window's true records start.
+struct WinWalk {
+  uint32_t cb, S, wt, lw;
+  uint64_t R;
+};
+__device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, int lane, uint32_t e,
+                                             uint32_t wend DEC_PH_PARAMS) {
+  // ---- 1: speculative chunk walks --------------------------------------
+  const uint32_t cb = e + kDecChunk * lane;
+  const uint32_t ce = min(cb + kDecChunk, wend);
+  VisMask vis = 0;
+  uint32_t X = cb, wt = 0;  // wt: output words of the walk
+  if (cb < wend) {
+    uint32_t pos = cb;
+    while (pos < ce) {
+      vis |= (VisMask)1 << (pos - cb);
+      const DecRec r = rec_at(pkw, pos);
+      wt += r.nw;
+      pos += r.len;
+    }
+    X = pos;
+  }
+  visa[lane] = vis;
+  wave_lds_order();
+  // ---- 2: walk on until landing on a visited position -------------------
+  uint32_t S = X, lw = 0;  // lw: output words of the landing walk
+  if (cb < wend) {
+    while (S < wend) {
+      const uint32_t r = S - e;
+      const uint32_t ow_ = chunk_div<kDecChunk>(r);
+      uint32_t base = __umul24(ow_, kDecChunk);
+      asm("" : "+v"(base));  // (else folded into a quarter-rate v_mad_u64_u32)
+      if ((visa[ow_] >> (r - base)) & 1) break;
+      const DecRec rr = rec_at(pkw, S);
+      lw += rr.nw;
+      S += rr.len;
+    }
+  }
+  WPH(2)
+  // ---- 3: reachability over lanes --------------------------------------
+  int nx = (cb < wend && S < wend) ? (int)chunk_div<kDecChunk>(S - e) : 64;
+  uint64_t R = 1ull << lane;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int src = (nx & 63) << 2;
+    const uint32_t rlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)R);
+    const uint32_t rhi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(R >> 32));
+    const int nn = __builtin_amdgcn_ds_bpermute(src, nx);
+    if (nx < 64) {
+      R |= ((uint64_t)rhi << 32) | rlo;
+      nx = nn;
+    }
+  }
+  WinWalk ww;
+  ww.cb = cb;
+  ww.S = S;
+  ww.wt = wt;
+  ww.lw = lw;
+  ww.R = R;
+  return ww;
+}
+
+// ---- 5: error checks, block map, expansion (rounds of kRound words) of a
+// window whose true records are known: an on-path lane holds the records
+// [entry, S), the first at window word o0 (myw words); T words in all, the
+// window's first record at piece position e, ow piece words before it
+// (decode_body; decode_piece_mw).  Returns false when a record fails (st
+// set); fin: the end of the record that fills the piece, else 0.
+template <bool kStream>
+__device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut, uint32_t *blk, int lane,
+                                         uint32_t e, int ow, int W, uint32_t P, int T, bool on,
+                                         uint32_t entry, uint32_t S, uint64_t onmask, int o0, int myw,
+                                         uint32_t enext, uint32_t lend, const uint8_t *gp, uint32_t glim,
+                                         uint32_t ph, uint64_t *dst, int &st, uint32_t &fin DEC_PH_PARAMS) {
+  bool failed = false;
+  fin = 0;
+  // errors and the filling record can only occur in a window reaching the
+  // piece's last word or within one window plus one record of its end
+  // (the window's records start before e + kWin; the longest record, a
+  // 0xFF tag with its word, count and 255 words, is 2,050 bytes)
+  const bool chk = (ow + T >= W) || (P - e < kDecChkReach);
+  for (int rb = 0; rb < T; rb += kRound) {
+    int err = 0x7fffffff;
+    wave_lds_order();  // (the visited masks / last round's map reads are done)
+#pragma unroll
+    for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = 0u;
+    wave_lds_order();
+    // after the first round only the lanes whose output meets this round
+    if (!(chk && rb == 0)) {
+      // no record here can fail or fill the piece: the map alone
+      if (rb == 0) {
+        // round 0 (usually the window's only one): every record's output
+        // is at or past the round's start, so it always marks a block
+        if (on) {
+          uint32_t rel = (uint32_t)o0;
+          for (uint32_t q = entry; q < S && rel <= (uint32_t)(kRound - kBlk);) {
+            const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+            const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+            atomicMax(&blk[(rel + kBlk - 1) / kBlk], ((rel + 256u) << 12) | (q - e));
+            rel += 1u + (zm & c1) + (fm & c9);
+            q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
+          }
+        }
+      } else
+      if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
+        int rel = o0 - rb;  // round-relative output of the record (> -256 when live)
+        // (records past the round's last block start mark nothing, nor
+        // do the ones after them)
+        for (uint32_t q = entry; q < S && rel <= kRound - kBlk;) {
+          const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+          const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+          const int nw = 1 + (int)((zm & c1) + (fm & c9));
+          if (rel + nw > 0)
+            atomicMax(&blk[(max(rel, 0) + kBlk - 1) / kBlk], ((uint32_t)(rel + 256) << 12) | (q - e));
+          rel += nw;
+          q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
+        }
+      }
+    } else
+    {
+      // round 0 of a window near the piece's end.  Only two records can
+      // fail or fill the piece: the one whose words reach word W (when the
+      // window gets there; the reference stops reading after it), else the
+      // window's last record (the only one whose bytes can pass P: every
+      // other record ends where the next begins, before wend <= P).  The
+      // map walk notes them; one lane then runs the reference's checks
+      // on its record (PackedInputStream.java:53-138).
+      uint32_t qc = 0xffffffffu;
+      int oc = 0;
+      if (on) {
+        const int wr = W - ow;  // words left in the piece (> 0)
+        uint32_t ql = entry;
+        int o = o0, ol = o0;
+        for (uint32_t q = entry; q < S;) {
+          const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+          const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+          const int nw = 1 + (int)((zm & c1) + (fm & c9));
+          const int idx = (o + kBlk - 1) / kBlk;  // (round 0: o >= 0)
+          if (idx < kRound / kBlk) atomicMax(&blk[idx], ((uint32_t)(o + 256) << 12) | (q - e));
+          if (o < wr && o + nw >= wr) {
+            qc = q;
+            oc = o;
+          }
+          ql = q;
+          ol = o;
+          o += nw;
+          q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
+        }
+        if (ow + T < W && lane == 63 - __builtin_clzll(onmask)) {
+          qc = ql;
+          oc = ol;
+        }
+      }
+      if (qc != 0xffffffffu) {
+        const uint32_t q = qc;
+        const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+        const uint32_t ntag = 1 + __builtin_popcount(tag);
+        const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+        const int nw = 1 + (int)((zm & c1) + (fm & c9));
+        const uint32_t adv = ntag + (zm & 1u) + (fm & (8u * c9 + 1u));
+        const int oo = ow + oc;
+        // truncated tag bytes / count / literal run -> EOF DecodeException;
+        // run past the piece -> DecodeException / BufferOverflowException
+        int code = 0;
+        if (q + ntag > P) code = 2;
+        else if (tag == 0 || tag == 0xffu) {
+          if (q + (tag ? 10u : 2u) > P) code = 2;
+          else if (oo + nw > W) code = 3;
+          else if (q + adv > P) code = 2;
+        }
+        if (!kStream && !code && oo + nw == W && q + adv < P) code = 4;
+        if (code) err = (int)(((q - e) << 3) | (uint32_t)code);
+        if (oo + nw == W) fin = q + adv;
+      }
+    }
+    if (rb == 0) {
+      err = __builtin_amdgcn_readfirstlane(wave_min(err));
+      if (err != 0x7fffffff) {
+        st = -(err & 7);
+        failed = true;
+        break;
+      }
+      fin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u(fin));
+    }
+    wave_lds_order();
+    {
+      // prefix max: lane l holds blocks [kMapPer * l, kMapPer * (l + 1))
+      uint32_t m[kMapPer];
+      int run = 0;
+#pragma unroll
+      for (int i = 0; i < kMapPer; ++i) {
+        run = max(run, (int)blk[lane * kMapPer + i]);
+        m[i] = (uint32_t)run;
+      }
+      const uint32_t pre = (uint32_t)wave_shr1(wave_incl_max(run), 0);
+#pragma unroll
+      for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = max(m[i], pre);
+    }
+    wave_lds_order();
+    WPH(5)
+    const int nb = (min(min(kRound, T - rb), W - ow - rb) + kBlk - 1) / kBlk;
+    // two copies of the expansion: one for windows whose records all lie
+    // in the loaded bytes (enext + 12 <= lend: the usual case), whose
+    // reads need no bound check and no memory path
+    auto expand = [&](auto allin) __attribute__((always_inline)) {
+    constexpr bool kAllIn = decltype(allin)::value;
+    for (int b = lane; b < nb; b += 64) {
+      const uint32_t v = blk[b];
+      uint32_t q = e + (v & 0xfffu);
+      int ofs = kBlk * b + 256 - (int)(v >> 12);
+      const int wbase = ow + rb + kBlk * b;  // piece word of the block's first word
+      const int wleft = ow + T - wbase - 1;   // words of the window after the block's first
+      uint64_t words[kBlk];
+#pragma unroll
+      for (int i = 0; i < kBlk; ++i) {
+        // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
+        // run (tag word, then the counted words), or a tagged word
+        // (the count bytes are read with the tag: one LDS round trip)
+        uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+        uint64_t x;
+        int nw;
+        uint32_t adv;
+        if (tag == 0) {
+          x = 0;
+          nw = 1 + c1;
+          adv = 2;
+        } else if (tag == 0xffu) {
+          const uint32_t rn = c9;
+          nw = 1 + (int)rn;
+          adv = 10 + 8 * rn;
+          x = read8<kAllIn>(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
+        } else {
+          const uint64_t raw = read8<kAllIn>(pkw, q + 1, lend, gp, glim, ph, e);
+          const uint64_t sel = lut[tag];
+          const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
+          const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
+          const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
+          x = (uint64_t)x0 | ((uint64_t)x1 << 32);
+          nw = 1;
+          adv = 1 + __builtin_popcount(tag);
+        }
+        words[i] = x;
+        // past the window's last word: stay put (never stored)
+        if (++ofs == nw && i < wleft) {
+          q += adv;
+          ofs = 0;
+        }
+      }
+      const int kw = min(kBlk, min(ow + T, W) - wbase);
+      uint64_t *d = dst + wbase;
+      if (kw == kBlk && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
+#pragma unroll
+        for (int i = 0; i < kBlk; i += 2) {
+          uint4 v4;
+          v4.x = (uint32_t)words[i];
+          v4.y = (uint32_t)(words[i] >> 32);
+          v4.z = (uint32_t)words[i + 1];
+          v4.w = (uint32_t)(words[i + 1] >> 32);
+          st_stream(v4, d + i);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kBlk; ++i)
+          if (i < kw) d[i] = words[i];
+      }
+    }
+    };
+    if (enext + 12 <= lend) expand(std::true_type{});
+    else
+      expand(std::false_type{});
+    wave_lds_order();  // blk reused by the next round
+    WPH(6)
+  }
+  return !failed;
+}
+
 // kStream = false: piece i's packed bytes are [in_off[i], in_off[i+1]) and a
 //   piece that fills before its range ends is CPK_ETRAILING.
 // kStream = true: packed streams, each a wave's: the pieces of stream j,
@@ -543,55 +834,10 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       wave_lds_order();
 
       WPH(1)
-      // ---- 1: speculative chunk walks --------------------------------------
-      const uint32_t cb = e + kDecChunk * lane;
-      const uint32_t ce = min(cb + kDecChunk, wend);
-      VisMask vis = 0;
-      uint32_t X = cb, wt = 0;  // wt: output words of the walk
-      if (cb < wend) {
-        uint32_t pos = cb;
-        while (pos < ce) {
-          vis |= (VisMask)1 << (pos - cb);
-          const DecRec r = rec_at(pkw, pos);
-          wt += r.nw;
-          pos += r.len;
-        }
-        X = pos;
-      }
-      visa[lane] = vis;
-      wave_lds_order();
-      // ---- 2: walk on until landing on a visited position -------------------
-      uint32_t S = X, lw = 0;  // lw: output words of the landing walk
-      if (cb < wend) {
-        while (S < wend) {
-          const uint32_t r = S - e;
-          const uint32_t ow_ = chunk_div<kDecChunk>(r);
-          uint32_t base = __umul24(ow_, kDecChunk);
-          asm("" : "+v"(base));  // (else folded into a quarter-rate v_mad_u64_u32)
-          if ((visa[ow_] >> (r - base)) & 1) break;
-          const DecRec rr = rec_at(pkw, S);
-          lw += rr.nw;
-          S += rr.len;
-        }
-      }
-      WPH(2)
-      // ---- 3: true chain over lanes -----------------------------------------
-      // lane j's successor is the owner of its landing point (always a later
-      // lane); the true records are on the lanes reachable from lane 0, found
-      // by pointer doubling (6 rounds cover a chain of 64)
-      int nx = (cb < wend && S < wend) ? (int)chunk_div<kDecChunk>(S - e) : 64;
-      uint64_t R = 1ull << lane;
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        const int src = (nx & 63) << 2;
-        const uint32_t rlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)R);
-        const uint32_t rhi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(R >> 32));
-        const int nn = __builtin_amdgcn_ds_bpermute(src, nx);
-        if (nx < 64) {
-          R |= ((uint64_t)rhi << 32) | rlo;
-          nx = nn;
-        }
-      }
+      // ---- 1-3: speculative walks, chain reachability ------------------------
+      const WinWalk ww = win_walks(pkw, visa, lane, e, wend DEC_PH_ARGS);
+      const uint32_t cb = ww.cb, wt = ww.wt, lw = ww.lw, S = ww.S;
+      const uint64_t R = ww.R;
       const uint64_t onmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)R, 0)) |
                               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(R >> 32), 0) << 32);
       const uint32_t enext =
@@ -621,206 +867,10 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       const int T = readlane(inc, 63);
       const int o0 = inc - myw;  // window-relative output of this lane's first record
       WPH(4)
-      // ---- 5: error checks, block map, expansion (rounds of 2048 words) -----
-      bool failed = false;
+      // ---- 5: error checks, block map, expansion ------------------------------
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
-      // errors and the filling record can only occur in a window reaching the
-      // piece's last word or within one window plus one record of its end
-      // (the window's records start before e + kWin; the longest record, a
-      // 0xFF tag with its word, count and 255 words, is 2,050 bytes)
-      const bool chk = (ow + T >= W) || (P - e < kDecChkReach);
-      for (int rb = 0; rb < T; rb += kRound) {
-        int err = 0x7fffffff;
-        wave_lds_order();  // (the visited masks / last round's map reads are done)
-#pragma unroll
-        for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = 0u;
-        wave_lds_order();
-        // after the first round only the lanes whose output meets this round
-        if (!(chk && rb == 0)) {
-          // no record here can fail or fill the piece: the map alone
-          if (rb == 0) {
-            // round 0 (usually the window's only one): every record's output
-            // is at or past the round's start, so it always marks a block
-            if (on) {
-              uint32_t rel = (uint32_t)o0;
-              for (uint32_t q = entry; q < S && rel <= (uint32_t)(kRound - kBlk);) {
-                const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
-                const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
-                atomicMax(&blk[(rel + kBlk - 1) / kBlk], ((rel + 256u) << 12) | (q - e));
-                rel += 1u + (zm & c1) + (fm & c9);
-                q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
-              }
-            }
-          } else
-          if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
-            int rel = o0 - rb;  // round-relative output of the record (> -256 when live)
-            // (records past the round's last block start mark nothing, nor
-            // do the ones after them)
-            for (uint32_t q = entry; q < S && rel <= kRound - kBlk;) {
-              const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
-              const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
-              const int nw = 1 + (int)((zm & c1) + (fm & c9));
-              if (rel + nw > 0)
-                atomicMax(&blk[(max(rel, 0) + kBlk - 1) / kBlk], ((uint32_t)(rel + 256) << 12) | (q - e));
-              rel += nw;
-              q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
-            }
-          }
-        } else
-        {
-          // round 0 of a window near the piece's end.  Only two records can
-          // fail or fill the piece: the one whose words reach word W (when the
-          // window gets there; the reference stops reading after it), else the
-          // window's last record (the only one whose bytes can pass P: every
-          // other record ends where the next begins, before wend <= P).  The
-          // map walk notes them; one lane then runs the reference's checks
-          // on its record (PackedInputStream.java:53-138).
-          uint32_t qc = 0xffffffffu;
-          int oc = 0;
-          if (on) {
-            const int wr = W - ow;  // words left in the piece (> 0)
-            uint32_t ql = entry;
-            int o = o0, ol = o0;
-            for (uint32_t q = entry; q < S;) {
-              const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
-              const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
-              const int nw = 1 + (int)((zm & c1) + (fm & c9));
-              const int idx = (o + kBlk - 1) / kBlk;  // (round 0: o >= 0)
-              if (idx < kRound / kBlk) atomicMax(&blk[idx], ((uint32_t)(o + 256) << 12) | (q - e));
-              if (o < wr && o + nw >= wr) {
-                qc = q;
-                oc = o;
-              }
-              ql = q;
-              ol = o;
-              o += nw;
-              q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
-            }
-            if (ow + T < W && lane == 63 - __builtin_clzll(onmask)) {
-              qc = ql;
-              oc = ol;
-            }
-          }
-          if (qc != 0xffffffffu) {
-            const uint32_t q = qc;
-            const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
-            const uint32_t ntag = 1 + __builtin_popcount(tag);
-            const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
-            const int nw = 1 + (int)((zm & c1) + (fm & c9));
-            const uint32_t adv = ntag + (zm & 1u) + (fm & (8u * c9 + 1u));
-            const int oo = ow + oc;
-            // truncated tag bytes / count / literal run -> EOF DecodeException;
-            // run past the piece -> DecodeException / BufferOverflowException
-            int code = 0;
-            if (q + ntag > P) code = 2;
-            else if (tag == 0 || tag == 0xffu) {
-              if (q + (tag ? 10u : 2u) > P) code = 2;
-              else if (oo + nw > W) code = 3;
-              else if (q + adv > P) code = 2;
-            }
-            if (!kStream && !code && oo + nw == W && q + adv < P) code = 4;
-            if (code) err = (int)(((q - e) << 3) | (uint32_t)code);
-            if (oo + nw == W) fin = q + adv;
-          }
-        }
-        if (rb == 0) {
-          err = __builtin_amdgcn_readfirstlane(wave_min(err));
-          if (err != 0x7fffffff) {
-            st = -(err & 7);
-            failed = true;
-            break;
-          }
-          fin = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u(fin));
-        }
-        wave_lds_order();
-        {
-          // prefix max: lane l holds blocks [kMapPer * l, kMapPer * (l + 1))
-          uint32_t m[kMapPer];
-          int run = 0;
-#pragma unroll
-          for (int i = 0; i < kMapPer; ++i) {
-            run = max(run, (int)blk[lane * kMapPer + i]);
-            m[i] = (uint32_t)run;
-          }
-          const uint32_t pre = (uint32_t)wave_shr1(wave_incl_max(run), 0);
-#pragma unroll
-          for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = max(m[i], pre);
-        }
-        wave_lds_order();
-        WPH(5)
-        const int nb = (min(min(kRound, T - rb), W - ow - rb) + kBlk - 1) / kBlk;
-        // two copies of the expansion: one for windows whose records all lie
-        // in the loaded bytes (enext + 12 <= lend: the usual case), whose
-        // reads need no bound check and no memory path
-        auto expand = [&](auto allin) __attribute__((always_inline)) {
-        constexpr bool kAllIn = decltype(allin)::value;
-        for (int b = lane; b < nb; b += 64) {
-          const uint32_t v = blk[b];
-          uint32_t q = e + (v & 0xfffu);
-          int ofs = kBlk * b + 256 - (int)(v >> 12);
-          const int wbase = ow + rb + kBlk * b;  // piece word of the block's first word
-          const int wleft = ow + T - wbase - 1;   // words of the window after the block's first
-          uint64_t words[kBlk];
-#pragma unroll
-          for (int i = 0; i < kBlk; ++i) {
-            // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
-            // run (tag word, then the counted words), or a tagged word
-            // (the count bytes are read with the tag: one LDS round trip)
-            uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
-            uint64_t x;
-            int nw;
-            uint32_t adv;
-            if (tag == 0) {
-              x = 0;
-              nw = 1 + c1;
-              adv = 2;
-            } else if (tag == 0xffu) {
-              const uint32_t rn = c9;
-              nw = 1 + (int)rn;
-              adv = 10 + 8 * rn;
-              x = read8<kAllIn>(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
-            } else {
-              const uint64_t raw = read8<kAllIn>(pkw, q + 1, lend, gp, glim, ph, e);
-              const uint64_t sel = lut[tag];
-              const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
-              const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
-              const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
-              x = (uint64_t)x0 | ((uint64_t)x1 << 32);
-              nw = 1;
-              adv = 1 + __builtin_popcount(tag);
-            }
-            words[i] = x;
-            // past the window's last word: stay put (never stored)
-            if (++ofs == nw && i < wleft) {
-              q += adv;
-              ofs = 0;
-            }
-          }
-          const int kw = min(kBlk, min(ow + T, W) - wbase);
-          uint64_t *d = dst + wbase;
-          if (kw == kBlk && ((reinterpret_cast<uintptr_t>(d) & 15) == 0)) {
-#pragma unroll
-            for (int i = 0; i < kBlk; i += 2) {
-              uint4 v4;
-              v4.x = (uint32_t)words[i];
-              v4.y = (uint32_t)(words[i] >> 32);
-              v4.z = (uint32_t)words[i + 1];
-              v4.w = (uint32_t)(words[i + 1] >> 32);
-              st_stream(v4, d + i);
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < kBlk; ++i)
-              if (i < kw) d[i] = words[i];
-          }
-        }
-        };
-        if (enext + 12 <= lend) expand(std::true_type{});
-        else
-          expand(std::false_type{});
-        wave_lds_order();  // blk reused by the next round
-        WPH(6)
-      }
+      const bool failed = !win_emit<kStream>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
+                                             enext, lend, gp, glim, ph, dst, st, fin DEC_PH_ARGS);
       if (failed) break;
       if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
         ow = W;
@@ -1163,6 +1213,8 @@ __global__ __launch_bounds__(kDecThreads, 1) void rm_small_kernel(
   rm_final_body(send_out, pst, sdesc + 3, info, mirror);
   if (mirror) small_done(mirror + kRmInfo, seq);
 }
+
+#include "decode_mw.hip"
 
 // ---- message write: Serialize.write = table piece + segment pieces --------
 // PackedOutputStream.write (:35-205) byte-serial over a word source, as the
@@ -1961,6 +2013,14 @@ namespace {
 // blocks and decoded in parallel (stream_split.hip); shorter ones by one wave
 constexpr uint64_t kSsMin = 256 * 1024;
 constexpr uint64_t kRmSsMin = 64 * 1024;  // cpk_read_message
+// cpk_read_message_host: streams under kRmMwMax bytes in one launch (pinned
+// memory, no DMA), by one wave (rm_small_kernel) under kRmMwMin, else by a
+// whole workgroup (rm_mw_kernel).  Measured (threshold_probe, config-2-like
+// messages): one wave 36.7 / mw 42.9 us at 3.9 KB packed, 51.2 / 45.7 at
+// 7.8 KB; mw 54 us at 64 KiB of words (one wave 151), 116 at 256 KiB (the
+// parallel block path 206)
+constexpr uint64_t kRmMwMin = 6 * 1024;
+constexpr uint64_t kRmMwMax = 512 * 1024;
 
 // the bytes a stream of `words` words may take: 10 per word at most
 uint64_t ss_reach(uint64_t avail, uint64_t words) {
@@ -2115,13 +2175,30 @@ static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, 
   const uint64_t reach = ss_reach(avail, out_cap_words + cpk::kRmHead);
   // (a lower bar than cpk_decode_stream's: a message's one-wave decode is
   //  ~0.5 GB/s, the parallel path ~250 us of fixed cost: even at 64 KiB)
-  const bool par = reach >= kRmSsMin && !getenv("CPK_STREAM_ONE_WAVE");
+  const bool one = getenv("CPK_STREAM_ONE_WAVE") != nullptr;
+  if (info_mirror && !one && !dec_v2(ctx) && reach >= kRmMwMin && reach < kRmMwMax) {
+    // (the host path: pinned bytes, copied to the device in the kernel)
+    if (!ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmMwMax + 128) != hipSuccess) return CPK_ENOMEM;
+    static bool attr = false;
+    if (!attr) {
+      if (hipFuncSetAttribute((const void *)cpk::rm_mw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)cpk::kMwLds) != hipSuccess)
+        return CPK_EDEVICE;
+      attr = true;
+    }
+    hipLaunchKernelGGL(cpk::rm_mw_kernel, dim3(1), dim3(cpk::kMwThreads), cpk::kMwLds, s,
+                       (const uint8_t *)d_packed, avail, traversal_limit_words, out_cap_words, swo, d_info, sdesc,
+                       (uint64_t *)d_out, in_off, pst, send_out, info_mirror, ctx->rm_copy, seq);
+    if (flagged) *flagged = true;
+    return hip_ok(hipGetLastError());
+  }
+  const bool par = reach >= kRmSsMin && !one;
   if (!par && !dec_v2(ctx)) {
     // (the host path's packed bytes are pinned host memory: copied to the
     // device once, in the kernel)
     uint8_t *dcopy = nullptr;
-    if (info_mirror && reach + 96 <= kRmSsMin + 128) {
-      if (!ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmSsMin + 128) != hipSuccess) return CPK_ENOMEM;
+    if (info_mirror && reach + 96 <= kRmMwMax + 128) {
+      if (!ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmMwMax + 128) != hipSuccess) return CPK_ENOMEM;
       dcopy = ctx->rm_copy;
     }
     hipLaunchKernelGGL(cpk::rm_small_kernel, dim3(1), dim3(cpk::kDecThreads), cpk::kDecLds, s,
@@ -2274,7 +2351,7 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   if (rc) return rc;
   HostSlot &sl = p->slot[0];
   uint64_t *info = sl.pin_meta;
-  if (R < kRmSsMin && !getenv("CPK_NO_SMALL")) {
+  if (R < kRmMwMax && !getenv("CPK_NO_SMALL")) {
     // the one-wave range: the kernels read the packed bytes from the pinned
     // slot and write the words and the info row into pinned memory in place
     // -- no DMA either way, one sync

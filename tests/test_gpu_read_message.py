@@ -187,3 +187,30 @@ def test_small_host_paths_back_to_back(ctx, oracle):
         assert st == 0 and got == segs and used == len(pk), k
         packed, _ = ctx.encode_messages_host([segs])
         assert bytes(packed) == pk, k
+
+
+def test_read_message_mid_size_workgroup_path(ctx, oracle):
+    """Streams of 6-512 KiB take the one-launch workgroup decoder
+    (decode_mw.hip: a piece's windows spread over 16 waves, entries chained
+    between them): clean messages of 1-9 segments (empty ones included) with
+    the next message behind them, cuts anywhere (ETRUNC), byte flips
+    (status, segments and bytes consumed equal the oracle's Serialize.read)
+    and both dense and sparse data."""
+    rng = np.random.default_rng(14)
+    for cfg_probs in ((.4, .3, .2, .1), (.05, .05, .1, .8), (.9, .05, .03, .02)):
+        for sizes in ([3000], [8192 * 4], [0, 5000, 0, 12000], [int(x) for x in rng.integers(0, 6000, size=9)]):
+            segs, pk = _msg(rng, oracle, sizes, cfg_probs)
+            if not 6 * 1024 <= len(pk) < 512 * 1024:
+                continue
+            _, nxt = _msg(rng, oracle, [7, 0, 3])
+            st, got, used = _check(ctx, oracle, pk + nxt)
+            assert st == 0 and got == segs and used == len(pk)
+            for cut in sorted(set([1, 8, 9, 17, len(pk) // 3, len(pk) // 2, len(pk) - 1] +
+                                  [int(c) for c in rng.integers(1, len(pk), size=12)])):
+                st, _, _ = _check(ctx, oracle, pk[:cut])
+                assert st == -2, cut
+            for _ in range(6):
+                b = bytearray(pk + nxt)
+                for i in rng.integers(0, len(pk), size=int(rng.integers(1, 4))):
+                    b[int(i)] = int(rng.integers(0, 256))
+                _check(ctx, oracle, bytes(b))

@@ -6,6 +6,7 @@
 //       -Lcapnproto-java_amd/lib -lcapnp_packed_hip -Wl,-rpath,$PWD/capnproto-java_amd/lib -o build/small_stress
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -42,8 +43,10 @@ static int run(cpk_ctx ctx, const std::vector<Msg> &ms, bool rd, bool wr, int it
   int bad = 0;
   std::vector<uint64_t> words(1300), info(CPK_MSG_INFO_WORDS), off(3);
   std::vector<uint8_t> out(20000);
+  const bool verbose = getenv("SS_VERBOSE") != nullptr;
   for (int k = 0; k < iters; ++k) {
     const Msg &m = ms[k % ms.size()];
+    if (verbose) std::fprintf(stderr, "%s iter %d (packed %zu)\n", tag, k, m.pk.size());
     if (rd) {
       const int rc = cpk_read_message_host(ctx, m.pk.data(), m.pk.size(), 1ull << 30, words.data(), words.size(),
                                            info.data());
