@@ -350,7 +350,9 @@ __device__ __forceinline__ void sp3_flush(uint8_t *out, uint32_t *stage, uint64_
 // need not be contiguous: a message's table may follow the segments).  The
 // run state a chunk leaves for the piece's next chunk passes through two LDS
 // words.  out_off[0..n] written.
-constexpr uint64_t kSpSmallWords = 32768;  // (256 KiB: four chunks, ~10 us each)
+// (32768 segment words and the tables: a 256 KiB message with its table
+// stays here -- 4 chunks, ~90 us, against ~135 us through the DMA pipeline)
+constexpr uint64_t kSpSmallWords = 32768 + 1024;
 constexpr uint32_t kSpSmallPieces = 512;   // piece descriptors staged in LDS (8 KiB)
 constexpr uint32_t kSpSmallLds = kSp3Lds + 16 * kSpSmallPieces;
 

@@ -4,9 +4,13 @@
 // org.capnproto.gpu.GpuDispatch, whatever -Dorg.capnproto.gpu says.
 // integration/capnproto-java.patch adds it to Compression.java:33-34, the
 // "gpu-packed" argument to TestCase.java:188-195 and its runs to
-// do_benchmarks.bash.  Messages below GpuDispatch.MIN_BYTES take the
-// reference's codec, as every dispatched SerializePacked call does
-// (-Dorg.capnproto.gpu.minBytes=0: every message on the GPU).
+// do_benchmarks.bash.  Messages below GpuDispatch.MIN_WRITE_BYTES /
+// MIN_READ_BYTES take the reference's codec, as every dispatched
+// SerializePacked call does: with the default thresholds none of the
+// harness's carsales / catrank / eval messages (a few KiB, under the 1 MiB
+// scratch of TestCase.java:46) reaches the GPU; the do_benchmarks.bash lines
+// the patch adds pass -Dorg.capnproto.gpu.minBytes=0, every message on the
+// GPU, to time the device path itself.
 package org.capnproto.benchmark;
 
 import java.io.IOException;

@@ -8,14 +8,15 @@
 // read runs Serialize.read's sequence (Serialize.java:119-178) on the device
 // in one library call (cpk_read_message_host).
 //
-// Size threshold: a message of fewer than MIN_BYTES unpacked bytes (table +
-// segments) stays on the reference's own PackedOutputStream /
-// PackedInputStream -- a GPU call costs tens of microseconds of launch and
-// copy latency, which only pays above the crossover measured in
-// INTEGRATION.md.  -Dorg.capnproto.gpu.minBytes=N (or CAPNP_GPU_MIN_BYTES)
-// moves it; 0 sends every message to the GPU.  For a read the size comes
-// from the message's segment table, peeked (not consumed) from the bytes the
-// stream has buffered.
+// Size thresholds: a message of fewer than MIN_WRITE_BYTES (written) or
+// MIN_READ_BYTES (read) unpacked bytes (table + segments) stays on the
+// reference's own PackedOutputStream / PackedInputStream -- a GPU call costs
+// ~20-50 microseconds of launch and PCIe latency, which only pays above the
+// crossovers measured in INTEGRATION.md.  -Dorg.capnproto.gpu.minWriteBytes
+// / minReadBytes (CAPNP_GPU_MIN_WRITE_BYTES / CAPNP_GPU_MIN_READ_BYTES) move
+// one, -Dorg.capnproto.gpu.minBytes (CAPNP_GPU_MIN_BYTES) both; 0 sends every
+// message to the GPU.  For a read the size comes from the message's segment
+// table, peeked (not consumed) from the bytes the stream has buffered.
 //
 // Streams: a GPU read consumes exactly the bytes the reference's
 // PackedInputStream would -- up to the end of the record that completes the
@@ -48,15 +49,22 @@ public final class GpuDispatch {
     private static final boolean ENABLED =
         Boolean.getBoolean("org.capnproto.gpu") || "1".equals(System.getenv("CAPNP_GPU"));
 
-    /** Messages below this many unpacked bytes take the reference's CPU codec
-     *  (default: the crossover measured in INTEGRATION.md). */
-    public static final long DEFAULT_MIN_BYTES = 1L << 20;
-    public static final long MIN_BYTES = minBytes();
+    /** Messages below these many unpacked bytes take the reference's CPU
+     *  codec (defaults: the write and read crossovers measured in
+     *  INTEGRATION.md, tests/cpp/threshold_probe.cpp). */
+    public static final long DEFAULT_MIN_WRITE_BYTES = 128L << 10;
+    public static final long DEFAULT_MIN_READ_BYTES = 512L << 10;
+    public static final long MIN_WRITE_BYTES =
+        threshold("minWriteBytes", "CAPNP_GPU_MIN_WRITE_BYTES", DEFAULT_MIN_WRITE_BYTES);
+    public static final long MIN_READ_BYTES =
+        threshold("minReadBytes", "CAPNP_GPU_MIN_READ_BYTES", DEFAULT_MIN_READ_BYTES);
 
-    private static long minBytes() {
-        String v = System.getProperty("org.capnproto.gpu.minBytes");
+    private static long threshold(String prop, String env, long dflt) {
+        String v = System.getProperty("org.capnproto.gpu." + prop);
+        if (v == null) v = System.getenv(env);
+        if (v == null) v = System.getProperty("org.capnproto.gpu.minBytes");  // (both at once)
         if (v == null) v = System.getenv("CAPNP_GPU_MIN_BYTES");
-        return v == null ? DEFAULT_MIN_BYTES : Long.parseLong(v.trim());
+        return v == null ? dflt : Long.parseLong(v.trim());
     }
 
     /** One context per process, created on first use (the library loads then). */
@@ -82,11 +90,11 @@ public final class GpuDispatch {
     /** SerializePacked.write(output, message) for a message of `segments`
      *  (MessageBuilder.getSegmentsForOutput, BuilderArena.java:143-154, or a
      *  MessageReader's segments, Serialize.java:293-299).  Returns false,
-     *  having written nothing, for a message below MIN_BYTES: the caller then
+     *  having written nothing, for a message below MIN_WRITE_BYTES: the caller then
      *  runs the reference's PackedOutputStream. */
     public static boolean write(org.capnproto.BufferedOutputStream output, ByteBuffer[] segments)
             throws IOException {
-        if (messageBytes(segments) < MIN_BYTES) return false;
+        if (messageBytes(segments) < MIN_WRITE_BYTES) return false;
         ByteBuffer bytes = packed(segments);
         while (bytes.hasRemaining()) output.write(bytes);
         return true;
@@ -95,10 +103,10 @@ public final class GpuDispatch {
     /** SerializePacked.writeToUnbuffered(channel, message): the packed bytes
      *  straight to the channel -- the bytes the reference's 8 KiB
      *  BufferedOutputStreamWrapper + flush put there (SerializePacked.java:
-     *  119-134).  False, nothing written, below MIN_BYTES. */
+     *  119-134).  False, nothing written, below MIN_WRITE_BYTES. */
     public static boolean writeToUnbuffered(WritableByteChannel output, ByteBuffer[] segments)
             throws IOException {
-        if (messageBytes(segments) < MIN_BYTES) return false;
+        if (messageBytes(segments) < MIN_WRITE_BYTES) return false;
         ByteBuffer bytes = packed(segments);
         while (bytes.hasRemaining()) output.write(bytes);
         return true;
@@ -126,7 +134,7 @@ public final class GpuDispatch {
     }
 
     /** SerializePacked.read(input, options): the message, read on the GPU;
-     *  null when it is below MIN_BYTES (or its table is not yet buffered) --
+     *  null when it is below MIN_READ_BYTES (or its table is not yet buffered) --
      *  nothing consumed, the caller runs the reference path over input. */
     public static org.capnproto.MessageReader read(org.capnproto.BufferedInputStream input,
                                                    org.capnproto.ReaderOptions options) throws IOException {
@@ -135,7 +143,7 @@ public final class GpuDispatch {
         ByteBuffer head = input.getReadBuffer();
         if (!head.hasRemaining()) throw new org.capnproto.DecodeException("premature EOF");
         long bytes = peekMessageBytes(head);
-        if (bytes < 0 || bytes < MIN_BYTES) return null;
+        if (bytes < 0 || bytes < MIN_READ_BYTES) return null;
         long words = bytes / 8;
         if (input instanceof org.capnproto.ArrayInputStream) {
             // the whole array is the read buffer (ArrayInputStream.java:53-58)
@@ -149,7 +157,7 @@ public final class GpuDispatch {
 
     /** SerializePacked.tryRead(input, options): Optional.empty() when the
      *  stream ends before a message starts (the documented contract,
-     *  SerializePacked.java:31-46); null when the message is below MIN_BYTES
+     *  SerializePacked.java:31-46); null when the message is below MIN_READ_BYTES
      *  (the caller then runs the reference path over input). */
     public static Optional<org.capnproto.MessageReader> tryRead(org.capnproto.BufferedInputStream input,
                                                                 org.capnproto.ReaderOptions options)

@@ -59,7 +59,7 @@ def main():
             edit(sp, sig, sig +
                  f"        if ({G}.enabled()) {{\n"
                  f"            {ret} m = {G}.{kind}(input, options);\n"
-                 f"            if (m != null) return m;  // (null: below {G}.MIN_BYTES, the codec below)\n"
+                 f"            if (m != null) return m;  // (null: below {G}.MIN_READ_BYTES, the codec below)\n"
                  f"        }}\n")
         for tail, kind in (("        return Serialize.tryRead(packedInput, options);\n", "tryRead"),
                            ("        return Serialize.read(packedInput, options);\n", "read")):
@@ -74,7 +74,7 @@ def main():
             edit(sp, f"{msg} message) throws java.io.IOException {{\n        PackedOutputStream packedOutputStream",
                  f"{msg} message) throws java.io.IOException {{\n"
                  f"        if ({G}.enabled() && {G}.write(output, {segs})) {{\n"
-                 "            return;  // (false: below MIN_BYTES, the codec below)\n"
+                 "            return;  // (false: below MIN_WRITE_BYTES, the codec below)\n"
                  "        }\n"
                  "        PackedOutputStream packedOutputStream")
             edit(sp, f"{msg} message) throws java.io.IOException {{\n        BufferedOutputStreamWrapper buffered",
@@ -106,9 +106,10 @@ def main():
         edit(db, 'alias run_java="java -cp runtime/target/classes:benchmark/target/classes"',
              'alias run_java="java -cp runtime/target/classes:benchmark/target/classes"\n'
              '# gpu-packed: the MI355X codec (libcapnp_packed_jni.so + libcapnp_packed_hip.so '
-             'on java.library.path)\n'
+             'on java.library.path), every message on the device (minBytes=0: the harness\'s '
+             'messages are all under the default size thresholds)\n'
              'alias run_java_gpu="java -Djava.library.path=${CAPNP_GPU_LIB:-lib} '
-             '-cp runtime/target/classes:benchmark/target/classes"')
+             '-Dorg.capnproto.gpu.minBytes=0 -cp runtime/target/classes:benchmark/target/classes"')
         for t in ("CarSales", "CatRank", "Eval"):
             line = f"time run_java org.capnproto.benchmark.{t} bytes no-reuse packed $ITERS\n"
             edit(db, line, line + f"time run_java_gpu org.capnproto.benchmark.{t} bytes no-reuse gpu-packed $ITERS\n")
