@@ -287,3 +287,14 @@ __global__ __launch_bounds__(kMwThreads, 1) void rm_mw_kernel(
   rm_final_body(send_out, pst, sdesc + 3, info, mirror);
   if (mirror) small_done(mirror + kRmInfo, seq);
 }
+
+// cpk_decode_stream of a mid-size stream: pieces 0..n-1 from packed[0, avail)
+// by one kMwWaves-wave workgroup (in_off[n]: the stream's end)
+__global__ __launch_bounds__(kMwThreads, 1) void stream_mw_kernel(const uint8_t *__restrict__ packed, uint64_t avail,
+                                                                  const uint64_t *__restrict__ swo, uint32_t n,
+                                                                  uint64_t *__restrict__ out,
+                                                                  uint64_t *__restrict__ in_off,
+                                                                  int32_t *__restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  decode_stream_mw(smem, packed, 0, avail, swo, 0, n, out, status, in_off, in_off + n);
+}

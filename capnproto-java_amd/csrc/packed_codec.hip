@@ -2021,6 +2021,20 @@ constexpr uint64_t kRmSsMin = 64 * 1024;  // cpk_read_message
 // parallel block path 206)
 constexpr uint64_t kRmMwMin = 6 * 1024;
 constexpr uint64_t kRmMwMax = 512 * 1024;
+// (cpk_decode_stream takes the workgroup decoder for streams of
+// [kRmMwMin, kSsMin) reachable bytes)
+int mw_attr() {
+  static int rc = -1;
+  if (rc < 0) {
+    rc = hipFuncSetAttribute((const void *)cpk::rm_mw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)cpk::kMwLds) == hipSuccess &&
+                 hipFuncSetAttribute((const void *)cpk::stream_mw_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)cpk::kMwLds) == hipSuccess
+             ? 0
+             : 1;
+  }
+  return rc;
+}
 
 // the bytes a stream of `words` words may take: 10 per word at most
 uint64_t ss_reach(uint64_t avail, uint64_t words) {
@@ -2128,6 +2142,13 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
       return ss_decode(ctx, (const uint8_t *)d_packed, avail, reach, d_swo, n, (uint64_t *)d_out, d_in_off,
                        d_status, s);
   }
+  if (avail >= kRmMwMin && !getenv("CPK_STREAM_ONE_WAVE")) {
+    // a mid-size stream: one workgroup, its 16 waves sharing each piece's windows
+    if (mw_attr()) return CPK_EDEVICE;
+    hipLaunchKernelGGL(cpk::stream_mw_kernel, dim3(1), dim3(cpk::kMwThreads), cpk::kMwLds, s,
+                       (const uint8_t *)d_packed, avail, d_swo, n, (uint64_t *)d_out, d_in_off, d_status);
+    return hip_ok(hipGetLastError());
+  }
   if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
     return CPK_EDEVICE;
   // one stream: one wave works, the others find no ticket
@@ -2176,20 +2197,16 @@ static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, 
   // (a lower bar than cpk_decode_stream's: a message's one-wave decode is
   //  ~0.5 GB/s, the parallel path ~250 us of fixed cost: even at 64 KiB)
   const bool one = getenv("CPK_STREAM_ONE_WAVE") != nullptr;
-  if (info_mirror && !one && !dec_v2(ctx) && reach >= kRmMwMin && reach < kRmMwMax) {
+  if (!one && !dec_v2(ctx) && reach >= kRmMwMin && reach < kRmMwMax) {
     // (the host path: pinned bytes, copied to the device in the kernel)
-    if (!ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmMwMax + 128) != hipSuccess) return CPK_ENOMEM;
-    static bool attr = false;
-    if (!attr) {
-      if (hipFuncSetAttribute((const void *)cpk::rm_mw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)cpk::kMwLds) != hipSuccess)
-        return CPK_EDEVICE;
-      attr = true;
-    }
+    if (info_mirror && !ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmMwMax + 128) != hipSuccess)
+      return CPK_ENOMEM;
+    if (mw_attr()) return CPK_EDEVICE;
     hipLaunchKernelGGL(cpk::rm_mw_kernel, dim3(1), dim3(cpk::kMwThreads), cpk::kMwLds, s,
                        (const uint8_t *)d_packed, avail, traversal_limit_words, out_cap_words, swo, d_info, sdesc,
-                       (uint64_t *)d_out, in_off, pst, send_out, info_mirror, ctx->rm_copy, seq);
-    if (flagged) *flagged = true;
+                       (uint64_t *)d_out, in_off, pst, send_out, info_mirror,
+                       info_mirror ? ctx->rm_copy : nullptr, seq);
+    if (flagged) *flagged = info_mirror != nullptr;
     return hip_ok(hipGetLastError());
   }
   const bool par = reach >= kRmSsMin && !one;

@@ -150,13 +150,15 @@ def test_read_message_capacity(ctx, oracle):
     assert st == 0 and got == segs and used == len(pk)
 
 
-def test_read_message_device_form(ctx, oracle):
+@pytest.mark.parametrize("sizes", [[4000, 0, 70000, 9], [3000, 0, 9000, 5]])
+def test_read_message_device_form(ctx, oracle, sizes):
     """cpk_read_message on device buffers: the info row and the decoded
-    words in HBM, the segments after the table's words."""
+    words in HBM, the segments after the table's words (the parallel block
+    path, and the one-workgroup decoder for the mid-size stream)."""
     import torch
     import capnp_packed as cp
     rng = np.random.default_rng(12)
-    segs, pk = _msg(rng, oracle, [4000, 0, 70000, 9])
+    segs, pk = _msg(rng, oracle, sizes)
     stream = pk + bytes(rng.integers(0, 256, size=5000, dtype=np.uint8))
     d_pk = torch.zeros((len(stream) + 64 + 15) // 16 * 16, dtype=torch.uint8, device="cuda")
     d_pk[: len(stream)] = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda()
@@ -166,7 +168,7 @@ def test_read_message_device_form(ctx, oracle):
     ctx.read_message(d_pk, len(stream), d_out, d_info)
     torch.cuda.synchronize()
     info = d_info.cpu().numpy()
-    assert info[0] == 0 and info[1] == len(pk) and info[2] == 4 and info[3] == words
+    assert info[0] == 0 and info[1] == len(pk) and info[2] == len(sizes) and info[3] == words
     out = d_out.cpu().numpy().view(np.uint8)
     got = [out[8 * int(info[4 + i]): 8 * int(info[5 + i])].tobytes() for i in range(4)]
     assert got == segs

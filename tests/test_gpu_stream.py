@@ -211,3 +211,31 @@ def test_parallel_stream_garbage_matches_one_wave(ctx, oracle):
             stream = bytes(b) + bytes(rng.integers(0, 256, size=300_000, dtype=np.uint8))
         _check(ctx, oracle, stream, swo)
 
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4])
+def test_mid_size_stream_workgroup_path(ctx, oracle, cfg):
+    """Streams of 6-256 KiB reachable bytes take the one-workgroup decoder
+    (decode_mw.hip): one piece, ragged pieces with empty ones, junk behind
+    the stream, cuts, flips and mis-sized pieces -- statuses, boundaries and
+    words equal to the oracle's and to the one-wave decoder's."""
+    rng = np.random.default_rng(20 + cfg)
+    for sizes in ([3000], [9000], [0, 1, 700, 0, 2500, 64, 3], [int(x) for x in rng.integers(0, 1500, size=20)]):
+        swo = _swo(sizes)
+        data = oracle.generate(oracle.preset(cfg), swo)
+        stream, off = _stream_of(oracle, data, swo)
+        junk = bytes(rng.integers(0, 256, size=3000, dtype=np.uint8))
+        bounds, _ = _check(ctx, oracle, stream + junk, swo)
+        assert np.array_equal(bounds, off)
+        for cut in rng.integers(1, len(stream), size=5):
+            _check(ctx, oracle, stream[: int(cut)], swo)
+        for _ in range(4):
+            b = bytearray(stream)
+            for i in rng.integers(0, len(b), size=2):
+                b[int(i)] = int(rng.integers(0, 256))
+            _check(ctx, oracle, bytes(b), swo)
+        if len(sizes) > 2 and sizes[1] > 3:
+            bad = list(sizes)
+            bad[1] -= 3
+            bad[2] += 3
+            _check(ctx, oracle, stream, _swo(bad))
