@@ -354,7 +354,11 @@ __device__ __forceinline__ void sp3_flush(uint8_t *out, uint32_t *stage, uint64_
 // stays here -- 4 chunks, ~90 us, against ~135 us through the DMA pipeline)
 constexpr uint64_t kSpSmallWords = 32768 + 1024;
 constexpr uint32_t kSpSmallPieces = 512;   // piece descriptors staged in LDS (8 KiB)
-constexpr uint32_t kSpSmallLds = kSp3Lds + 16 * kSpSmallPieces;
+// pieces of at most this many words (a message's segment table, tiny
+// segments) are packed byte-serially by one thread from LDS: ~5 us of the
+// chunk machinery (loads, three barriers, the flush) saved per piece
+constexpr uint32_t kSpSerialWords = 16;
+constexpr uint32_t kSpSmallLds = kSp3Lds + 16 * kSpSmallPieces + 8 * kSpSerialWords;
 
 __device__ __forceinline__ Sp3Unit sp3_unit_at(const uint64_t *pw, uint32_t W, uint32_t p, uint32_t c, int w) {
   Sp3Unit u;
@@ -387,6 +391,7 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
   uint64_t *scr = reinterpret_cast<uint64_t *>(smem + kSp3oScr);
   uint32_t *stage = reinterpret_cast<uint32_t *>(smem + kSp3oStage);
   uint64_t *ldesc = reinterpret_cast<uint64_t *>(smem + kSp3Lds);
+  uint64_t *sbuf = reinterpret_cast<uint64_t *>(smem + kSp3Lds + 16 * kSpSmallPieces);
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   if (flag) small_begin();
@@ -407,6 +412,23 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
     const uint32_t W = (uint32_t)sp_ld(&ldesc[2 * p + 1]);
     const uint32_t nch = max((((W + 63) >> 6) + kSpCS - 1) / kSpCS, 1u);
     if (threadIdx.x == 0) out_off[p] = g;
+    if (W <= kSpSerialWords) {
+      // PackedOutputStream.write (:35-205) byte-serially, as the tables'
+      // kernel packs them (serial_pack), the words read in one round trip
+      if (threadIdx.x < W) sbuf[threadIdx.x] = in[w0 + threadIdx.x];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint64_t o = g;
+        serial_pack(W, [&](uint32_t i) { return sbuf[i]; }, [&](uint32_t b) {
+          if (o < ocap) out[o] = (uint8_t)b;
+          ++o;
+        });
+        scr[28] = o - g;
+      }
+      __syncthreads();
+      g += sp_ld(&scr[28]);
+      continue;
+    }
     for (uint32_t c = 0; c < nch; ++c) {
       const Sp3Unit u = sp3_unit_at(in + w0, W, p, c, w);
       uint64_t V[kSpWS], LA[4];
