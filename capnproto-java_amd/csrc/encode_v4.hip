@@ -237,8 +237,10 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;
     // software pipeline: the next kE4Pf steps' loads are in flight while
     // these are classified
-    // steps of loads in flight ahead of the size pass's classification
-constexpr int PF = 4;
+    // steps of loads in flight ahead of the size pass's classification (8:
+    // config-3 messages' e4 encode 7.06 -> 7.00 ms, config 2 6.39 -> 6.29
+    // against 4, r4K_ab.log; 64 VGPRs, no spill at 8 workgroups per CU)
+    constexpr int PF = 8;
     uint64_t v[PF], vn[PF];
     // loads clamped to the piece's last word, not predicated (no exec-mask
     // branches around them); words past the end are masked by `valid`
