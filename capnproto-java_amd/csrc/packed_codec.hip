@@ -710,7 +710,8 @@ struct DecStreams {
   const uint64_t *sbeg, *send, *spc;
   uint32_t ns;
   uint64_t *send_out;
-  const uint32_t *skip;  // (batch form: nonzero = the other decoder took the batch)
+  const uint32_t *skip;   // (batch form: nonzero = the other decoder took the batch)
+  const uint32_t *order;  // (stream form: ticket -> stream, largest first; null: in order)
 };
 template <bool kStream>
 __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__restrict__ packed,
@@ -763,6 +764,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
           more = false;
           break;
         }
+        if (sd.order) j = sd.order[j];
         sj = j;
         snext = sd.sbeg ? (uint32_t)sd.spc[j] : 0u;
         sende = sd.sbeg ? (uint32_t)sd.spc[j + 1] : n;
@@ -989,6 +991,43 @@ __device__ int read_table(const uint8_t *p, uint64_t n, uint64_t limit, uint64_t
   // when that segment is allocated: the message fails either way
   if (big) return CPK_EFRAME;
   return CPK_OK;
+}
+
+// ---- stream tickets, largest first --------------------------------------
+// A wave decodes a message's stream whole, so a large message taken last
+// leaves the other waves idle while it finishes (config 3: 1 MiB messages
+// among 16 KiB ones; taken largest first the decode is 3.8 % shorter).  A
+// counting sort by the bit length of the word count: order[t] = the t-th
+// message to take, larger classes first (within a class in any order -- the
+// output does not depend on it).  (The two-pass encoder's segments taken
+// the same way: 51.3 -> 57.0 ms on config 3 -- the passes stream the words
+// in memory order, and lose that locality.)
+constexpr int kOrdClasses = 64;
+__device__ __forceinline__ uint32_t ord_class(uint64_t w) {
+  return (uint32_t)(kOrdClasses - 1) - (w ? 64u - (uint32_t)__builtin_clzll(w) : 0u);
+}
+__global__ void ord_hist_kernel(const uint64_t *__restrict__ words, uint32_t n, uint32_t *hist) {
+  __shared__ uint32_t h[kOrdClasses];
+  if (threadIdx.x < kOrdClasses) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&h[ord_class(words[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x < kOrdClasses && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+__global__ void ord_scan_kernel(uint32_t *hist) {
+  if (threadIdx.x != 0) return;
+  uint32_t run = 0;
+  for (int c = 0; c < kOrdClasses; ++c) {
+    const uint32_t k = hist[c];
+    hist[c] = run;
+    run += k;
+  }
+}
+__global__ void ord_scatter_kernel(const uint64_t *__restrict__ words, uint32_t n, uint32_t *cursor,
+                                   uint32_t *__restrict__ order) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) order[atomicAdd(&cursor[ord_class(words[i])], 1u)] = i;
 }
 
 // pass 1: per message its table's status, segment count, words and the
@@ -1467,6 +1506,16 @@ struct DeviceGuard {
     if (cur != prev) hipSetDevice(prev);
   }
 };
+
+// order[0..n) = 0..n-1 by size class, largest first (cpk::ord_*); hist:
+// kOrdClasses u32 of scratch
+void ord_launch(const uint64_t *words, uint32_t n, uint32_t *hist, uint32_t *order, hipStream_t s) {
+  const unsigned tb = 256, tg = (n + tb - 1) / tb;
+  (void)hipMemsetAsync(hist, 0, 4 * cpk::kOrdClasses, s);
+  hipLaunchKernelGGL(cpk::ord_hist_kernel, dim3(tg), dim3(tb), 0, s, words, n, hist);
+  hipLaunchKernelGGL(cpk::ord_scan_kernel, dim3(1), dim3(64), 0, s, hist);
+  hipLaunchKernelGGL(cpk::ord_scatter_kernel, dim3(tg), dim3(tb), 0, s, words, n, hist, order);
+}
 
 int ensure_status(cpk_ctx ctx, uint64_t n) {
   if (n <= ctx->status_cap) return CPK_OK;
@@ -2262,10 +2311,12 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
   if (nm == 0) return hip_ok(hipMemsetAsync(d_msg_seg_off, 0, 8, s));
   // scratch: words | begin | words offsets [nm+1] | block sums x2
   const uint32_t nb = (uint32_t)((nm + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
-  int rc = ensure_status(ctx, 3ull * nm + 1 + 2ull * nb);
+  // (+ the stream order: nm u32 and kOrdClasses u32)
+  int rc = ensure_status(ctx, 3ull * nm + 1 + 2ull * nb + (nm + 1) / 2 + cpk::kOrdClasses / 2);
   if (rc) return rc;
   uint64_t *mwords = ctx->status, *mbeg = mwords + nm, *mwoff = mbeg + nm;
   uint64_t *bs0 = mwoff + nm + 1, *bs1 = bs0 + nb;
+  uint32_t *ord = reinterpret_cast<uint32_t *>(bs1 + nb), *ohist = ord + ((nm + 1) & ~1u);
   const unsigned tb = 256, tg = (nm + tb - 1) / tb;
   // the segment counts go to d_msg_seg_off[0..nm) and are scanned into it
   // (e4_scan_down: each thread reads its entries before it writes them)
@@ -2295,10 +2346,14 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
   if (h_totals[1]) {
     if (hipMemsetAsync(ctx->tickets + cpk::kTkDec, 0, 8 * cpk::kTkStride * 4, s) != hipSuccess)
       return CPK_EDEVICE;
+    // the messages' streams largest first (ord_*: a counting sort by size class)
+    ord_launch(mwords, nm, ohist, ord, s);
     // the stream ends overwrite the words array (no longer needed)
     dec_launch(ctx, true, (nm + 3) / 4, (const uint8_t *)d_packed, d_seg_in_off, (const uint64_t *)d_seg_word_off,
                (uint32_t)h_totals[1], (uint64_t *)d_out, d_seg_status, 0,
-               cpk::DecStreams{mbeg, d_msg_off + 1, d_msg_seg_off, nm, mwords}, s);
+               cpk::DecStreams{mbeg, d_msg_off + 1, d_msg_seg_off, nm, mwords, nullptr,
+                               ord},
+               s);
     hipLaunchKernelGGL(cpk::msg_final_kernel, dim3(tg), dim3(tb), 0, s, d_msg_off, nm,
                        (const uint64_t *)d_msg_seg_off, (const uint64_t *)mwords,
                        (const int32_t *)d_seg_status, d_msg_status);
