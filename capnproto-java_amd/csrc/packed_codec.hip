@@ -2059,8 +2059,11 @@ static int decode_batch_impl(cpk_ctx ctx, const void *d_packed, const uint64_t *
 
 namespace {
 // streams of at least this many bytes (after the bound below) are cut into
-// blocks and decoded in parallel (stream_split.hip); shorter ones by one wave
-constexpr uint64_t kSsMin = 256 * 1024;
+// blocks and decoded in parallel (stream_split.hip); shorter ones by one
+// workgroup (decode_mw.hip; one wave under kRmMwMin).  Device-resident
+// (tools/stream_bench.py, config-2 data, one piece): 0.32 MiB packed 0.17 ms
+// by the workgroup against 0.23 ms by the block path, 0.65 MiB 0.31 / 0.23
+constexpr uint64_t kSsMin = 384 * 1024;
 constexpr uint64_t kRmSsMin = 64 * 1024;  // cpk_read_message
 // cpk_read_message_host: streams under kRmMwMax bytes in one launch (pinned
 // memory, no DMA), by one wave (rm_small_kernel) under kRmMwMin, else by a

@@ -1,6 +1,6 @@
 """Stream decode (cpk_decode_stream / cpk_decode_stream_host): pieces back to
 back in one packed stream, each read() stopping when its piece is full
-(PackedInputStream.java:35-140, Serialize.java:165-175).  Streams of 256 KiB
+(PackedInputStream.java:35-140, Serialize.java:165-175).  Streams of 384 KiB
 and more take the parallel block path (csrc/stream_split.hip); each case is
 checked against the oracle piece by piece AND against the one-wave decoder
 (CPK_STREAM_ONE_WAVE=1), errors included.
@@ -215,7 +215,7 @@ def test_parallel_stream_garbage_matches_one_wave(ctx, oracle):
 
 @pytest.mark.parametrize("cfg", [2, 3, 4])
 def test_mid_size_stream_workgroup_path(ctx, oracle, cfg):
-    """Streams of 6-256 KiB reachable bytes take the one-workgroup decoder
+    """Streams of 6-384 KiB reachable bytes take the one-workgroup decoder
     (decode_mw.hip): one piece, ragged pieces with empty ones, junk behind
     the stream, cuts, flips and mis-sized pieces -- statuses, boundaries and
     words equal to the oracle's and to the one-wave decoder's."""

@@ -20,7 +20,7 @@ import capnp_packed as cp  # noqa: E402
 
 
 def main():
-    sizes = [int(a) for a in sys.argv[1:]] or [64]
+    sizes = [float(a) for a in sys.argv[1:]] or [64]
     if os.environ.get("SB_LIB"):  # (A/B of builds)
         cp.load(Path(os.environ["SB_LIB"]))
     ctx = cp.Context(0)
@@ -76,7 +76,7 @@ def main():
             np.array_equal(dec.view(np.int64), d_in.cpu().numpy())
         U = words * 8
         gib = 1 << 30
-        print(f"stream {P / (1 << 20):8.1f} MiB packed ({U / (1 << 20):7.1f} MiB words):"
+        print(f"stream {P / (1 << 20):8.3f} MiB packed ({U / (1 << 20):7.1f} MiB words):"
               f"  device {td * 1e3:8.3f} ms ({P / td / gib:7.1f} GiB/s packed, {U / td / gib:7.1f} GiB/s words) ok={okd}"
               f"  1-wave {t1 * 1e3:9.1f} ms ({P / t1 / gib:6.2f} GiB/s) ok={ok1}"
               f"  host {np.median(th) * 1e3:8.2f} ms ({P / np.median(th) / gib:6.2f} GiB/s packed,"
