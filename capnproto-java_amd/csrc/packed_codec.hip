@@ -1640,12 +1640,25 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     free(c);
     return CPK_ENOMEM;
   }
-  if (hipFuncSetAttribute((const void *)cpk::decode_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, cpk::kDecLds) != hipSuccess) {
-    hipFree(c->tickets);
-    free(c);
-    return CPK_EDEVICE;
-  }
+  // the kernels' dynamic LDS, above the 64 KiB default for some: set here,
+  // with the context's device current (the attribute is per device)
+  const struct {
+    const void *f;
+    uint32_t bytes;
+  } lds[] = {{(const void *)cpk::decode_kernel<false>, cpk::kDecLds},
+             {(const void *)cpk::decode_kernel<true>, cpk::kDecLds},
+             {(const void *)cpk::sp_encode_kernel<true>, cpk::kSpLds},
+             {(const void *)cpk::sp_encode_kernel<false>, cpk::kSpLds},
+             {(const void *)cpk::sp_small_kernel, cpk::kSpSmallLds},
+             {(const void *)cpk::rm_mw_kernel, cpk::kMwLds},
+             {(const void *)cpk::stream_mw_kernel, cpk::kMwLds},
+             {(const void *)cpk::ss_scan_kernel, cpk::kSsLds}};
+  for (const auto &k : lds)
+    if (hipFuncSetAttribute(k.f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)k.bytes) != hipSuccess) {
+      hipFree(c->tickets);
+      free(c);
+      return CPK_EDEVICE;
+    }
   *out = c;
   return CPK_OK;
 }
@@ -1735,16 +1748,6 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
   // (gated: the ticket was set by e4_gate_kernel -- exhausted unless the
   // batch is the single pass's)
   if (!gated && hipMemsetAsync(ctx->tickets + cpk::kTkPlan, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
-  if (cpk::kSpLds > 65536) {  // (more than the default dynamic LDS limit)
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void *)cpk::sp_encode_kernel<true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)cpk::kSpLds);
-      hipFuncSetAttribute((const void *)cpk::sp_encode_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)cpk::kSpLds);
-      attr = true;
-    }
-  }
   // (gated: both forms enqueued, the one the gate did not pick returns at once)
   const uint32_t *pick = gated ? ctx->tickets + cpk::kTkGate + 6 : nullptr;
   unsigned grid = (unsigned)(cpk::kSpWpe * ctx->cus);
@@ -2083,20 +2086,6 @@ constexpr uint64_t kRmSsMin = 64 * 1024;  // cpk_read_message
 // parallel block path 206)
 constexpr uint64_t kRmMwMin = 6 * 1024;
 constexpr uint64_t kRmMwMax = 512 * 1024;
-// (cpk_decode_stream takes the workgroup decoder for streams of
-// [kRmMwMin, kSsMin) reachable bytes)
-int mw_attr() {
-  static int rc = -1;
-  if (rc < 0) {
-    rc = hipFuncSetAttribute((const void *)cpk::rm_mw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)cpk::kMwLds) == hipSuccess &&
-                 hipFuncSetAttribute((const void *)cpk::stream_mw_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)cpk::kMwLds) == hipSuccess
-             ? 0
-             : 1;
-  }
-  return rc;
-}
 
 // the bytes a stream of `words` words may take: 10 per word at most
 uint64_t ss_reach(uint64_t avail, uint64_t words) {
@@ -2155,13 +2144,6 @@ int ss_decode(cpk_ctx ctx, const uint8_t *pk, uint64_t avail, uint64_t reach, co
   if (hipMemsetAsync(B.N2, 0, 4 * nb, s) != hipSuccess || hipMemsetAsync(B.flag, 0, 8, s) != hipSuccess ||
       hipMemsetAsync(ctx->tickets + kTkDec, 0, 8 * kTkStride * 4, s) != hipSuccess)
     return CPK_EDEVICE;
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void *)ss_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kSsLds) != hipSuccess)
-      return CPK_EDEVICE;
-    attr = true;
-  }
   const unsigned tb = 256, gb = (unsigned)((nb + tb - 1) / tb);
   const uint64_t nsub = (nb + kSsSub - 1) / kSsSub;
   hipLaunchKernelGGL(ss_scan_kernel, dim3((unsigned)ng), dim3(kSsThreads), kSsLds, s, pk, reach, swo, n, nb, B);
@@ -2206,7 +2188,6 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
   }
   if (avail >= kRmMwMin && !getenv("CPK_STREAM_ONE_WAVE")) {
     // a mid-size stream: one workgroup, its 16 waves sharing each piece's windows
-    if (mw_attr()) return CPK_EDEVICE;
     hipLaunchKernelGGL(cpk::stream_mw_kernel, dim3(1), dim3(cpk::kMwThreads), cpk::kMwLds, s,
                        (const uint8_t *)d_packed, avail, d_swo, n, (uint64_t *)d_out, d_in_off, d_status);
     return hip_ok(hipGetLastError());
@@ -2263,7 +2244,6 @@ static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, 
     // (the host path: pinned bytes, copied to the device in the kernel)
     if (info_mirror && !ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmMwMax + 128) != hipSuccess)
       return CPK_ENOMEM;
-    if (mw_attr()) return CPK_EDEVICE;
     hipLaunchKernelGGL(cpk::rm_mw_kernel, dim3(1), dim3(cpk::kMwThreads), cpk::kMwLds, s,
                        (const uint8_t *)d_packed, avail, traversal_limit_words, out_cap_words, swo, d_info, sdesc,
                        (uint64_t *)d_out, in_off, pst, send_out, info_mirror,
