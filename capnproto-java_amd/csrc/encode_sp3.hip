@@ -380,11 +380,18 @@ __device__ __forceinline__ Sp3Unit sp3_unit_at(const uint64_t *pw, uint32_t W, u
   return u;
 }
 
+// the descriptors of a batch of at most kSpArgPieces pieces, passed by value
+// (no dependent round trip to pinned memory before the first word loads)
+constexpr uint32_t kSpArgPieces = 8;
+struct SpSmallArgs {
+  uint64_t d[2 * kSpArgPieces];
+};
 __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t *__restrict__ in,
                                                                  const uint64_t *__restrict__ desc, uint32_t n,
                                                                  uint8_t *__restrict__ out,
                                                                  uint64_t *__restrict__ out_off, uint64_t ocap,
-                                                                 uint32_t *err, uint64_t *flag, uint64_t seq) {
+                                                                 uint32_t *err, uint64_t *flag, uint64_t seq,
+                                                                 SpSmallArgs da) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kSp3oLut);
   uint64_t *msk = reinterpret_cast<uint64_t *>(smem + kSp3oMsk);
@@ -397,7 +404,11 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
   if (flag) small_begin();
   // the descriptors in LDS at once (they may be host memory: one round
   // trip, not two dependent ones per piece)
-  for (uint32_t i = threadIdx.x; i < 2 * n; i += kSpThreads) ldesc[i] = desc[i];
+  if (n <= kSpArgPieces) {
+    if (threadIdx.x < 2 * n) ldesc[threadIdx.x] = da.d[threadIdx.x];
+  } else {
+    for (uint32_t i = threadIdx.x; i < 2 * n; i += kSpThreads) ldesc[i] = desc[i];
+  }
   fill_luts(lut, false);
   for (uint32_t i = threadIdx.x; i < kSp3Stage / 16; i += kSpThreads)
     reinterpret_cast<uint4 *>(stage)[i] = make_uint4(0u, 0u, 0u, 0u);

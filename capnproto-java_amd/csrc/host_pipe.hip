@@ -202,9 +202,11 @@ int small_encode(cpk_ctx ctx, uint64_t np, uint64_t words, Lay lay, void *h_out,
   uint64_t *desc = s.pin_meta, *off = desc + 2 * np;
   lay((uint64_t *)s.pin_in, desc);
   const uint64_t seq = small_arm(ctx, off + np + 1);
+  cpk::SpSmallArgs da = {};
+  if (np <= cpk::kSpArgPieces) memcpy(da.d, desc, 16 * np);
   hipLaunchKernelGGL(cpk::sp_small_kernel, dim3(1), dim3(cpk::kSpThreads), cpk::kSpSmallLds, p->sk,
                      (const uint64_t *)s.pin_in, (const uint64_t *)desc, (uint32_t)np, (uint8_t *)s.pin_out, off,
-                     ocap, ctx->tickets + cpk::kTkErr, off + np + 1, seq);
+                     ocap, ctx->tickets + cpk::kTkErr, off + np + 1, seq, da);
   if (hipGetLastError() != hipSuccess || small_wait(p->sk, off + np + 1, seq)) return CPK_EDEVICE;
   const uint64_t P = off[np];
   if (P > ocap) return CPK_EDEVICE;
