@@ -200,7 +200,8 @@ def test_read_message_mid_size_workgroup_path(ctx, oracle):
     and both dense and sparse data."""
     rng = np.random.default_rng(14)
     for cfg_probs in ((.4, .3, .2, .1), (.05, .05, .1, .8), (.9, .05, .03, .02)):
-        for sizes in ([3000], [8192 * 4], [0, 5000, 0, 12000], [int(x) for x in rng.integers(0, 6000, size=9)]):
+        for sizes in ([3000], [8192 * 4], [0, 5000, 0, 12000], [int(x) for x in rng.integers(0, 6000, size=9)],
+                      [int(x) if x > 40 else 0 for x in rng.integers(0, 400, size=300)]):
             segs, pk = _msg(rng, oracle, sizes, cfg_probs)
             if not 6 * 1024 <= len(pk) < 512 * 1024:
                 continue
