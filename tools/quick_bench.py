@@ -1,5 +1,10 @@
 """A/B timing of codec builds in one process: python tools/quick_bench.py lib1.so [lib2.so ...]
-Each lib is loaded in a subprocess-free way via ctypes (separate handles)."""
+Each lib is loaded in a subprocess-free way via ctypes (separate handles).
+Spec "lib.so@E[:K=V,...]": CPK_ENCODER=E for that library's context -- 0 the
+dense single pass (no device gate: CPK_SP_FORM is ignored), 4 the two
+passes, 5 the library's default (the device gate: single pass, its sparse
+form for mostly-zero batches, or the two passes) -- plus env knobs read at
+context creation."""
 import ctypes, sys, time
 from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
