@@ -193,6 +193,124 @@ __device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &
 
 #include "sp_roles.hip"  // SpSt, sp_roles: the run roles as mask algebra (shared with encode_sp.hip)
 
+
+// ---- size pass: roles lane-parallel over a group of <= 64 steps ------------
+// (the single pass's A2 form, encode_sp.hip sp_a2p, restated for a wave that
+// walks one piece: lane j holds step j's masks; scalar helpers read them by
+// readlane)
+struct E4Grp {
+  uint32_t zl, zh, dll, dlh, dl_, dh_;  // lane j: step j's Z / DL / D masks
+};
+__device__ __forceinline__ uint64_t e4g_z(const E4Grp &G, int j) { return sp_rl(G.zl, G.zh, j); }
+__device__ __forceinline__ uint64_t e4g_dl(const E4Grp &G, int j) { return sp_rl(G.dll, G.dlh, j); }
+__device__ __forceinline__ uint64_t e4g_d(const E4Grp &G, int j) { return sp_rl(G.dl_, G.dh_, j); }
+// first D word at or after group position x (< lim), else lim
+__device__ int e4g_first_d(const E4Grp &G, int cnt, int x, int lim) {
+  if (x >= lim) return lim;
+  int q = x >> 6;
+  uint64_t m = e4g_d(G, q) & (~0ull << (x & 63));
+  while (!m) {
+    if (++q >= cnt) return lim;
+    m = e4g_d(G, q);
+  }
+  return min(q * 64 + __builtin_ctzll(m), lim);
+}
+// the run state after the group's cnt steps (encode_sp.hip sp_state_at)
+__device__ SpSt e4g_state_after(const E4Grp &G, int cnt, SpSt cst) {
+  SpSt st = {0u, 0u, 0u};
+  const uint64_t Zp = e4g_z(G, cnt - 1), DLp = e4g_dl(G, cnt - 1);
+  if (Zp >> 63) {
+    int q = cnt - 1;
+    uint32_t zl = 0;
+    uint64_t z = Zp;
+    while (z == ~0ull) {
+      zl += 64;
+      if (--q < 0) break;
+      z = e4g_z(G, q);
+    }
+    st.zl = zl + (q >= 0 ? (uint32_t)__builtin_clzll(~z) : cst.zl);
+  }
+  if (!(DLp >> 63)) return st;
+  st.dlo = 1;
+  int q = cnt - 1;
+  uint64_t d = DLp;
+  while (d == ~0ull) {
+    if (--q < 0) break;
+    d = e4g_dl(G, q);
+  }
+  const int P = 64 * cnt;
+  int h;
+  if (q >= 0 || !cst.dlo || !cst.hd) {
+    const int start = q >= 0 ? 64 * q + 64 - __builtin_clzll(~d) : 0;
+    h = e4g_first_d(G, cnt, start, P);
+    if (h >= P) return st;
+  } else {
+    h = -(int)cst.hd;
+  }
+  for (;;) {
+    const int h2 = e4g_first_d(G, cnt, max(h + 256, 0), P);
+    if (h2 >= P) break;
+    h = h2;
+  }
+  st.hd = (uint32_t)min(P - h, 256);
+  return st;
+}
+__device__ __forceinline__ uint32_t e4g_from(uint32_t v, int src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+// the group's bytes beyond its words' nonzero bytes (tags, counts, the zero
+// byte of literal-run members); false when a D/L stretch reaching into the
+// group is longer than 192 words (the sequential form takes it)
+__device__ __forceinline__ bool e4g_bytes_par(const E4Grp &G, int cnt, uint32_t wrem, SpSt st, int lane,
+                                             uint64_t &bytes) {
+  const bool act = lane < cnt;
+  const uint64_t Z = act ? ((uint64_t)G.zl | ((uint64_t)G.zh << 32)) : 0ull;
+  const uint64_t DL = act ? ((uint64_t)G.dll | ((uint64_t)G.dlh << 32)) : 0ull;
+  const uint64_t D = act ? ((uint64_t)G.dl_ | ((uint64_t)G.dh_ << 32)) : 0ull;
+  const uint64_t below = (1ull << lane) - 1;
+  const uint32_t dlo = (uint32_t)wave_shr1((int)(uint32_t)(DL >> 63), (int)st.dlo);
+  const uint32_t topdl = DL == ~0ull ? 64u : (uint32_t)__builtin_clzll(~DL);
+  const uint64_t notall = __ballot(!act || DL != ~0ull);
+  const uint64_t kdm = notall & below;
+  const int kd = kdm ? 63 - __builtin_clzll(kdm) : -1;
+  const uint32_t topdl_k = e4g_from(topdl, kd < 0 ? 0 : kd);
+  const uint32_t len = kd >= 0 ? topdl_k + 64u * (uint32_t)(lane - 1 - kd)
+                               : (st.dlo ? st.hd : 0u) + 64u * (uint32_t)lane;
+  const bool cont = act && dlo && (DL & 1);
+  if (__ballot(cont && len > 192)) return false;
+  const uint64_t anyD = __ballot(act && D != 0);
+  const bool topd = topdl > 0 && (D >> (64 - topdl)) != 0;
+  const uint64_t TD = __ballot(act && topd);
+  const uint64_t btw = anyD & below & (kd >= 0 ? (~0ull << kd) << 1 : ~0ull);
+  const bool head = btw != 0 || (kd >= 0 ? ((TD >> kd) & 1) != 0 : (st.dlo && st.hd));
+  const uint64_t cin = (cont && head) ? 1ull : 0ull;
+  const uint64_t A = ((D << 1) | cin) & DL;
+  const uint64_t C = (DL + A) ^ DL ^ A;
+  const uint64_t Mem = DL & (A | C);
+  const uint32_t zc = (uint32_t)wave_shr1((int)(uint32_t)(Z >> 63), st.zl ? 1 : 0);
+  uint64_t Zh = Z & ~((Z << 1) | zc);
+  {
+    const uint32_t topz = Z == ~0ull ? 64u : (uint32_t)__builtin_clzll(~Z);
+    const uint64_t kzm = __ballot(!act || Z != ~0ull) & below;
+    const int kz = kzm ? 63 - __builtin_clzll(kzm) : -1;
+    const uint32_t topz_k = e4g_from(topz, kz < 0 ? 0 : kz);
+    const uint32_t zl = kz >= 0 ? topz_k + 64u * (uint32_t)(lane - 1 - kz) : st.zl + 64u * (uint32_t)lane;
+    const uint32_t j0 = (256u - (zl & 255u)) & 255u;
+    if (__ballot(act && zc && (Z & 1) && j0 < 64)) {
+      const uint64_t pre = j0 >= 63 ? ~0ull : ((2ull << j0) - 1);
+      if (act && zc && (Z & 1) && j0 < 64 && (Z & pre) == pre) Zh |= 1ull << j0;
+    }
+  }
+  const uint32_t vr = act ? wrem - 64u * (uint32_t)lane : 0u;
+  const uint64_t V = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
+  const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~V;
+  const uint32_t b = act ? (uint32_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
+                                      __builtin_popcountll(HC))
+                         : 0u;
+  bytes += (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)b), 63);
+  return true;
+}
+
 // next piece for this wave from the per-XCD counters (as the decoder)
 __device__ __forceinline__ uint32_t e4_next_piece(uint32_t *ticket, int &xq, int &dry, uint32_t n) {
   uint32_t seg;
@@ -229,8 +347,12 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     // adds at most one partial step)
     uint64_t *bvp = bvbuf + (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
     const uint64_t rows = stride ? stride : ~0ull;  // (a piece over the hint: error, no rows)
-    E4St st = {2, 0, 0};
-    int gl = 2;
+    // run state entering each group of 64 steps (the single pass's SpSt),
+    // the previous step's last-word classes for the boundaries
+    SpSt st = {0u, 0u, 0u};
+    uint32_t zprev = 0, dlprev = 0;
+    uint64_t bytes = 0;
+    E4Grp G = {0u, 0u, 0u, 0u, 0u, 0u};
     uint32_t acc = 0;
     // (32-bit step / word indices: a piece is at most 2^31 words, Serialize
     // limits segments to 2^29 - 1, Serialize.java:45-53)
@@ -250,27 +372,69 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     for (uint32_t s0 = 0; s0 < nsteps; s0 += PF) {
 #pragma unroll
       for (int j = 0; j < PF; ++j) vn[j] = src[min(((s0 + PF + j) << 6) + lane, kl)];
-      uint64_t x = ~0ull;  // lane j keeps step s0 + j's boundary row
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
         const uint32_t k = ((s0 + j) << 6) + lane;
         const bool valid = k < W32;
         if (s0 + j < nsteps) {
-          const E4Cls c = e4_classify(v[j], valid, gl);
-          const E4Role r = e4_roles(e4_tag(v[j]), valid, c, st, lane, lem);
-          acc += r.nb;
-          x = lane == j ? c.BV : x;
+          // per word its tag and nonzero bytes; per step, into lane
+          // (s0 + j) & 63, the zero-word / <= 1 zero byte / tag-0xff masks
+          const uint32_t m = valid ? e4_tag(v[j]) : 0u;
+          const uint32_t pc = (uint32_t)__builtin_popcount(m);
+          acc += pc;
+          const uint64_t Z = __ballot(valid && m == 0), DL = __ballot(pc >= 7), D = __ballot(m == 0xffu);
+          const int jj = (int)((s0 + j) & 63);
+          G.zl = sp_wl(G.zl, (uint32_t)Z, jj);
+          G.zh = sp_wl(G.zh, (uint32_t)(Z >> 32), jj);
+          G.dll = sp_wl(G.dll, (uint32_t)DL, jj);
+          G.dlh = sp_wl(G.dlh, (uint32_t)(DL >> 32), jj);
+          G.dl_ = sp_wl(G.dl_, (uint32_t)D, jj);
+          G.dh_ = sp_wl(G.dh_, (uint32_t)(D >> 32), jj);
         }
       }
-      // the group's boundary rows for the emit pass: lanes 0..PF-1, one store
-      if (lane < PF && s0 + lane < nsteps && s0 + lane < rows) bvp[s0 + lane] = x;
+      if (((s0 + PF) & 63) == 0 || s0 + PF >= nsteps) {
+        // a group of 64 steps (or the piece's last): its roles and bytes
+        // lane-parallel, its boundary rows, the state it leaves
+        const uint32_t g0 = s0 & ~63u;
+        const int cnt = (int)min(64u, nsteps - g0);
+        const uint32_t wrem = W32 - 64u * g0;
+        if (e4g_bytes_par(G, cnt, wrem, st, lane, bytes)) {
+          st = e4g_state_after(G, cnt, st);
+        } else {
+          for (int j = 0; j < cnt; ++j) {
+            const uint64_t Z = e4g_z(G, j), DL = e4g_dl(G, j), D = e4g_d(G, j);
+            const uint32_t vr = wrem - 64u * (uint32_t)j;
+            const uint64_t V = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
+            uint64_t Zh, Mem;
+            sp_roles(Z, DL, D, st, Zh, Mem);
+            const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~V;
+            bytes += (uint64_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
+                                __builtin_popcountll(HC));
+          }
+        }
+        // run boundaries for the emit pass (e4_classify's BV): past the
+        // piece's end, every M word, each zero run / D/L stretch's first word
+        {
+          const bool act = lane < cnt;
+          const uint64_t Z = act ? ((uint64_t)G.zl | ((uint64_t)G.zh << 32)) : 0ull;
+          const uint64_t DL = act ? ((uint64_t)G.dll | ((uint64_t)G.dlh << 32)) : 0ull;
+          const uint32_t vr = act ? wrem - 64u * (uint32_t)lane : 0u;
+          const uint64_t V = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
+          const uint64_t zp = (uint32_t)wave_shr1((int)(uint32_t)(Z >> 63), (int)zprev);
+          const uint64_t dp = (uint32_t)wave_shr1((int)(uint32_t)(DL >> 63), (int)dlprev);
+          const uint64_t BV = ~V | (V & ~Z & ~DL) | (Z & ~((Z << 1) | zp)) | (DL & ~((DL << 1) | dp));
+          if (act && g0 + lane < rows) bvp[g0 + lane] = BV;
+          zprev = (uint32_t)(e4g_z(G, cnt - 1) >> 63);
+          dlprev = (uint32_t)(e4g_dl(G, cnt - 1) >> 63);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < PF; ++j) v[j] = vn[j];
     }
     // wave sum in two 16-bit halves (a piece's packed size may pass 2^31)
     const uint32_t thi = (uint32_t)wave_incl_add((int)(acc >> 16));
     const uint32_t tlo = (uint32_t)wave_incl_add((int)(acc & 0xffffu));
-    if (lane == 63) sizes[seg] = ((uint64_t)thi << 16) + tlo;
+    if (lane == 63) sizes[seg] = ((uint64_t)thi << 16) + tlo + bytes;
   }
 }
 
