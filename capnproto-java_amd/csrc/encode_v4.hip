@@ -23,6 +23,11 @@ constexpr uint32_t kE4oLut = 0;                                   // u64[256]
 constexpr uint32_t kE4oRing = 2048;                               // u32[waves][512]
 constexpr uint32_t kE4Lds = kE4oRing + kE4Waves * kE4RingBytes;   // 10 KiB
 
+// the size pass's row per 64-word step for the emit pass: run boundaries,
+// literal-run members, heads (3 u64); at most 4 GiB of rows
+constexpr uint64_t kE4RowBytes = 24;
+constexpr uint64_t kE4MaxRows = (1ull << 32) / kE4RowBytes;
+
 constexpr uint32_t kE4RingLines = kE4RingBytes / 16;
 constexpr uint32_t kE4RingDw = kE4RingBytes / 4;
 
@@ -74,121 +79,9 @@ __device__ __forceinline__ void e4_flush(uint8_t *out, uint32_t *ring, uint64_t 
 
 constexpr int kE4Wpe = 8;
 
-// Run state entering a step (wave-uniform): g 0 zero run, 1 D/L stretch,
-// 2 none (piece start or after an M word); len: words of the run before the
-// step; hd: D/L stretch only, words since its last 0xFF head (capped at 256),
-// 0 = no head yet (PackedOutputStream.java:143-161).
-struct E4St {
-  int g, len, hd;
-};
-
-// Classification of one step: BV = run boundaries (a word whose run starts
-// there: group change, every M word, the piece's first word) plus the words
-// past the piece's end, and the D words (tag 0xff).  (A valid word's masks
-// below it never hold a past-the-end word, so BV serves as the boundaries.)
-struct E4Cls {
-  uint64_t D, BV;
-  int gl;  // group of the step's last word (2: M, or past the end)
-};
-
+// word group: 0 zero word, 1 D/L (<= 1 zero byte), 2 M, 3 past the piece's end
 __device__ __forceinline__ int e4_group(uint32_t m, bool valid) {
   return !valid ? 3 : (m == 0 ? 0 : (__builtin_popcount(m) >= 7 ? 1 : 2));
-}
-
-// gl: group of the word before the step (2 at the piece start); updated to
-// the group of the step's last word (2 for M or past the end)
-__device__ __forceinline__ E4Cls e4_classify(uint64_t word, bool valid, int &gl) {
-  const uint32_t m = e4_tag(word);
-  const int g = e4_group(m, valid);
-  const int gp = wave_shr1(g, gl);
-  E4Cls c;
-  c.BV = __ballot(!valid || g != gp || g == 2);
-  c.D = __ballot(valid && m == 0xffu);
-  const int g63 = __builtin_amdgcn_readlane(g, 63);
-  gl = min(g63, 2);  // (3, past the end, counts as 2)
-  c.gl = gl;
-  return c;
-}
-
-// Roles of one step's words (lane = word; PackedOutputStream.java:119-193
-// restated per word, as encode_kernel's pass 2):
-//   Z word: a 0x00 head every 256 words from its zero run's start (2 bytes);
-//   M word: 1 + popcount bytes;
-//   D/L word: a member of the 0xFF run of the stretch's last head (8 bytes
-//   verbatim) if one lies within 255 words before it, else a head (D: 10
-//   bytes with the count, L: 8).
-// nb = packed bytes, memb / head flags; st advances to the next step.
-struct E4Role {
-  uint32_t nb, memb, head;
-};
-// per lane: mask bit set ? b : a, as one v_cndmask
-__device__ __forceinline__ int e4_vsel(int a, int b, uint64_t mask) {
-  int r;
-  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(mask));
-  return r;
-}
-__device__ __forceinline__ E4Role e4_roles(uint32_t m, bool valid, const E4Cls &c, E4St &st,
-                                           int lane, uint64_t lem) {
-  const int g = e4_group(m, valid);
-  // this lane's run start (step-relative; the carried run started st.len
-  // words before the step) and the last D before this lane
-  // (__clzll(0) = 64: the highest set bit is -1 for an empty mask; the
-  // selects are forced v_cndmasks: hipcc otherwise branches on the mask)
-  const uint64_t bl = c.BV & lem, dl = c.D & (lem >> 1);
-  const int rs = e4_vsel(63 - __clzll((long long)bl), -st.len, __ballot(bl == 0));
-  const int lastD = e4_vsel(63 - __clzll((long long)dl), st.hd > 0 ? -st.hd : -(1 << 30),
-                            __ballot(dl == 0));
-  const uint32_t zh = (g == 0 && ((lane - rs) & 255) == 0) ? 1u : 0u;
-  uint32_t memb = (g == 1 && lastD >= rs) ? 1u : 0u;
-  uint32_t dh = (valid && m == 0xffu && !memb) ? 1u : 0u;
-  int h1 = -1;
-  // (st.len + f > 256 needs st.len > 192: f, the first boundary, is <= 64)
-  if (st.g == 1 && st.len > 192) {
-   const int f = c.BV ? __builtin_ctzll(c.BV) : 64;  // words [0, f) continue the carried run
-   if (st.len + f > 256) {
-    // the carried stretch is longer than 256 words: members lie within 255
-    // words after a head, the next head is the first D 256 or more words
-    // after the last (:143-161)
-    const uint64_t rng = f >= 64 ? ~0ull : ((1ull << f) - 1);
-    uint64_t mc = 0;
-    if (st.hd > 0 && st.hd <= 255) {
-      const int me = 255 - st.hd;
-      mc = me >= 63 ? ~0ull : ((2ull << me) - 1);
-    }
-    const int js = st.hd > 0 ? max(0, 256 - st.hd) : 0;
-    const uint64_t dc = js >= 64 ? 0ull : (c.D & rng & (~0ull << js));
-    if (dc) {
-      h1 = __builtin_ctzll(dc);
-      mc |= h1 == 63 ? 0ull : (~0ull << (h1 + 1));
-    }
-    // (words of the carried stretch, all D/L; selects, not a branch)
-    const bool inr = (rng >> lane) & 1;
-    memb = inr ? (uint32_t)((mc >> lane) & 1) : memb;
-    dh = inr ? (h1 == lane ? 1u : 0u) : dh;
-   }
-  }
-  E4Role r;
-  // (a sum of selects: nested per-lane ternaries become branches)
-  r.nb = (g == 2 ? 1u + __builtin_popcount(m) : 0u) + (g == 1 ? 8u + 2u * dh : 0u) +
-         (g == 0 ? 2u * zh : 0u);
-  r.memb = memb;
-  r.head = zh | dh;
-  // the run state entering the next step (past the piece's end: unused)
-  if (c.BV) {
-    const int lb = 63 - __builtin_clzll(c.BV);
-    st.g = c.gl;
-    st.len = 64 - lb;
-    const uint64_t dd = c.D & (~0ull << lb);  // (a D there means a D/L run)
-    st.hd = dd ? 64 - __builtin_ctzll(dd) : 0;
-  } else if (st.g != 2) {
-    st.len += 64;
-    if (st.g == 1) {
-      if (h1 >= 0) st.hd = 64 - h1;
-      else if (st.hd > 0) st.hd = min(st.hd + 64, 256);
-      else st.hd = c.D ? 64 - __builtin_ctzll(c.D) : 0;
-    }
-  }
-  return r;
 }
 
 #include "sp_roles.hip"  // SpSt, sp_roles: the run roles as mask algebra (shared with encode_sp.hip)
@@ -262,7 +155,7 @@ __device__ __forceinline__ uint32_t e4g_from(uint32_t v, int src) {
 // byte of literal-run members); false when a D/L stretch reaching into the
 // group is longer than 192 words (the sequential form takes it)
 __device__ __forceinline__ bool e4g_bytes_par(const E4Grp &G, int cnt, uint32_t wrem, SpSt st, int lane,
-                                             uint64_t &bytes) {
+                                             uint64_t &bytes, uint64_t &memo, uint64_t &hco) {
   const bool act = lane < cnt;
   const uint64_t Z = act ? ((uint64_t)G.zl | ((uint64_t)G.zh << 32)) : 0ull;
   const uint64_t DL = act ? ((uint64_t)G.dll | ((uint64_t)G.dlh << 32)) : 0ull;
@@ -308,6 +201,8 @@ __device__ __forceinline__ bool e4g_bytes_par(const E4Grp &G, int cnt, uint32_t 
                                       __builtin_popcountll(HC))
                          : 0u;
   bytes += (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)b), 63);
+  memo = Mem;
+  hco = HC;
   return true;
 }
 
@@ -329,7 +224,6 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip) {
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;  // (the single pass took the batch)
   const int lane = lane_id();
-  const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
   int xq = xcc_id(), dry = 0;
   for (;;) {
     const uint32_t seg = e4_next_piece(ticket, xq, dry, n);
@@ -345,7 +239,7 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     // this piece's step rows in bvbuf: `stride` rows per piece when the
     // size hint bounds them, else packed by word offset (disjoint: a piece
     // adds at most one partial step)
-    uint64_t *bvp = bvbuf + (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
+    uint64_t *bvp = bvbuf + 3 * (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
     const uint64_t rows = stride ? stride : ~0ull;  // (a piece over the hint: error, no rows)
     // run state entering each group of 64 steps (the single pass's SpSt),
     // the previous step's last-word classes for the boundaries
@@ -398,9 +292,12 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
         const uint32_t g0 = s0 & ~63u;
         const int cnt = (int)min(64u, nsteps - g0);
         const uint32_t wrem = W32 - 64u * g0;
-        if (e4g_bytes_par(G, cnt, wrem, st, lane, bytes)) {
+        // lane j: step j's literal-run members and heads (the emit pass's roles)
+        uint64_t MemL = 0, HCL = 0;
+        if (e4g_bytes_par(G, cnt, wrem, st, lane, bytes, MemL, HCL)) {
           st = e4g_state_after(G, cnt, st);
         } else {
+          uint32_t ml = 0, mh = 0, hl = 0, hh = 0;
           for (int j = 0; j < cnt; ++j) {
             const uint64_t Z = e4g_z(G, j), DL = e4g_dl(G, j), D = e4g_d(G, j);
             const uint32_t vr = wrem - 64u * (uint32_t)j;
@@ -410,7 +307,13 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
             const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~V;
             bytes += (uint64_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
                                 __builtin_popcountll(HC));
+            ml = sp_wl(ml, (uint32_t)Mem, j);
+            mh = sp_wl(mh, (uint32_t)(Mem >> 32), j);
+            hl = sp_wl(hl, (uint32_t)HC, j);
+            hh = sp_wl(hh, (uint32_t)(HC >> 32), j);
           }
+          MemL = ((uint64_t)mh << 32) | ml;
+          HCL = ((uint64_t)hh << 32) | hl;
         }
         // run boundaries for the emit pass (e4_classify's BV): past the
         // piece's end, every M word, each zero run / D/L stretch's first word
@@ -423,7 +326,12 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
           const uint64_t zp = (uint32_t)wave_shr1((int)(uint32_t)(Z >> 63), (int)zprev);
           const uint64_t dp = (uint32_t)wave_shr1((int)(uint32_t)(DL >> 63), (int)dlprev);
           const uint64_t BV = ~V | (V & ~Z & ~DL) | (Z & ~((Z << 1) | zp)) | (DL & ~((DL << 1) | dp));
-          if (act && g0 + lane < rows) bvp[g0 + lane] = BV;
+          if (act && g0 + lane < rows) {
+            uint64_t *row = bvp + 3ull * (g0 + lane);
+            row[0] = BV;
+            row[1] = MemL;
+            row[2] = HCL;
+          }
           zprev = (uint32_t)(e4g_z(G, cnt - 1) >> 63);
           dlprev = (uint32_t)(e4g_dl(G, cnt - 1) >> 63);
         }
@@ -526,38 +434,33 @@ __global__ __launch_bounds__(kE4ScanThreads) void e4_scan_down(const uint64_t *_
 }
 
 // ---- pass 2: the packed bytes ----------------------------------------------------
-// One step of the emit walk.  c[0] is this step's classification, bv1..bv4
-// the boundaries of the next four steps (for the counts of heads whose run
-// reaches past this step).
+// One step of the emit walk.  bv0..bv4: the run boundaries of this step and
+// the next four (for the counts of heads whose run reaches past this step);
+// mem / hc: this step's literal-run members and heads, all three from the
+// size pass's rows.
 __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t bv0,
                                              uint64_t bv1, uint64_t bv2, uint64_t bv3,
-                                             uint64_t bv4, E4St &st, int lane, uint64_t lem,
+                                             uint64_t bv4, uint64_t mem, uint64_t hc, int lane,
                                              const uint64_t *lut, uint32_t *ring, uint8_t *out,
                                              uint64_t &rpos, uint64_t &fl, uint64_t obase) {
   const uint32_t m = e4_tag(word);
-  // this step's classification: the boundaries came with the look-ahead
-  // (only they are kept for 4 steps: SGPR pressure), D and the last group
-  // are recomputed here
-  E4Cls c;
-  c.BV = bv0;
-  c.D = __ballot(valid && m == 0xffu);
-  {
-    const int g63 = __builtin_amdgcn_readlane(e4_group(m, valid), 63);
-    c.gl = min(g63, 2);
-  }
-  const E4Role r = e4_roles(m, valid, c, st, lane, lem);
+  const int g = e4_group(m, valid);
+  const uint32_t memb = (uint32_t)(mem >> lane) & 1u, head = (uint32_t)(hc >> lane) & 1u;
   // a head's count: words to its run's end, at most 255 (:123-131, :143-164)
   uint32_t cnt = 0;
-  if (__ballot(r.head)) {
+  if (hc) {
     const uint64_t gtm = lane == 63 ? 0ull : (~0ull << (lane + 1));
-    const uint64_t bb = c.BV & gtm;
+    const uint64_t bb = bv0 & gtm;
     const int nbr = bv1 ? 64 + __builtin_ctzll(bv1)
                         : bv2 ? 128 + __builtin_ctzll(bv2)
                               : bv3 ? 192 + __builtin_ctzll(bv3)
                                     : bv4 ? 256 + __builtin_ctzll(bv4) : 320;
     const int re = bb ? __builtin_ctzll(bb) : nbr;
-    cnt = r.head ? (uint32_t)min(255, re - lane - 1) : 0u;
+    cnt = head ? (uint32_t)min(255, re - lane - 1) : 0u;
   }
+  // bytes: M 1 + popcount, D/L 8 (a member verbatim, an L head tag + 7),
+  // + 2 for a head's count byte and (Z) tag / (D) extra byte
+  const uint32_t nb = (g == 2 ? 1u + __builtin_popcount(m) : 0u) + (g == 1 ? 8u : 0u) + 2u * head;
   // the string: tag, the nonzero bytes (v_perm with the compaction LUT), the
   // count after a 0x00 / 0xFF tag; a literal-run member is its 8 bytes (:163-171)
   const uint32_t lo = (uint32_t)word, hi = (uint32_t)(word >> 32);
@@ -568,12 +471,11 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
   uint32_t s0 = m | (c0p << 8);
   uint32_t s1 = __builtin_amdgcn_alignbyte(c1, c0p, 3);
   uint32_t s2 = __builtin_amdgcn_alignbyte(m == 0xffu ? cnt : 0u, c1, 3);
-  if (r.memb) {
+  if (memb) {
     s0 = lo;
     s1 = hi;
     s2 = 0;
   }
-  const uint32_t nb = r.nb;
   const int incl = wave_incl_add((int)nb);
   const uint32_t o = (uint32_t)incl - nb;
   const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
@@ -617,7 +519,6 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
   for (uint32_t i = lane; i < kE4RingLines; i += 64)
     reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
-  const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
   int xq = xcc_id(), dry = 0;
   for (;;) {
     const uint32_t seg = e4_next_piece(ticket, xq, dry, n);
@@ -628,13 +529,12 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     const uint64_t *src = in + w0;
     const uint64_t obase = out_off[seg];
     uint64_t rpos = obase, fl = obase >> 4;
-    E4St st = {2, 0, 0};
     // the boundaries of every step come from the size pass (bvbuf); past
     // the piece every word is a boundary.  Words: this group of four steps
     // and the next one's loads in flight.
     const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;  // (pieces < 2^31 words)
     if (stride && nsteps > stride) continue;  // over the size hint: reported, output undefined
-    const uint64_t *bvp = bvbuf + (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
+    const uint64_t *bvp = bvbuf + 3 * (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
     uint64_t vc[4], vl[4];
     const uint32_t kl = W32 - 1;  // loads clamped, not predicated
 #pragma unroll
@@ -642,14 +542,19 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     for (uint32_t s0 = 0; s0 < nsteps; s0 += 4) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) vl[j] = E4_LD2(src + min(((s0 + 4 + j) << 6) + lane, kl));
-      uint64_t bv[8];
+      uint64_t bv[8], mem[4], hc[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bv[j] = s0 + j < nsteps ? bvp[s0 + j] : ~0ull;
+      for (int j = 0; j < 8; ++j) bv[j] = s0 + j < nsteps ? bvp[3 * (s0 + j)] : ~0ull;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mem[j] = s0 + j < nsteps ? bvp[3 * (s0 + j) + 1] : 0ull;
+        hc[j] = s0 + j < nsteps ? bvp[3 * (s0 + j) + 2] : 0ull;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         if (s0 + j < nsteps)
           e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W32, bv[j], bv[j + 1], bv[j + 2], bv[j + 3],
-                       bv[j + 4], st, lane, lem, lut, ring, out, rpos, fl, obase);
+                       bv[j + 4], mem[j], hc[j], lane, lut, ring, out, rpos, fl, obase);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) vc[j] = vl[j];

@@ -1488,8 +1488,8 @@ struct cpk_ctx_s {
   uint32_t sp_epoch;      //   launch epoch tagging the look-back words, 1..65535
   uint64_t *sp_desc;      //   message batches: piece descriptors | segment tables
   uint64_t sp_desc_cap;   //   u64 entries
-  uint64_t *e4_bv;        // encoder v4: run boundaries per 64-word step
-  uint64_t e4_bv_cap;     //   entries
+  uint64_t *e4_bv;        // encoder v4: per 64-word step its run boundaries, members, heads
+  uint64_t e4_bv_cap;     //   steps (kE4RowBytes each)
   HostPipe *pipe;         // cpk_encode_host / cpk_decode_host staging (lazy)
   uint64_t *ss_buf;       // parallel stream decode scratch (stream_split.hip)
   uint64_t ss_cap;        //   u64 entries
@@ -1792,7 +1792,7 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
   int rc = ensure_status(ctx, (uint64_t)n + nb + 1);
   if (rc) return rc;
   uint64_t stride = hint ? (hint + 63) / 64 : 0, rows;
-  if (stride && stride > (1ull << 29) / n) stride = 0;  // (> 4 GiB of rows: pack them; no overflow)
+  if (stride && stride > cpk::kE4MaxRows / n) stride = 0;  // (> 4 GiB of rows: pack them; no overflow)
   if (stride) {
     rows = (uint64_t)n * stride;
   } else {
@@ -1808,7 +1808,7 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
     ctx->e4_bv = nullptr;
     ctx->e4_bv_cap = 0;
     const uint64_t cap = rows + rows / 4;
-    if (hipMalloc(&ctx->e4_bv, cap * 8) != hipSuccess) return CPK_ENOMEM;
+    if (hipMalloc(&ctx->e4_bv, cap * cpk::kE4RowBytes) != hipSuccess) return CPK_ENOMEM;
     ctx->e4_bv_cap = cap;
   }
   uint64_t *sizes = ctx->status, *bsum = ctx->status + n;
@@ -1886,14 +1886,14 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
   uint64_t *ssize = ctx->status, *tsize = ssize + nseg, *comb = tsize + nm, *soff = comb + np;
   uint64_t *bsum = soff + nseg;
   uint64_t stride = (max_seg_words + 63) / 64;
-  if (nseg && stride > (1ull << 29) / nseg) return CPK_EUNSUPPORTED;  // (> 4 GiB of step rows)
+  if (nseg && stride > cpk::kE4MaxRows / nseg) return CPK_EUNSUPPORTED;  // (> 4 GiB of step rows)
   const uint64_t rows = (uint64_t)(nseg ? nseg : 1) * stride;
   if (rows > ctx->e4_bv_cap) {
     if (ctx->e4_bv) hipFree(ctx->e4_bv);
     ctx->e4_bv = nullptr;
     ctx->e4_bv_cap = 0;
     const uint64_t cap = rows + rows / 4;
-    if (hipMalloc(&ctx->e4_bv, cap * 8) != hipSuccess) return CPK_ENOMEM;
+    if (hipMalloc(&ctx->e4_bv, cap * cpk::kE4RowBytes) != hipSuccess) return CPK_ENOMEM;
     ctx->e4_bv_cap = cap;
   }
   if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
