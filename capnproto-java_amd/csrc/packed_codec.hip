@@ -1781,20 +1781,17 @@ static uint64_t sp_unit_bound(uint64_t n, uint64_t hint) {
   return n * per;
 }
 
-// Encoder v4 (encode_v4.hip): size pass, scan, emit pass.  Pieces of any
-// size; a piece over the hint is reported (output undefined).  The size pass
-// leaves each 64-word step's run boundaries for the emit pass: `stride` rows
-// per piece from the hint, or packed by word offset when there is no hint (the
-// batch's word count is then read back, synchronising the stream).
-int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, uint64_t hint,
-              void *d_out, uint64_t *d_out_off, hipStream_t s, bool gate = false) {
-  const uint32_t nb = (uint32_t)((n + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
-  int rc = ensure_status(ctx, (uint64_t)n + nb + 1);
-  if (rc) return rc;
-  uint64_t stride = hint ? (hint + 63) / 64 : 0, rows;
-  if (stride && stride > cpk::kE4MaxRows / n) stride = 0;  // (> 4 GiB of rows: pack them; no overflow)
+// The size pass's rows for the emit pass (kE4RowBytes per 64-word step):
+// `stride` rows per piece from the hint when they fit in 4 GiB, else packed
+// by word offset (stride 0: the batch's word count is read back, synchronising
+// the stream)
+static int e4_rows(cpk_ctx ctx, const uint64_t *d_swo, uint32_t n, uint64_t hint, hipStream_t s,
+                   uint64_t &stride) {
+  stride = hint ? (hint + 63) / 64 : 0;
+  if (stride && stride > cpk::kE4MaxRows / (n ? n : 1)) stride = 0;  // (no overflow)
+  uint64_t rows;
   if (stride) {
-    rows = (uint64_t)n * stride;
+    rows = (uint64_t)(n ? n : 1) * stride;
   } else {
     uint64_t ends[2];
     if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1811,6 +1808,22 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
     if (hipMalloc(&ctx->e4_bv, cap * cpk::kE4RowBytes) != hipSuccess) return CPK_ENOMEM;
     ctx->e4_bv_cap = cap;
   }
+  return CPK_OK;
+}
+
+// Encoder v4 (encode_v4.hip): size pass, scan, emit pass.  Pieces of any
+// size; a piece over the hint is reported (output undefined).  The size pass
+// leaves each 64-word step's run boundaries for the emit pass: `stride` rows
+// per piece from the hint, or packed by word offset when there is no hint (the
+// batch's word count is then read back, synchronising the stream).
+int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, uint64_t hint,
+              void *d_out, uint64_t *d_out_off, hipStream_t s, bool gate = false) {
+  const uint32_t nb = (uint32_t)((n + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
+  int rc = ensure_status(ctx, (uint64_t)n + nb + 1);
+  if (rc) return rc;
+  uint64_t stride;
+  rc = e4_rows(ctx, d_swo, n, hint, s, stride);
+  if (rc) return rc;
   uint64_t *sizes = ctx->status, *bsum = ctx->status + n;
   if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
   if (gate) {
@@ -1885,17 +1898,9 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
   if (rc) return rc;
   uint64_t *ssize = ctx->status, *tsize = ssize + nseg, *comb = tsize + nm, *soff = comb + np;
   uint64_t *bsum = soff + nseg;
-  uint64_t stride = (max_seg_words + 63) / 64;
-  if (nseg && stride > cpk::kE4MaxRows / nseg) return CPK_EUNSUPPORTED;  // (> 4 GiB of step rows)
-  const uint64_t rows = (uint64_t)(nseg ? nseg : 1) * stride;
-  if (rows > ctx->e4_bv_cap) {
-    if (ctx->e4_bv) hipFree(ctx->e4_bv);
-    ctx->e4_bv = nullptr;
-    ctx->e4_bv_cap = 0;
-    const uint64_t cap = rows + rows / 4;
-    if (hipMalloc(&ctx->e4_bv, cap * cpk::kE4RowBytes) != hipSuccess) return CPK_ENOMEM;
-    ctx->e4_bv_cap = cap;
-  }
+  uint64_t stride;
+  rc = e4_rows(ctx, d_swo, nseg, max_seg_words, s, stride);
+  if (rc) return rc;
   if (hipMemsetAsync(ctx->tickets, 0, cpk::kTkErr * 4, s) != hipSuccess) return CPK_EDEVICE;
   const unsigned tb = 256, tg = (nm + tb - 1) / tb;
   unsigned grid = (unsigned)(8 * ctx->cus);

@@ -576,10 +576,13 @@ def test_decode_messages_matches_serialize_read(ctx, oracle):
     assert {oracle.OK, oracle.ETRAILING, oracle.ETRUNC, cp.EFRAME} <= kinds, kinds
 
 
-def test_encode_messages_matches_serialize_write(ctx, oracle):
+@pytest.mark.parametrize("hint", ["exact", "huge"])
+def test_encode_messages_matches_serialize_write(ctx, oracle, hint):
     """cpk_encode_messages (segment tables built and packed on the device)
     == SerializePacked.write per message, back to back; then the device
-    message decode reads them back."""
+    message decode reads them back.  hint "huge": a max_seg_words of 2^30,
+    whose per-segment step rows would pass 4 GiB, so the two-pass encoder
+    packs them by word offset instead."""
     import torch
     import capnp_packed as cp
     rng = np.random.default_rng(41)
@@ -600,7 +603,7 @@ def test_encode_messages_matches_serialize_write(ctx, oracle):
     cap = cp.batch_capacity(swo) + sum(10 * ((len(m) + 2) // 2 + 1) for m in msgs)
     d_pk = torch.zeros((cap + 63) // 16 * 16, dtype=torch.uint8, device="cuda")
     d_off = torch.zeros(len(msgs) + len(segs) + 1, dtype=torch.int64, device="cuda")
-    maxw = int(max(np.diff(swo)))
+    maxw = int(max(np.diff(swo))) if hint == "exact" else 1 << 30
     ctx.encode_messages(d_in, d_swo, d_mseg, maxw, d_pk, d_off)
     assert ctx.take_error() == cp.OK
     off = d_off.cpu().numpy()
