@@ -256,6 +256,7 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     // steps of loads in flight ahead of the size pass's classification (8:
     // config-3 messages' e4 encode 7.06 -> 7.00 ms, config 2 6.39 -> 6.29
     // against 4, r4K_ab.log; 64 VGPRs, no spill at 8 workgroups per CU)
+    // (4 and 16 measured neutral / +15 %, r4AL_ab.log)
     constexpr int PF = 8;
     uint64_t v[PF], vn[PF];
     // loads clamped to the piece's last word, not predicated (no exec-mask
@@ -535,29 +536,32 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;  // (pieces < 2^31 words)
     if (stride && nsteps > stride) continue;  // over the size hint: reported, output undefined
     const uint64_t *bvp = bvbuf + 3 * (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
-    uint64_t vc[4], vl[4];
+    // steps of loads in flight ahead of the emit (2 and 8 measured 1-2 %
+    // slower, r4AL_ab.log)
+    constexpr int EPF = 4;
+    uint64_t vc[EPF], vl[EPF];
     const uint32_t kl = W32 - 1;  // loads clamped, not predicated
 #pragma unroll
-    for (int j = 0; j < 4; ++j) vc[j] = E4_LD2(src + min(((uint32_t)j << 6) + lane, kl));
-    for (uint32_t s0 = 0; s0 < nsteps; s0 += 4) {
+    for (int j = 0; j < EPF; ++j) vc[j] = E4_LD2(src + min(((uint32_t)j << 6) + lane, kl));
+    for (uint32_t s0 = 0; s0 < nsteps; s0 += EPF) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) vl[j] = E4_LD2(src + min(((s0 + 4 + j) << 6) + lane, kl));
-      uint64_t bv[8], mem[4], hc[4];
+      for (int j = 0; j < EPF; ++j) vl[j] = E4_LD2(src + min(((s0 + EPF + j) << 6) + lane, kl));
+      uint64_t bv[EPF + 4], mem[EPF], hc[EPF];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bv[j] = s0 + j < nsteps ? bvp[3 * (s0 + j)] : ~0ull;
+      for (int j = 0; j < EPF + 4; ++j) bv[j] = s0 + j < nsteps ? bvp[3 * (s0 + j)] : ~0ull;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < EPF; ++j) {
         mem[j] = s0 + j < nsteps ? bvp[3 * (s0 + j) + 1] : 0ull;
         hc[j] = s0 + j < nsteps ? bvp[3 * (s0 + j) + 2] : 0ull;
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < EPF; ++j) {
         if (s0 + j < nsteps)
           e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W32, bv[j], bv[j + 1], bv[j + 2], bv[j + 3],
                        bv[j + 4], mem[j], hc[j], lane, lut, ring, out, rpos, fl, obase);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) vc[j] = vl[j];
+      for (int j = 0; j < EPF; ++j) vc[j] = vl[j];
     }
     wave_lds_order();
     e4_flush(out, ring, fl, rpos >> 4, obase, lane);
