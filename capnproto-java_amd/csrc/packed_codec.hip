@@ -634,12 +634,15 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
       const int wbase = ow + rb + kBlk * b;  // piece word of the block's first word
       const int wleft = ow + T - wbase - 1;   // words of the window after the block's first
       uint64_t words[kBlk];
+      // (the record's tag and count bytes are read once per record, not per
+      // word: a literal run's words then need only their own reads, all in
+      // flight together)
+      uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
 #pragma unroll
       for (int i = 0; i < kBlk; ++i) {
         // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
         // run (tag word, then the counted words), or a tagged word
         // (the count bytes are read with the tag: one LDS round trip)
-        uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
         uint64_t x;
         int nw;
         uint32_t adv;
@@ -667,6 +670,11 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         if (++ofs == nw && i < wleft) {
           q += adv;
           ofs = 0;
+          if (i + 1 < kBlk) {
+            tag = pkw[q];
+            c1 = pkw[q + 1];
+            c9 = pkw[q + 9];
+          }
         }
       }
       const int kw = min(kBlk, min(ow + T, W) - wbase);
