@@ -152,10 +152,11 @@ __device__ __forceinline__ uint32_t e4g_from(uint32_t v, int src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
 // the group's bytes beyond its words' nonzero bytes (tags, counts, the zero
-// byte of literal-run members); false when a D/L stretch reaching into the
-// group is longer than 192 words (the sequential form takes it)
-__device__ __forceinline__ bool e4g_bytes_par(const E4Grp &G, int cnt, uint32_t wrem, SpSt st, int lane,
-                                             uint64_t &bytes, uint64_t &memo, uint64_t &hco) {
+// byte of literal-run members).  Returns the steps it leaves out: those a D/L
+// stretch enters longer than 192 words (its heads may chain within the step;
+// the caller takes them one at a time, sp_roles on the state there)
+__device__ __forceinline__ uint64_t e4g_bytes_par(const E4Grp &G, int cnt, uint32_t wrem, SpSt st, int lane,
+                                                 uint64_t &bytes, uint64_t &memo, uint64_t &hco) {
   const bool act = lane < cnt;
   const uint64_t Z = act ? ((uint64_t)G.zl | ((uint64_t)G.zh << 32)) : 0ull;
   const uint64_t DL = act ? ((uint64_t)G.dll | ((uint64_t)G.dlh << 32)) : 0ull;
@@ -170,7 +171,8 @@ __device__ __forceinline__ bool e4g_bytes_par(const E4Grp &G, int cnt, uint32_t 
   const uint32_t len = kd >= 0 ? topdl_k + 64u * (uint32_t)(lane - 1 - kd)
                                : (st.dlo ? st.hd : 0u) + 64u * (uint32_t)lane;
   const bool cont = act && dlo && (DL & 1);
-  if (__ballot(cont && len > 192)) return false;
+  const bool longc = cont && len > 192;
+  const uint64_t lng = __ballot(longc);
   const uint64_t anyD = __ballot(act && D != 0);
   const bool topd = topdl > 0 && (D >> (64 - topdl)) != 0;
   const uint64_t TD = __ballot(act && topd);
@@ -197,13 +199,13 @@ __device__ __forceinline__ bool e4g_bytes_par(const E4Grp &G, int cnt, uint32_t 
   const uint32_t vr = act ? wrem - 64u * (uint32_t)lane : 0u;
   const uint64_t V = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
   const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~V;
-  const uint32_t b = act ? (uint32_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
-                                      __builtin_popcountll(HC))
-                         : 0u;
+  const uint32_t b = (act && !longc) ? (uint32_t)(__builtin_popcountll(~ZO & ~Mem) +
+                                                   __builtin_popcountll(Mem & ~D) + __builtin_popcountll(HC))
+                                    : 0u;
   bytes += (uint32_t)__builtin_amdgcn_readlane(wave_incl_add((int)b), 63);
   memo = Mem;
   hco = HC;
-  return true;
+  return lng;
 }
 
 // next piece for this wave from the per-XCD counters (as the decoder)
@@ -295,27 +297,25 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
         const uint32_t wrem = W32 - 64u * g0;
         // lane j: step j's literal-run members and heads (the emit pass's roles)
         uint64_t MemL = 0, HCL = 0;
-        if (e4g_bytes_par(G, cnt, wrem, st, lane, bytes, MemL, HCL)) {
-          st = e4g_state_after(G, cnt, st);
-        } else {
-          uint32_t ml = 0, mh = 0, hl = 0, hh = 0;
-          for (int j = 0; j < cnt; ++j) {
-            const uint64_t Z = e4g_z(G, j), DL = e4g_dl(G, j), D = e4g_d(G, j);
-            const uint32_t vr = wrem - 64u * (uint32_t)j;
-            const uint64_t V = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
-            uint64_t Zh, Mem;
-            sp_roles(Z, DL, D, st, Zh, Mem);
-            const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~V;
-            bytes += (uint64_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
-                                __builtin_popcountll(HC));
-            ml = sp_wl(ml, (uint32_t)Mem, j);
-            mh = sp_wl(mh, (uint32_t)(Mem >> 32), j);
-            hl = sp_wl(hl, (uint32_t)HC, j);
-            hh = sp_wl(hh, (uint32_t)(HC >> 32), j);
-          }
-          MemL = ((uint64_t)mh << 32) | ml;
-          HCL = ((uint64_t)hh << 32) | hl;
+        uint64_t lng = e4g_bytes_par(G, cnt, wrem, st, lane, bytes, MemL, HCL);
+        // steps a long D/L stretch enters (~15 % of config-3 groups have
+        // one or two): the sequential roles on the run state there
+        while (lng) {
+          const int j = __builtin_ctzll(lng);
+          lng &= lng - 1;
+          SpSt sj = j ? e4g_state_after(G, j, st) : st;
+          const uint64_t Z = e4g_z(G, j), DL = e4g_dl(G, j), D = e4g_d(G, j);
+          const uint32_t vr = wrem - 64u * (uint32_t)j;
+          const uint64_t V = vr >= 64 ? ~0ull : ((1ull << vr) - 1);
+          uint64_t Zh, Mem;
+          sp_roles(Z, DL, D, sj, Zh, Mem);
+          const uint64_t HC = Zh | (D & ~Mem), ZO = (Z & ~Zh) | ~V;
+          bytes += (uint64_t)(__builtin_popcountll(~ZO & ~Mem) + __builtin_popcountll(Mem & ~D) +
+                              __builtin_popcountll(HC));
+          MemL = lane == j ? Mem : MemL;
+          HCL = lane == j ? HC : HCL;
         }
+        st = e4g_state_after(G, cnt, st);
         // run boundaries for the emit pass (e4_classify's BV): past the
         // piece's end, every M word, each zero run / D/L stretch's first word
         {
