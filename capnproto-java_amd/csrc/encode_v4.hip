@@ -34,6 +34,9 @@ constexpr uint32_t kE4RingDw = kE4RingBytes / 4;
 // nonzero-byte tag of a word (PackedOutputStream.java:64-117): bit i set iff
 // byte i != 0.  SWAR: bit 7 of every byte of t = byte != 0, gathered by shifts.
 #define E4_LD2(p) (*(p))
+// the size pass's loads: nontemporal (U is read again only by the emit pass,
+// long after; config-3 encode -2 %, r4AT_e4_size_nt_ab.log)
+#define E4_SLD(p) ld_stream(p)
 
 __device__ __forceinline__ uint32_t e4_tag(uint64_t v) {
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
@@ -265,10 +268,10 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     // branches around them); words past the end are masked by `valid`
     const uint32_t kl = W32 - 1;
 #pragma unroll
-    for (int j = 0; j < PF; ++j) v[j] = src[min(((uint32_t)j << 6) + lane, kl)];
+    for (int j = 0; j < PF; ++j) v[j] = E4_SLD(src + min(((uint32_t)j << 6) + lane, kl));
     for (uint32_t s0 = 0; s0 < nsteps; s0 += PF) {
 #pragma unroll
-      for (int j = 0; j < PF; ++j) vn[j] = src[min(((s0 + PF + j) << 6) + lane, kl)];
+      for (int j = 0; j < PF; ++j) vn[j] = E4_SLD(src + min(((s0 + PF + j) << 6) + lane, kl));
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
         const uint32_t k = ((s0 + j) << 6) + lane;
