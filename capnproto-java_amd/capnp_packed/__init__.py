@@ -35,7 +35,7 @@ EXPORTS = [
     "cpk_decode_stream_host", "cpk_generate", "cpk_count_mismatch", "cpk_ctx_take_error",
     "cpk_decode_messages", "cpk_encode_messages", "cpk_encode_messages_host",
     "cpk_decode_messages_host", "cpk_encode_host_gather", "cpk_encode_messages_host_gather",
-    "cpk_read_message", "cpk_read_message_host",
+    "cpk_read_message", "cpk_read_message_host", "cpk_ctx_small_fallbacks",
 ]
 MSG_HEAD_WORDS, MSG_INFO_WORDS = 257, 517  # CPK_MSG_HEAD_WORDS, CPK_MSG_INFO_WORDS
 
@@ -90,6 +90,7 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_generate": ([vp, ctypes.POINTER(GenParams), vp, u32, vp, vp], i32),
         "cpk_count_mismatch": ([vp, vp, vp, u64, vp, vp], i32),
         "cpk_ctx_take_error": ([vp, vp], i32),
+        "cpk_ctx_small_fallbacks": ([vp], u64),
         "cpk_decode_messages": ([vp, vp, vp, u32, u64, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp], i32),
         "cpk_encode_messages": ([vp, vp, vp, u32, vp, u32, u64, vp, vp, vp], i32),
         "cpk_encode_messages_host": ([vp, vp, vp, u32, vp, u32, vp, u64, vp], i32),
@@ -169,6 +170,11 @@ class Context:
         """Synchronises `stream`; CPK_EINVAL if an encode since the last call
         met a piece larger than its max_seg_words hint (output undefined)."""
         return self._lib.cpk_ctx_take_error(self.handle, self._stream(stream))
+
+    def small_fallbacks(self) -> int:
+        """One-launch host calls whose completion flag was not seen within
+        5 ms (a stream sync stood in); 0 in normal operation."""
+        return int(self._lib.cpk_ctx_small_fallbacks(self.handle))
 
     def decode_batch(self, d_packed, d_in_off, d_seg_word_off, d_out, d_status, stream=None):
         n = d_seg_word_off.numel() - 1

@@ -33,6 +33,7 @@ struct MwShared {
   int32_t st;     // the ended piece's status ...
   uint32_t fin;   // ... and (CPK_OK) the end of its bytes
   uint32_t rounds;  // rounds the piece took (the most any wave ran)
+  uint32_t tmo;     // a chain wait timed out (the piece reports CPK_EDEVICE)
 };
 constexpr uint32_t kMwLds = 2048 + kMwWaves * kDecWaveLds + sizeof(MwShared);
 
@@ -41,12 +42,16 @@ __device__ __forceinline__ void mw_put(uint64_t *slot, uint32_t tag, uint32_t v)
 }
 // (bounded: a chain that never arrives -- cannot happen, every window of
 // the round is held by a resident wave -- reads as 0xffffffff, which ends the
-// piece: an entry past the bytes / the piece already over)
-__device__ __forceinline__ uint32_t mw_get(uint64_t *slot, uint32_t tag) {
+// piece: an entry past the bytes / the piece already over; the timeout is
+// noted in *tmo and the piece reports CPK_EDEVICE, not a decode status)
+__device__ __forceinline__ uint32_t mw_get(uint64_t *slot, uint32_t tag, uint32_t *tmo) {
   uint64_t v;
   uint32_t spins = 0;
   while (((v = __hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 32) != tag) {
-    if (++spins > (1u << 22)) return 0xffffffffu;
+    if (++spins > (1u << 22)) {
+      atomicOr(tmo, 1u);
+      return 0xffffffffu;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
@@ -98,10 +103,10 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
     pkw = wbuf + (int64_t)padw - (int64_t)g;
     ph = (padw - g) & 3;
     wave_lds_order();
-    ww = win_walks(pkw, visa, lane, g, wend DEC_PH_ARGS);
+    ww = win_walks(pkw, wbuf, visa, lane, g, wend DEC_PH_ARGS);
   }
   // ---- the entry (serial over the windows) ----------------------------------
-  const uint32_t ein = mw_get(&ms.E[slot], t);
+  const uint32_t ein = mw_get(&ms.E[slot], t, &ms.tmo);
   uint64_t onmask = 0;
   uint32_t S = ww.S, enext = ein;
   int j = 0;
@@ -163,7 +168,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
     o0 = inc - myw;
   }
   // ---- the output offset (serial), then the map and expansion ---------------
-  const uint32_t owin = mw_get(&ms.O[slot], t);
+  const uint32_t owin = mw_get(&ms.O[slot], t, &ms.tmo);
   if (owin == kMwDone) {  // the piece ended in an earlier window
     if (lane == 0) mw_put(&ms.O[nslot], t + 1, kMwDone);
     return true;
@@ -189,7 +194,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
   if (!chk && lane == 0) mw_put(&ms.O[nslot], t + 1, (uint32_t)(ow + T));
   int st = CPK_OK;
   uint32_t fin = 0;
-  const bool ok = win_emit<true>(pkw, lut, blk, lane, ein, ow, W, P, T, on, entry, S, onmask, o0, myw, enext,
+  const bool ok = win_emit<true>(pkw, wbuf, lut, blk, lane, ein, ow, W, P, T, on, entry, S, onmask, o0, myw, enext,
                                  lend, gp, (uint32_t)(((a + P + 15) & ~15ull) - a), ph, dst, st,
                                  fin DEC_PH_ARGS);
   if (!ok) end_piece(st, 0);
@@ -214,6 +219,7 @@ __device__ void decode_stream_mw(uint8_t *smem, const uint8_t *__restrict__ pack
   // LDS keeps what an earlier kernel left there: no slot may hold a tag this
   // launch will wait for (tags count up from 0 in every launch)
   if (threadIdx.x < kMwWaves) ms.E[threadIdx.x] = ms.O[threadIdx.x] = ~0ull;
+  if (threadIdx.x == 0) ms.tmo = 0;
   __syncthreads();
   uint64_t scur = sbeg;
   int sfail = CPK_OK;
@@ -248,7 +254,7 @@ __device__ void decode_stream_mw(uint8_t *smem, const uint8_t *__restrict__ pack
     if (lane == 0) atomicMax(&ms.rounds, r + 1);
     __syncthreads();
     tb += ms.rounds * kMwWaves;
-    const int st = ms.st;
+    const int st = ms.tmo ? CPK_EDEVICE : ms.st;
     if (threadIdx.x == 0) {
       status[seg] = st;
       in_off[seg] = a;

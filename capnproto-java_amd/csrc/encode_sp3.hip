@@ -412,7 +412,10 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
   fill_luts(lut, false);
   for (uint32_t i = threadIdx.x; i < kSp3Stage / 16; i += kSpThreads)
     reinterpret_cast<uint4 *>(stage)[i] = make_uint4(0u, 0u, 0u, 0u);
-  if (threadIdx.x == 0) scr[24] = scr[25] = 0;
+  // scr[13]: this launch's chunk-state timeouts (LDS; the context's error
+  // word may hold an earlier call's, so the result cannot be judged by it)
+  uint32_t *lerr = reinterpret_cast<uint32_t *>(&scr[13]);
+  if (threadIdx.x == 0) scr[24] = scr[25] = scr[13] = 0;
   SpRegs R;
   R.zl = R.zh = R.dll = R.dlh = R.dl_ = R.dh_ = 0;
   R.oml = R.omh = R.ohl = R.ohh = R.oel = R.oeh = 0;
@@ -450,13 +453,20 @@ __global__ __launch_bounds__(kSpThreads, 1) void sp_small_kernel(const uint64_t 
       const uint64_t pst = (prev && threadIdx.x == 0) ? ld_status(prev) : 0;
       uint32_t Xlast = 0;
       uint64_t wbefore = 0;
-      const uint64_t ct = sp3_chunk(R, V, LA, u, msk, scr, pst, prev, next, 1u, err, w, lane, Xlast, wbefore);
+      const uint64_t ct = sp3_chunk(R, V, LA, u, msk, scr, pst, prev, next, 1u, lerr, w, lane, Xlast, wbefore);
       if (u.cnt) sp3_b(R, V, u.cnt, lut, stage, (uint32_t)wbefore, lane);
       __syncthreads();
       sp3_flush(out, stage, g, ct, ocap);
       g += ct;
     }
   }
-  if (threadIdx.x == 0) out_off[n] = g;
+  // a timed-out chunk hand-off: the total reads past any capacity and the
+  // host reports CPK_EDEVICE (small_encode), the context's word notes it too
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const bool bad = *reinterpret_cast<volatile uint32_t *>(lerr) != 0;
+    if (bad) atomicOr(err, 4u);
+    out_off[n] = bad ? ~0ull : g;
+  }
   if (flag) small_done(flag, seq);
 }

@@ -207,7 +207,7 @@ int small_encode(cpk_ctx ctx, uint64_t np, uint64_t words, Lay lay, void *h_out,
   hipLaunchKernelGGL(cpk::sp_small_kernel, dim3(1), dim3(cpk::kSpThreads), cpk::kSpSmallLds, p->sk,
                      (const uint64_t *)s.pin_in, (const uint64_t *)desc, (uint32_t)np, (uint8_t *)s.pin_out, off,
                      ocap, ctx->tickets + cpk::kTkErr, off + np + 1, seq, da);
-  if (hipGetLastError() != hipSuccess || small_wait(p->sk, off + np + 1, seq)) return CPK_EDEVICE;
+  if (hipGetLastError() != hipSuccess || small_wait(ctx, p->sk, off + np + 1, seq)) return CPK_EDEVICE;
   const uint64_t P = off[np];
   if (P > ocap) return CPK_EDEVICE;
   if (P > h_out_cap) return CPK_ENOMEM;
@@ -314,7 +314,9 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
     if (h_swo[i + 1] < h_swo[i]) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
   if (small_ok(h_swo[n] - h_swo[0], n)) {
-    const HostChunk all{0, n, 0, 8 * (h_swo[n] - h_swo[0]), 0, 0};
+    // (in0: the words' absolute byte offset in the caller's buffer, as
+    // host_chunks sets it; the gather form copies piece by piece)
+    const HostChunk all{0, n, 8 * h_swo[0], 8 * (h_swo[n] - h_swo[0]), 0, 0};
     return small_encode(
         ctx, n, h_swo[n] - h_swo[0],
         [&](uint64_t *pin, uint64_t *desc) {

@@ -225,69 +225,14 @@ __device__ __forceinline__ void st_stream(uint4 w, void *p) {
 }
 
 // ------------------------------------------------------------ look-back
-// status word per piece: [63:62] flag (1 aggregate, 2 inclusive prefix),
-// [61:0] value.  One 8-byte relaxed agent-scope granule: the data is the
-// flag (cdna_hip_programming.md Guideline 16, form R2).
-constexpr uint64_t kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62;
-constexpr uint64_t kValMask = (1ull << 62) - 1;
-
+// One 8-byte relaxed agent-scope granule per status word: the data is the
+// flag (cdna_hip_programming.md Guideline 16, form R2); the single-pass
+// encoder's words (encode_sp.hip: sp_word) carry flag, epoch and value.
 __device__ __forceinline__ void st_status(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t ld_status(uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Publish a tile's aggregate as early as it is known (one lane).
-__device__ __forceinline__ void lb_publish(uint64_t *status, uint32_t tile, uint64_t agg) {
-  st_status(&status[tile], (tile == 0 ? kFlagInc : kFlagAgg) | agg);
-}
-// Wide form: each poll reads the 256 nearest predecessors (4 per lane), so
-// the inclusive-prefix frontier advances 256 items per memory round trip
-// instead of 64 -- the bound on items per second when thousands of waves
-// resolve at once.
-__device__ uint64_t lb_resolve_wide(uint64_t *status, uint32_t tile, uint64_t agg) {
-  const int lane = lane_id();
-  if (tile == 0) return 0;
-  uint64_t excl = 0;
-  int64_t top = (int64_t)tile - 1;
-  uint32_t spins = 0;
-  for (;;) {
-    uint64_t v[4];
-    int fi = 4;  // first inclusive among this lane's four (nearest first)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t idx = top - 4 * lane - i;
-      v[i] = idx >= 0 ? ld_status(&status[idx]) : kFlagInc;
-    }
-#pragma unroll
-    for (int i = 3; i >= 0; --i)
-      if ((v[i] >> 62) == 2) fi = i;
-    const uint64_t has = __ballot(fi < 4);
-    const int fl = has ? __builtin_ctzll(has) : 64;
-    const int firstPos = fl < 64 ? 4 * fl + __builtin_amdgcn_readlane(fi, fl) : 256;
-    bool z = false;
-    uint64_t sum = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int pos = 4 * lane + i;
-      if (pos <= firstPos) {
-        z = z || (v[i] >> 62) == 0;
-        sum += v[i] & kValMask;
-      }
-    }
-    if (__ballot(z)) {
-      if (++spins > (1u << 24)) break;  // cannot happen with in-order tickets
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
-    excl += sum;
-    if (firstPos < 256) break;
-    top -= 256;
-  }
-  if (lane == 0) st_status(&status[tile], kFlagInc | (excl + agg));
-  return excl;
 }
 
 // ------------------------------------------------------------ decoder
@@ -406,6 +351,86 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
+// ---- granule cursor (round 5) ------------------------------------------
+// The decoder is bound by its LDS pipe (SQ_LDS_IDX_ACTIVE ~90 % of CU cycles
+// over a config-2 decode, profiles/r4SQ_config2_sq.txt): every record a walk
+// visited cost three byte reads (tag and both possible count bytes) and every
+// expanded word three more dword reads.  A walk moves forward a record at a
+// time, so a lane can keep the 16 bytes [g, g + 16) of the window buffer
+// around its position in registers as two 8-byte aligned granules and load
+// one granule per step (aligned ds_read_b64; unaligned 8/16-byte LDS reads
+// are correct on gfx950 but cost ~10x per instruction,
+// tools/micro/lds_read_cost.hip); the tag, both counts and the record's
+// eight payload bytes then come out of registers (v_alignbyte).
+// Offsets are bytes from the window buffer's base wb (16-byte aligned);
+// the bytes read are exactly the LDS bytes the byte reads of rec_at /
+// read8<true> would read, so the walks see the same values, garbage past
+// the loaded bytes included.
+#ifndef CPK_DEC_GC
+#define CPK_DEC_GC 1
+#endif
+struct GCur {
+  uint32_t g;  // buffer offset of d0 (8-aligned); kGcNone: nothing loaded
+  uint32_t d0, d1, d2, d3;
+};
+constexpr uint32_t kGcNone = 0xffff0000u;
+__device__ __forceinline__ uint2 gc_ld(const uint8_t *wb, uint32_t o) {
+  return *reinterpret_cast<const uint2 *>(wb + o);
+}
+// make buffer offset o fall in the cursor's first granule: one load when it
+// moves one granule on (the usual step), two after a longer jump
+__device__ __forceinline__ void gc_seek(GCur &c, const uint8_t *wb, uint32_t o) {
+  const uint32_t ng = o & ~7u;
+  if (ng != c.g) {
+    uint2 lo = make_uint2(c.d2, c.d3);
+    if (ng != c.g + 8) lo = gc_ld(wb, ng);
+    const uint2 hi = gc_ld(wb, ng + 8);
+    c.d0 = lo.x;
+    c.d1 = lo.y;
+    c.d2 = hi.x;
+    c.d3 = hi.y;
+    c.g = ng;
+  }
+}
+// bytes o..o+3 (w0), o+4..o+7 (w1), o+8..o+11 (w2) of a sought cursor;
+// w2's bytes past o+15 (o at granule byte 7) are not loaded (zero)
+struct GWords {
+  uint32_t w0, w1, w2;
+};
+__device__ __forceinline__ GWords gc_words(const GCur &c, uint32_t o) {
+  const uint32_t d = o - c.g, s = d & 3;
+  const bool h = (d & 4) != 0;
+  const uint32_t a0 = h ? c.d1 : c.d0, a1 = h ? c.d2 : c.d1, a2 = h ? c.d3 : c.d2, a3 = h ? 0u : c.d3;
+  GWords w;
+  w.w0 = __builtin_amdgcn_alignbyte(a1, a0, s);
+  w.w1 = __builtin_amdgcn_alignbyte(a2, a1, s);
+  w.w2 = __builtin_amdgcn_alignbyte(a3, a2, s);
+  return w;
+}
+// the record at buffer offset o (rec_at through the cursor); also its tag
+// and count bytes for callers that need them
+struct GRec {
+  uint32_t len, nw, tag, c1, c9;
+};
+__device__ __forceinline__ GRec gc_rec(GCur &c, const uint8_t *wb, uint32_t o) {
+  gc_seek(c, wb, o);
+  const uint32_t d = o - c.g, s = d & 3;
+  const bool h = (d & 4) != 0;
+  const uint32_t a0 = h ? c.d1 : c.d0, a1 = h ? c.d2 : c.d1, a2 = h ? c.d3 : c.d2, a3 = h ? 0u : c.d3;
+  const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, s);
+  const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, s);
+  GRec r;
+  r.tag = w0 & 0xffu;
+  r.c1 = (w0 >> 8) & 0xffu;
+  r.c9 = (w2 >> 8) & 0xffu;
+  // (a 0xFF tag at granule byte 7: its count is the byte after the cursor)
+  if (r.tag == 0xffu && d == 7) r.c9 = wb[o + 9];
+  const uint32_t zm = 0u - (uint32_t)(r.tag == 0), fm = 0u - (uint32_t)(r.tag == 0xffu);
+  r.len = 1u + __builtin_popcount(r.tag) + (zm & 1u) + (fm & (8u * r.c9 + 1u));
+  r.nw = 1u + (zm & r.c1) + (fm & r.c9);
+  return r;
+}
+
 // (stats build: the window phases' clock sums live in the caller)
 #ifdef CPK_PHASE_STATS
 #define DEC_PH_PARAMS , unsigned long long &wph_last, unsigned long long *wph_acc
@@ -426,18 +451,27 @@ struct WinWalk {
   uint32_t cb, S, wt, lw;
   uint64_t R;
 };
-__device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, int lane, uint32_t e,
-                                             uint32_t wend DEC_PH_PARAMS) {
+__device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, const uint8_t *wb, VisMask *visa, int lane,
+                                             uint32_t e, uint32_t wend DEC_PH_PARAMS) {
   // ---- 1: speculative chunk walks --------------------------------------
   const uint32_t cb = e + kDecChunk * lane;
   const uint32_t ce = min(cb + kDecChunk, wend);
   VisMask vis = 0;
   uint32_t X = cb, wt = 0;  // wt: output words of the walk
+#if CPK_DEC_GC
+  const uint32_t rel = (uint32_t)(pkw - wb);  // buffer offset of piece position 0 (mod 2^32)
+  GCur gc;
+  gc.g = kGcNone;
+#endif
   if (cb < wend) {
     uint32_t pos = cb;
     while (pos < ce) {
       vis |= (VisMask)1 << (pos - cb);
+#if CPK_DEC_GC
+      const GRec r = gc_rec(gc, wb, pos + rel);
+#else
       const DecRec r = rec_at(pkw, pos);
+#endif
       wt += r.nw;
       pos += r.len;
     }
@@ -454,7 +488,11 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
       uint32_t base = __umul24(ow_, kDecChunk);
       asm("" : "+v"(base));  // (else folded into a quarter-rate v_mad_u64_u32)
       if ((visa[ow_] >> (r - base)) & 1) break;
+#if CPK_DEC_GC
+      const GRec rr = gc_rec(gc, wb, S + rel);  // (the chunk walk's cursor goes on)
+#else
       const DecRec rr = rec_at(pkw, S);
+#endif
       lw += rr.nw;
       S += rr.len;
     }
@@ -463,6 +501,18 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   // ---- 3: reachability over lanes --------------------------------------
   int nx = (cb < wend && S < wend) ? (int)chunk_div<kDecChunk>(S - e) : 64;
   uint64_t R = 1ull << lane;
+#if CPK_DEC_GC
+  // the usual chain: every lane lands in the next lane's chunk (or past the
+  // window), so the lanes reachable from l are l .. the first lane at or
+  // after l that lands nowhere -- two ballots instead of 18 bpermutes
+  if (__builtin_amdgcn_readfirstlane((int)(__ballot(nx < 64 && nx != lane + 1) != 0)) == 0) {
+    const uint64_t stop = __ballot(nx >= 64);  // (lane 63 always: its landing is past the window)
+    const uint64_t up = stop & (~0ull << lane);
+    const int k = __builtin_ctzll(up);
+    R = (k == 63 ? ~0ull : ((2ull << k) - 1)) & (~0ull << lane);
+  } else
+#endif
+  {
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     const int src = (nx & 63) << 2;
@@ -473,6 +523,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
       R |= ((uint64_t)rhi << 32) | rlo;
       nx = nn;
     }
+  }
   }
   WinWalk ww;
   ww.cb = cb;
@@ -490,13 +541,16 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
 // (decode_body; decode_piece_mw).  Returns false when a record fails (st
 // set); fin: the end of the record that fills the piece, else 0.
 template <bool kStream>
-__device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut, uint32_t *blk, int lane,
-                                         uint32_t e, int ow, int W, uint32_t P, int T, bool on,
+__device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, const uint64_t *lut, uint32_t *blk,
+                                         int lane, uint32_t e, int ow, int W, uint32_t P, int T, bool on,
                                          uint32_t entry, uint32_t S, uint64_t onmask, int o0, int myw,
                                          uint32_t enext, uint32_t lend, const uint8_t *gp, uint32_t glim,
                                          uint32_t ph, uint64_t *dst, int &st, uint32_t &fin DEC_PH_PARAMS) {
   bool failed = false;
   fin = 0;
+#if CPK_DEC_GC
+  const uint32_t rel = (uint32_t)(pkw - wb);  // buffer offset of piece position 0 (mod 2^32)
+#endif
   // errors and the filling record can only occur in a window reaching the
   // piece's last word or within one window plus one record of its end
   // (the window's records start before e + kWin; the longest record, a
@@ -515,29 +569,53 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         // round 0 (usually the window's only one): every record's output
         // is at or past the round's start, so it always marks a block
         if (on) {
-          uint32_t rel = (uint32_t)o0;
-          for (uint32_t q = entry; q < S && rel <= (uint32_t)(kRound - kBlk);) {
+          uint32_t ro = (uint32_t)o0;
+#if CPK_DEC_GC
+          GCur gc;
+          gc.g = kGcNone;
+          for (uint32_t q = entry; q < S && ro <= (uint32_t)(kRound - kBlk);) {
+            const GRec r = gc_rec(gc, wb, q + rel);
+            atomicMax(&blk[(ro + kBlk - 1) / kBlk], ((ro + 256u) << 12) | (q - e));
+            ro += r.nw;
+            q += r.len;
+          }
+#else
+          for (uint32_t q = entry; q < S && ro <= (uint32_t)(kRound - kBlk);) {
             const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
             const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
-            atomicMax(&blk[(rel + kBlk - 1) / kBlk], ((rel + 256u) << 12) | (q - e));
-            rel += 1u + (zm & c1) + (fm & c9);
+            atomicMax(&blk[(ro + kBlk - 1) / kBlk], ((ro + 256u) << 12) | (q - e));
+            ro += 1u + (zm & c1) + (fm & c9);
             q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
           }
+#endif
         }
       } else
       if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
-        int rel = o0 - rb;  // round-relative output of the record (> -256 when live)
+        int ro = o0 - rb;  // round-relative output of the record (> -256 when live)
         // (records past the round's last block start mark nothing, nor
         // do the ones after them)
-        for (uint32_t q = entry; q < S && rel <= kRound - kBlk;) {
+#if CPK_DEC_GC
+        GCur gc;
+        gc.g = kGcNone;
+        for (uint32_t q = entry; q < S && ro <= kRound - kBlk;) {
+          const GRec r = gc_rec(gc, wb, q + rel);
+          const int nw = (int)r.nw;
+          if (ro + nw > 0)
+            atomicMax(&blk[(max(ro, 0) + kBlk - 1) / kBlk], ((uint32_t)(ro + 256) << 12) | (q - e));
+          ro += nw;
+          q += r.len;
+        }
+#else
+        for (uint32_t q = entry; q < S && ro <= kRound - kBlk;) {
           const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
           const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
           const int nw = 1 + (int)((zm & c1) + (fm & c9));
-          if (rel + nw > 0)
-            atomicMax(&blk[(max(rel, 0) + kBlk - 1) / kBlk], ((uint32_t)(rel + 256) << 12) | (q - e));
-          rel += nw;
+          if (ro + nw > 0)
+            atomicMax(&blk[(max(ro, 0) + kBlk - 1) / kBlk], ((uint32_t)(ro + 256) << 12) | (q - e));
+          ro += nw;
           q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
         }
+#endif
       }
     } else
     {
@@ -696,7 +774,63 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
       }
     }
     };
+#if CPK_DEC_GC
+    // the usual window (every record in the loaded bytes): each word is the
+    // eight bytes after a cursor position y -- the record's tag for its head
+    // word and a zero run's words (LUT[0] gives zeros), tag + 1 + 8 * ofs for
+    // word ofs of a 0xFF run (LUT[0xFF] is the identity) -- through the
+    // record's LUT selector: one granule load per step, no byte reads
+    auto expand_gc = [&]() __attribute__((always_inline)) {
+      for (int b = lane; b < nb; b += 64) {
+        const uint32_t v = blk[b];
+        uint32_t q = e + (v & 0xfffu);
+        int ofs = kBlk * b + 256 - (int)(v >> 12);
+        const int wbase = ow + rb + kBlk * b;
+        const int wleft = ow + T - wbase - 1;
+        const int kw = min(kBlk, min(ow + T, W) - wbase);
+        uint64_t *d = dst + wbase;
+        const bool full = kw == kBlk && ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
+        GCur gc;
+        gc.g = kGcNone;
+        GRec r = gc_rec(gc, wb, q + rel);
+        uint64_t sel = lut[r.tag];
+        uint32_t xl[2];  // the pair's first word, stored with the second
+#pragma unroll
+        for (int i = 0; i < kBlk; ++i) {
+          const uint32_t y = (r.tag == 0xffu && ofs > 0) ? q + 1u + 8u * (uint32_t)ofs : q;
+          gc_seek(gc, wb, y + rel);
+          const GWords gw = gc_words(gc, y + rel);
+          const uint32_t rl = __builtin_amdgcn_alignbyte(gw.w1, gw.w0, 1);  // bytes y+1 .. y+4
+          const uint32_t rh = __builtin_amdgcn_alignbyte(gw.w2, gw.w1, 1);  // bytes y+5 .. y+8
+          const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
+          const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
+          if (i & 1) {
+            if (full) {
+              st_stream(make_uint4(xl[0], xl[1], x0, x1), d + i - 1);
+            } else {
+              if (i - 1 < kw) d[i - 1] = (uint64_t)xl[0] | ((uint64_t)xl[1] << 32);
+              if (i < kw) d[i] = (uint64_t)x0 | ((uint64_t)x1 << 32);
+            }
+          } else {
+            xl[0] = x0;
+            xl[1] = x1;
+          }
+          // past the window's last word: stay put (never stored)
+          if (++ofs == (int)r.nw && i < wleft) {
+            q += r.len;
+            ofs = 0;
+            if (i + 1 < kBlk) {
+              r = gc_rec(gc, wb, q + rel);
+              sel = lut[r.tag];
+            }
+          }
+        }
+      }
+    };
+    if (enext + 12 <= lend) expand_gc();
+#else
     if (enext + 12 <= lend) expand(std::true_type{});
+#endif
     else
       expand(std::false_type{});
     wave_lds_order();  // blk reused by the next round
@@ -845,7 +979,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
 
       WPH(1)
       // ---- 1-3: speculative walks, chain reachability ------------------------
-      const WinWalk ww = win_walks(pkw, visa, lane, e, wend DEC_PH_ARGS);
+      const WinWalk ww = win_walks(pkw, wbuf, visa, lane, e, wend DEC_PH_ARGS);
       const uint32_t cb = ww.cb, wt = ww.wt, lw = ww.lw, S = ww.S;
       const uint64_t R = ww.R;
       const uint64_t onmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)R, 0)) |
@@ -866,8 +1000,17 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       int myw = 0;
       if (on) {
         uint32_t pre = 0;
+#if CPK_DEC_GC
+        GCur gc;
+        gc.g = kGcNone;
+        const uint32_t rel = (uint32_t)(pkw - wbuf);
+#endif
         for (uint32_t q = cb; q < entry;) {
+#if CPK_DEC_GC
+          const GRec r = gc_rec(gc, wbuf, q + rel);
+#else
           const DecRec r = rec_at(pkw, q);
+#endif
           pre += r.nw;
           q += r.len;
         }
@@ -879,7 +1022,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       WPH(4)
       // ---- 5: error checks, block map, expansion ------------------------------
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
-      const bool failed = !win_emit<kStream>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
+      const bool failed = !win_emit<kStream>(pkw, wbuf, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
                                              enext, lend, gp, glim, ph, dst, st, fin DEC_PH_ARGS);
       if (failed) break;
       if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
@@ -1505,6 +1648,7 @@ struct cpk_ctx_s {
   uint64_t *fl_buf;       // cpk_decode_batch of a few large pieces: boundaries found [33] (lazy)
   uint8_t *rm_copy;       // cpk_read_message_host, one-wave path: the packed bytes on the device (lazy)
   uint64_t small_seq;     // the one-launch host paths' completion flag values (small_wait)
+  uint64_t small_fallbacks;  // small_wait calls that fell back to a stream sync (lost flags)
   uint64_t *sp_units;     // single pass, pieces over one chunk: unit counts | starts | block sums | unit table
   uint64_t sp_units_cap;  //   u64 entries
 };
@@ -1566,13 +1710,16 @@ static uint64_t small_arm(cpk_ctx ctx, uint64_t *flag) {
   __atomic_store_n(flag, 0ull, __ATOMIC_RELEASE);
   return kSmallTag | (++ctx->small_seq & ((1ull << 48) - 1));
 }
-static int small_wait(hipStream_t s, const uint64_t *flag, uint64_t seq) {
+static int small_wait(cpk_ctx ctx, hipStream_t s, const uint64_t *flag, uint64_t seq) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t i = 1;; ++i) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
     __builtin_ia32_pause();
     if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
   }
+  // counted (cpk_ctx_small_fallbacks): a lost flag would otherwise only cost
+  // 5 ms per call and pass every test
+  ++ctx->small_fallbacks;
   if (hipStreamSynchronize(s) != hipSuccess) return 1;
   return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
 }
@@ -1689,6 +1836,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
 }
 
 int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
+uint64_t cpk_ctx_small_fallbacks(cpk_ctx ctx) { return ctx ? ctx->small_fallbacks : 0; }
 
 // Single-pass encoder (encode_sp.hip): one launch, the look-back words
 // epoch-tagged (cleared only when the epoch wraps or the array grows).  Work
@@ -2443,7 +2591,7 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
       pipe_drain(p);
       return rc;
     }
-    if (flagged ? small_wait(p->sk, info + kRmInfo, seq) : hipStreamSynchronize(p->sk)) return CPK_EDEVICE;
+    if (flagged ? small_wait(ctx, p->sk, info + kRmInfo, seq) : hipStreamSynchronize(p->sk)) return CPK_EDEVICE;
     const int st = (int)(int64_t)info[0];
     const uint32_t count = (uint32_t)info[2];
     for (int i = 0; i < 4; ++i) h_info[i] = info[i];

@@ -82,6 +82,11 @@ uint64_t cpk_batch_packed_capacity(const uint64_t *h_seg_word_off, uint32_t n);
 int cpk_ctx_create(int device, cpk_ctx *out);
 void cpk_ctx_destroy(cpk_ctx ctx);
 int cpk_ctx_device(cpk_ctx ctx);
+/* Times a one-launch host path (small messages) gave up spinning on its
+ * kernel's pinned completion flag after 5 ms and fell back to a stream
+ * synchronisation since the context was created.  Zero in normal operation:
+ * a count that grows means a lost completion flag (a device-side bug). */
+uint64_t cpk_ctx_small_fallbacks(cpk_ctx ctx);
 
 /* Batch encode of n pieces, device-resident (replaces n calls of
  * PackedOutputStream.write, PackedOutputStream.java:35-205).  Pieces of any

@@ -463,6 +463,23 @@ def test_host_forms_pipelined_chunks(ctx, oracle, chunk_kb, monkeypatch):
         assert st[i] == ost, (i, st[i], ost)
 
 
+@pytest.mark.parametrize("chunk_kb", [None, "1"])
+def test_encode_host_first_offset_above_zero(ctx, oracle, chunk_kb, monkeypatch):
+    """cpk_encode_host with seg_word_off[0] > 0: the pieces are words
+    [swo[i], swo[i+1]) of the caller's buffer, on the one-launch small path
+    (no CPK_HOST_CHUNK_KB) and on the pipelined chunks alike (the
+    small path once copied from word 0)."""
+    if chunk_kb:
+        monkeypatch.setenv("CPK_HOST_CHUNK_KB", chunk_kb)
+    rng = np.random.default_rng(17)
+    data = _random_words(rng, 300, [.4, .3, .2, .1])
+    swo = np.array([5, 105, 300], dtype=np.uint64)
+    pk, off = ctx.encode_host(data, swo)
+    want = [oracle.pack(data[8 * int(swo[i]):8 * int(swo[i + 1])]) for i in range(2)]
+    assert off.tolist() == [0, len(want[0]), len(want[0]) + len(want[1])]
+    assert pk.tobytes() == b"".join(want)
+
+
 @pytest.mark.parametrize("chunk_kb", ["1", "64"])
 def test_encode_host_gather_matches_contiguous(ctx, oracle, chunk_kb, monkeypatch):
     """cpk_encode_host_gather (pieces left in their own host buffers, SURVEY.md

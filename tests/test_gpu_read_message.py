@@ -183,12 +183,15 @@ def test_small_host_paths_back_to_back(ctx, oracle):
     rng = np.random.default_rng(13)
     msgs = [_msg(rng, oracle, [int(x) for x in rng.integers(1, 600, size=int(rng.integers(1, 4)))])
             for _ in range(6)]
+    f0 = ctx.small_fallbacks()
     for k in range(300):
         segs, pk = msgs[k % len(msgs)]
         st, got, used, _ = _rd(ctx, pk)
         assert st == 0 and got == segs and used == len(pk), k
         packed, _ = ctx.encode_messages_host([segs])
         assert bytes(packed) == pk, k
+    # every call saw its kernel's completion flag (no 5 ms stream-sync fallback)
+    assert ctx.small_fallbacks() == f0
 
 
 def test_read_message_mid_size_workgroup_path(ctx, oracle):
