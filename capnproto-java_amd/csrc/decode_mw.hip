@@ -103,7 +103,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
     pkw = wbuf + (int64_t)padw - (int64_t)g;
     ph = (padw - g) & 3;
     wave_lds_order();
-    ww = win_walks(pkw, wbuf, visa, lane, g, wend DEC_PH_ARGS);
+    ww = win_walks(pkw, visa, lane, g, wend DEC_PH_ARGS);
   }
   // ---- the entry (serial over the windows) ----------------------------------
   const uint32_t ein = mw_get(&ms.E[slot], t, &ms.tmo);
@@ -194,9 +194,9 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
   if (!chk && lane == 0) mw_put(&ms.O[nslot], t + 1, (uint32_t)(ow + T));
   int st = CPK_OK;
   uint32_t fin = 0;
-  const bool ok = win_emit<true>(pkw, wbuf, lut, blk, lane, ein, ow, W, P, T, on, entry, S, onmask, o0, myw, enext,
+  const bool ok = win_emit<true>(pkw, lut, blk, lane, ein, ow, W, P, T, on, entry, S, onmask, o0, myw, enext,
                                  lend, gp, (uint32_t)(((a + P + 15) & ~15ull) - a), ph, dst, st,
-                                 fin DEC_PH_ARGS);
+                                 fin, false DEC_PH_ARGS);
   if (!ok) end_piece(st, 0);
   else if (fills && fin) end_piece(CPK_OK, fin);
   else if (chk && lane == 0) mw_put(&ms.O[nslot], t + 1, (uint32_t)(ow + T));

@@ -417,6 +417,7 @@ __global__ void dec_stream_check_kernel(const uint64_t *__restrict__ found, cons
   if (__syncthreads_and(ok) && i == 0) {
     skip[0] = 1u;
     skip[1] = 1u;
+    skip[2] = 1u;
   }
 }
 
@@ -424,8 +425,12 @@ __global__ void dec_gate_kernel(const uint64_t *__restrict__ in_off, const uint6
                                 uint32_t *skip) {
   if (threadIdx.x == 0) {
     const uint64_t P = in_off[n] - in_off[0], U = 8 * (swo[n] - swo[0]);
-    const bool v2 = 100 * P < 15 * U;
-    skip[0] = v2 ? 1u : 0u;
+    // skip[0]: the block-map decoder, [1] the record-index one (sparse
+    // batches), [2] the block-map decoder's dense form (serial walks of
+    // windows of few long records: packed bytes >= 80 % of the words')
+    const bool v2 = 100 * P < 15 * U, dense = 100 * P >= 80 * U;
+    skip[0] = (v2 || dense) ? 1u : 0u;
     skip[1] = v2 ? 0u : 1u;
+    skip[2] = dense ? 0u : 1u;
   }
 }

@@ -268,9 +268,15 @@ constexpr uint32_t kWin = 64 * kDecChunk;         // packed bytes resolved per w
 constexpr uint32_t kDecLook = 240;
 constexpr uint32_t kWinBuf = (kWin + 15 + kDecLook + 16 + 15) & ~15u;  // + pad, look-ahead, slack
 // (8 workgroups per CU with 48-byte chunks; larger rounds cost occupancy)
-constexpr int kRound = 1280;  // output words expanded per round
+#ifndef CPK_DEC_ROUND
+#define CPK_DEC_ROUND 1280
+#endif
+constexpr int kRound = CPK_DEC_ROUND;  // output words expanded per round
 // (4: 64 lanes cover a window's blocks in fewer, fuller passes; measured faster than 8)
-constexpr int kBlk = 4;  // output words per expansion block
+#ifndef CPK_DEC_BLK
+#define CPK_DEC_BLK 4
+#endif
+constexpr int kBlk = CPK_DEC_BLK;  // output words per expansion block
 // a lane's visited positions: one bit per chunk byte
 typedef std::conditional<(kDecChunk <= 32), uint32_t, uint64_t>::type VisMask;
 static_assert(kDecChunk <= 64, "visited mask bits");
@@ -286,6 +292,15 @@ constexpr int kMapPer = kRound / kBlk / 64;  // map entries per lane in the fill
 static_assert((kRound / kBlk == 64 * kMapPer && kWin <= 4096 && kRound + 256 < (1 << 19)),
               "max-map entry: 12-bit window position, 19-bit output position");
 constexpr uint32_t kDecChkReach = (kWin + 2064);
+// Dense windows (few, long records: 0xFF runs) are walked by one lane
+// (decode_body<.., kSerial>, the form picked for dense batches): taken when
+// the previous window looked dense (over 5.3 packed bytes per word); a serial
+// walk passing kDecSerMax records gives the window back to the parallel
+// walks, which then keep the next kDecSerCool windows.
+#ifndef CPK_DEC_SER_MAX
+#define CPK_DEC_SER_MAX 128
+#endif
+constexpr uint32_t kDecSerMax = CPK_DEC_SER_MAX, kDecSerCool = 32;
 static_assert(kDecChkReach >= kWin + 2050, "a window's last record must fall inside the checked reach");
 constexpr int kWinLinesPerLane = (int)((kWin + 15 + kDecLook + 15) / 16 + 63) / 64;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;  // 21,760 at 56-byte chunks
@@ -301,14 +316,25 @@ __device__ __forceinline__ int wave_min(int v) {
   return v;
 }
 
+// The tag at piece position q and both possible count bytes (c1 after a
+// 0x00 tag, c9 after 0xFF), read together: one LDS round trip per record on
+// the walks.  (Round 5: reading a count byte only for the tags that have one
+// cut the decoder's LDS cycles 22 % and made it 6 % slower -- the dependent
+// second read and its exec-mask branches, docs/tuning_log.md.)
+__device__ __forceinline__ void rec_bytes(const uint8_t *pkw, uint32_t q, uint32_t &tag, uint32_t &c1, uint32_t &c9) {
+  tag = pkw[q];
+  c1 = pkw[q + 1];
+  c9 = pkw[q + 9];
+}
+
 // The record whose tag is at piece position q: its byte length and output
-// words (PackedInputStream.java:82-134).  The tag and both possible count
-// bytes are read together: one LDS round trip per record on the walks.
+// words (PackedInputStream.java:82-134).
 struct DecRec {
   uint32_t len, nw;
 };
 __device__ __forceinline__ DecRec rec_at(const uint8_t *pkw, uint32_t q) {
-  const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+  uint32_t tag, c1, c9;
+  rec_bytes(pkw, q, tag, c1, c9);
   // masks, not nested selects (hipcc turns those into exec-mask branches)
   const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
   DecRec r;
@@ -351,86 +377,6 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-// ---- granule cursor (round 5) ------------------------------------------
-// The decoder is bound by its LDS pipe (SQ_LDS_IDX_ACTIVE ~90 % of CU cycles
-// over a config-2 decode, profiles/r4SQ_config2_sq.txt): every record a walk
-// visited cost three byte reads (tag and both possible count bytes) and every
-// expanded word three more dword reads.  A walk moves forward a record at a
-// time, so a lane can keep the 16 bytes [g, g + 16) of the window buffer
-// around its position in registers as two 8-byte aligned granules and load
-// one granule per step (aligned ds_read_b64; unaligned 8/16-byte LDS reads
-// are correct on gfx950 but cost ~10x per instruction,
-// tools/micro/lds_read_cost.hip); the tag, both counts and the record's
-// eight payload bytes then come out of registers (v_alignbyte).
-// Offsets are bytes from the window buffer's base wb (16-byte aligned);
-// the bytes read are exactly the LDS bytes the byte reads of rec_at /
-// read8<true> would read, so the walks see the same values, garbage past
-// the loaded bytes included.
-#ifndef CPK_DEC_GC
-#define CPK_DEC_GC 1
-#endif
-struct GCur {
-  uint32_t g;  // buffer offset of d0 (8-aligned); kGcNone: nothing loaded
-  uint32_t d0, d1, d2, d3;
-};
-constexpr uint32_t kGcNone = 0xffff0000u;
-__device__ __forceinline__ uint2 gc_ld(const uint8_t *wb, uint32_t o) {
-  return *reinterpret_cast<const uint2 *>(wb + o);
-}
-// make buffer offset o fall in the cursor's first granule: one load when it
-// moves one granule on (the usual step), two after a longer jump
-__device__ __forceinline__ void gc_seek(GCur &c, const uint8_t *wb, uint32_t o) {
-  const uint32_t ng = o & ~7u;
-  if (ng != c.g) {
-    uint2 lo = make_uint2(c.d2, c.d3);
-    if (ng != c.g + 8) lo = gc_ld(wb, ng);
-    const uint2 hi = gc_ld(wb, ng + 8);
-    c.d0 = lo.x;
-    c.d1 = lo.y;
-    c.d2 = hi.x;
-    c.d3 = hi.y;
-    c.g = ng;
-  }
-}
-// bytes o..o+3 (w0), o+4..o+7 (w1), o+8..o+11 (w2) of a sought cursor;
-// w2's bytes past o+15 (o at granule byte 7) are not loaded (zero)
-struct GWords {
-  uint32_t w0, w1, w2;
-};
-__device__ __forceinline__ GWords gc_words(const GCur &c, uint32_t o) {
-  const uint32_t d = o - c.g, s = d & 3;
-  const bool h = (d & 4) != 0;
-  const uint32_t a0 = h ? c.d1 : c.d0, a1 = h ? c.d2 : c.d1, a2 = h ? c.d3 : c.d2, a3 = h ? 0u : c.d3;
-  GWords w;
-  w.w0 = __builtin_amdgcn_alignbyte(a1, a0, s);
-  w.w1 = __builtin_amdgcn_alignbyte(a2, a1, s);
-  w.w2 = __builtin_amdgcn_alignbyte(a3, a2, s);
-  return w;
-}
-// the record at buffer offset o (rec_at through the cursor); also its tag
-// and count bytes for callers that need them
-struct GRec {
-  uint32_t len, nw, tag, c1, c9;
-};
-__device__ __forceinline__ GRec gc_rec(GCur &c, const uint8_t *wb, uint32_t o) {
-  gc_seek(c, wb, o);
-  const uint32_t d = o - c.g, s = d & 3;
-  const bool h = (d & 4) != 0;
-  const uint32_t a0 = h ? c.d1 : c.d0, a1 = h ? c.d2 : c.d1, a2 = h ? c.d3 : c.d2, a3 = h ? 0u : c.d3;
-  const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, s);
-  const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, s);
-  GRec r;
-  r.tag = w0 & 0xffu;
-  r.c1 = (w0 >> 8) & 0xffu;
-  r.c9 = (w2 >> 8) & 0xffu;
-  // (a 0xFF tag at granule byte 7: its count is the byte after the cursor)
-  if (r.tag == 0xffu && d == 7) r.c9 = wb[o + 9];
-  const uint32_t zm = 0u - (uint32_t)(r.tag == 0), fm = 0u - (uint32_t)(r.tag == 0xffu);
-  r.len = 1u + __builtin_popcount(r.tag) + (zm & 1u) + (fm & (8u * r.c9 + 1u));
-  r.nw = 1u + (zm & r.c1) + (fm & r.c9);
-  return r;
-}
-
 // (stats build: the window phases' clock sums live in the caller)
 #ifdef CPK_PHASE_STATS
 #define DEC_PH_PARAMS , unsigned long long &wph_last, unsigned long long *wph_acc
@@ -451,27 +397,18 @@ struct WinWalk {
   uint32_t cb, S, wt, lw;
   uint64_t R;
 };
-__device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, const uint8_t *wb, VisMask *visa, int lane,
-                                             uint32_t e, uint32_t wend DEC_PH_PARAMS) {
+__device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, int lane, uint32_t e,
+                                             uint32_t wend DEC_PH_PARAMS) {
   // ---- 1: speculative chunk walks --------------------------------------
   const uint32_t cb = e + kDecChunk * lane;
   const uint32_t ce = min(cb + kDecChunk, wend);
   VisMask vis = 0;
   uint32_t X = cb, wt = 0;  // wt: output words of the walk
-#if CPK_DEC_GC
-  const uint32_t rel = (uint32_t)(pkw - wb);  // buffer offset of piece position 0 (mod 2^32)
-  GCur gc;
-  gc.g = kGcNone;
-#endif
   if (cb < wend) {
     uint32_t pos = cb;
     while (pos < ce) {
       vis |= (VisMask)1 << (pos - cb);
-#if CPK_DEC_GC
-      const GRec r = gc_rec(gc, wb, pos + rel);
-#else
       const DecRec r = rec_at(pkw, pos);
-#endif
       wt += r.nw;
       pos += r.len;
     }
@@ -488,11 +425,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, const uint8_t *
       uint32_t base = __umul24(ow_, kDecChunk);
       asm("" : "+v"(base));  // (else folded into a quarter-rate v_mad_u64_u32)
       if ((visa[ow_] >> (r - base)) & 1) break;
-#if CPK_DEC_GC
-      const GRec rr = gc_rec(gc, wb, S + rel);  // (the chunk walk's cursor goes on)
-#else
       const DecRec rr = rec_at(pkw, S);
-#endif
       lw += rr.nw;
       S += rr.len;
     }
@@ -501,17 +434,6 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, const uint8_t *
   // ---- 3: reachability over lanes --------------------------------------
   int nx = (cb < wend && S < wend) ? (int)chunk_div<kDecChunk>(S - e) : 64;
   uint64_t R = 1ull << lane;
-#if CPK_DEC_GC
-  // the usual chain: every lane lands in the next lane's chunk (or past the
-  // window), so the lanes reachable from l are l .. the first lane at or
-  // after l that lands nowhere -- two ballots instead of 18 bpermutes
-  if (__builtin_amdgcn_readfirstlane((int)(__ballot(nx < 64 && nx != lane + 1) != 0)) == 0) {
-    const uint64_t stop = __ballot(nx >= 64);  // (lane 63 always: its landing is past the window)
-    const uint64_t up = stop & (~0ull << lane);
-    const int k = __builtin_ctzll(up);
-    R = (k == 63 ? ~0ull : ((2ull << k) - 1)) & (~0ull << lane);
-  } else
-#endif
   {
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
@@ -541,16 +463,14 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, const uint8_t *
 // (decode_body; decode_piece_mw).  Returns false when a record fails (st
 // set); fin: the end of the record that fills the piece, else 0.
 template <bool kStream>
-__device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, const uint64_t *lut, uint32_t *blk,
-                                         int lane, uint32_t e, int ow, int W, uint32_t P, int T, bool on,
+__device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut, uint32_t *blk, int lane,
+                                         uint32_t e, int ow, int W, uint32_t P, int T, bool on,
                                          uint32_t entry, uint32_t S, uint64_t onmask, int o0, int myw,
                                          uint32_t enext, uint32_t lend, const uint8_t *gp, uint32_t glim,
-                                         uint32_t ph, uint64_t *dst, int &st, uint32_t &fin DEC_PH_PARAMS) {
+                                         uint32_t ph, uint64_t *dst, int &st, uint32_t &fin,
+                                         bool premapped DEC_PH_PARAMS) {
   bool failed = false;
   fin = 0;
-#if CPK_DEC_GC
-  const uint32_t rel = (uint32_t)(pkw - wb);  // buffer offset of piece position 0 (mod 2^32)
-#endif
   // errors and the filling record can only occur in a window reaching the
   // piece's last word or within one window plus one record of its end
   // (the window's records start before e + kWin; the longest record, a
@@ -558,6 +478,8 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, 
   const bool chk = (ow + T >= W) || (P - e < kDecChkReach);
   for (int rb = 0; rb < T; rb += kRound) {
     int err = 0x7fffffff;
+    // (premapped: the serial walk filled round 0's map, decode_body)
+    if (!(premapped && rb == 0)) {
     wave_lds_order();  // (the visited masks / last round's map reads are done)
 #pragma unroll
     for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = 0u;
@@ -570,44 +492,23 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, 
         // is at or past the round's start, so it always marks a block
         if (on) {
           uint32_t ro = (uint32_t)o0;
-#if CPK_DEC_GC
-          GCur gc;
-          gc.g = kGcNone;
           for (uint32_t q = entry; q < S && ro <= (uint32_t)(kRound - kBlk);) {
-            const GRec r = gc_rec(gc, wb, q + rel);
-            atomicMax(&blk[(ro + kBlk - 1) / kBlk], ((ro + 256u) << 12) | (q - e));
-            ro += r.nw;
-            q += r.len;
-          }
-#else
-          for (uint32_t q = entry; q < S && ro <= (uint32_t)(kRound - kBlk);) {
-            const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+            uint32_t tag, c1, c9;
+            rec_bytes(pkw, q, tag, c1, c9);
             const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
             atomicMax(&blk[(ro + kBlk - 1) / kBlk], ((ro + 256u) << 12) | (q - e));
             ro += 1u + (zm & c1) + (fm & c9);
             q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
           }
-#endif
         }
       } else
       if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
         int ro = o0 - rb;  // round-relative output of the record (> -256 when live)
         // (records past the round's last block start mark nothing, nor
         // do the ones after them)
-#if CPK_DEC_GC
-        GCur gc;
-        gc.g = kGcNone;
         for (uint32_t q = entry; q < S && ro <= kRound - kBlk;) {
-          const GRec r = gc_rec(gc, wb, q + rel);
-          const int nw = (int)r.nw;
-          if (ro + nw > 0)
-            atomicMax(&blk[(max(ro, 0) + kBlk - 1) / kBlk], ((uint32_t)(ro + 256) << 12) | (q - e));
-          ro += nw;
-          q += r.len;
-        }
-#else
-        for (uint32_t q = entry; q < S && ro <= kRound - kBlk;) {
-          const uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+          uint32_t tag, c1, c9;
+          rec_bytes(pkw, q, tag, c1, c9);
           const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
           const int nw = 1 + (int)((zm & c1) + (fm & c9));
           if (ro + nw > 0)
@@ -615,7 +516,6 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, 
           ro += nw;
           q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
         }
-#endif
       }
     } else
     {
@@ -674,6 +574,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, 
         if (oo + nw == W) fin = q + adv;
       }
     }
+    }
     if (rb == 0) {
       err = __builtin_amdgcn_readfirstlane(wave_min(err));
       if (err != 0x7fffffff) {
@@ -715,7 +616,8 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, 
       // (the record's tag and count bytes are read once per record, not per
       // word: a literal run's words then need only their own reads, all in
       // flight together)
-      uint32_t tag = pkw[q], c1 = pkw[q + 1], c9 = pkw[q + 9];
+      uint32_t tag, c1, c9;
+      rec_bytes(pkw, q, tag, c1, c9);
 #pragma unroll
       for (int i = 0; i < kBlk; ++i) {
         // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
@@ -748,11 +650,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, 
         if (++ofs == nw && i < wleft) {
           q += adv;
           ofs = 0;
-          if (i + 1 < kBlk) {
-            tag = pkw[q];
-            c1 = pkw[q + 1];
-            c9 = pkw[q + 9];
-          }
+          if (i + 1 < kBlk) rec_bytes(pkw, q, tag, c1, c9);
         }
       }
       const int kw = min(kBlk, min(ow + T, W) - wbase);
@@ -774,63 +672,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint8_t *wb, 
       }
     }
     };
-#if CPK_DEC_GC
-    // the usual window (every record in the loaded bytes): each word is the
-    // eight bytes after a cursor position y -- the record's tag for its head
-    // word and a zero run's words (LUT[0] gives zeros), tag + 1 + 8 * ofs for
-    // word ofs of a 0xFF run (LUT[0xFF] is the identity) -- through the
-    // record's LUT selector: one granule load per step, no byte reads
-    auto expand_gc = [&]() __attribute__((always_inline)) {
-      for (int b = lane; b < nb; b += 64) {
-        const uint32_t v = blk[b];
-        uint32_t q = e + (v & 0xfffu);
-        int ofs = kBlk * b + 256 - (int)(v >> 12);
-        const int wbase = ow + rb + kBlk * b;
-        const int wleft = ow + T - wbase - 1;
-        const int kw = min(kBlk, min(ow + T, W) - wbase);
-        uint64_t *d = dst + wbase;
-        const bool full = kw == kBlk && ((reinterpret_cast<uintptr_t>(d) & 15) == 0);
-        GCur gc;
-        gc.g = kGcNone;
-        GRec r = gc_rec(gc, wb, q + rel);
-        uint64_t sel = lut[r.tag];
-        uint32_t xl[2];  // the pair's first word, stored with the second
-#pragma unroll
-        for (int i = 0; i < kBlk; ++i) {
-          const uint32_t y = (r.tag == 0xffu && ofs > 0) ? q + 1u + 8u * (uint32_t)ofs : q;
-          gc_seek(gc, wb, y + rel);
-          const GWords gw = gc_words(gc, y + rel);
-          const uint32_t rl = __builtin_amdgcn_alignbyte(gw.w1, gw.w0, 1);  // bytes y+1 .. y+4
-          const uint32_t rh = __builtin_amdgcn_alignbyte(gw.w2, gw.w1, 1);  // bytes y+5 .. y+8
-          const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
-          const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
-          if (i & 1) {
-            if (full) {
-              st_stream(make_uint4(xl[0], xl[1], x0, x1), d + i - 1);
-            } else {
-              if (i - 1 < kw) d[i - 1] = (uint64_t)xl[0] | ((uint64_t)xl[1] << 32);
-              if (i < kw) d[i] = (uint64_t)x0 | ((uint64_t)x1 << 32);
-            }
-          } else {
-            xl[0] = x0;
-            xl[1] = x1;
-          }
-          // past the window's last word: stay put (never stored)
-          if (++ofs == (int)r.nw && i < wleft) {
-            q += r.len;
-            ofs = 0;
-            if (i + 1 < kBlk) {
-              r = gc_rec(gc, wb, q + rel);
-              sel = lut[r.tag];
-            }
-          }
-        }
-      }
-    };
-    if (enext + 12 <= lend) expand_gc();
-#else
     if (enext + 12 <= lend) expand(std::true_type{});
-#endif
     else
       expand(std::false_type{});
     wave_lds_order();  // blk reused by the next round
@@ -855,7 +697,7 @@ struct DecStreams {
   const uint32_t *skip;   // (batch form: nonzero = the other decoder took the batch)
   const uint32_t *order;  // (stream form: ticket -> stream, largest first; null: in order)
 };
-template <bool kStream>
+template <bool kStream, bool kSerial = false>
 __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__restrict__ packed,
                                             uint64_t *__restrict__ in_off, const uint64_t *__restrict__ swo,
                                             uint32_t n, uint64_t *__restrict__ out, int32_t *__restrict__ status,
@@ -878,6 +720,10 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
   uint64_t slim = avail;  //   end of the stream's bytes
   int sfail = CPK_OK;     //   a failed piece stops the stream
   uint32_t snext = 0, sende = 0, sj = 0;  // next piece, end of the stream's pieces, stream
+  bool ser = false;   // the next window is walked by one lane (the last one looked dense)
+  uint32_t cool = 0;  // windows before the next serial attempt after one gave up
+  int tprev = 0;      // the last window's words (a window near the piece's end stays parallel:
+                      // in a stream the bytes do not say where the piece ends)
 
   for (uint32_t sidx = 0;; ++sidx) {
     // every branch below is on wave-uniform (SGPR) values: the compiler
@@ -976,10 +822,62 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       const uint8_t *pkw = wbuf + (int64_t)padw - (int64_t)e;
       const uint32_t ph = (padw - e) & 3;  // LDS byte phase of piece position 0
       wave_lds_order();
+      if constexpr (kSerial) {
+        // ---- a dense window: its true records walked by one lane -----------
+        // In a window of few, long records (the 0xFF runs of dense data) the
+        // 64 speculative chunk walks mostly walk verbatim run bytes, and the
+        // chain, count and map walks follow; one lane walking the true chain
+        // from e visits only the ~30 true records
+        // (PackedInputStream.java:82-134) and fills round 0's block map in
+        // order with plain stores (a later record marking the same block is
+        // the larger entry, as ds_max keeps it).  Only for windows that can
+        // neither fail nor fill the piece and whose words fit one round: a
+        // walk that meets the piece's last word, the round's end or
+        // kDecSerMax records gives the window to the parallel path.  (The
+        // decode_kernel<.., true> form, picked for dense batches: its extra
+        // state costs the parallel path ~2 % on config-2 data.)
+        if (ser && P - e >= kDecChkReach && W - ow > 2 * tprev) {
+          wave_lds_order();
+#pragma unroll
+          for (int i = 0; i < kMapPer; ++i) blk[lane * kMapPer + i] = 0u;
+          wave_lds_order();
+          uint32_t q = e, nrec = 0;
+          int o = 0, ok = 1;
+          if (lane == 0) {
+            const int wr = W - ow;  // words left in the piece
+            while (q < wend) {
+              const DecRec r = rec_at(pkw, q);
+              if (o + (int)r.nw >= wr || o + (int)r.nw > kRound || ++nrec > kDecSerMax) {
+                ok = 0;
+                break;
+              }
+              if (o <= kRound - kBlk) blk[(o + kBlk - 1) / kBlk] = ((uint32_t)(o + 256) << 12) | (q - e);
+              o += (int)r.nw;
+              q += r.len;
+            }
+          }
+          if (readlane(ok, 0)) {
+            const int T = readlane(o, 0);
+            const uint32_t enext = (uint32_t)readlane((int)q, 0);
+            uint32_t fin = 0;
+            const bool failed = !win_emit<kStream>(pkw, lut, blk, lane, e, ow, W, P, T, false, e, e, 0ull, 0,
+                                                   0, enext, lend, gp, glim, ph, dst, st, fin, true DEC_PH_ARGS);
+            if (failed) break;  // (cannot happen: no record here is checked)
+            ow += T;
+            e = enext;
+            tprev = T;
+            continue;
+          }
+          // too many records (dense but tagged words, e.g. one zero byte per
+          // word): the parallel path, and no serial walk for a while
+          ser = false;
+          cool = kDecSerCool;
+        }
+      }
 
       WPH(1)
       // ---- 1-3: speculative walks, chain reachability ------------------------
-      const WinWalk ww = win_walks(pkw, wbuf, visa, lane, e, wend DEC_PH_ARGS);
+      const WinWalk ww = win_walks(pkw, visa, lane, e, wend DEC_PH_ARGS);
       const uint32_t cb = ww.cb, wt = ww.wt, lw = ww.lw, S = ww.S;
       const uint64_t R = ww.R;
       const uint64_t onmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)R, 0)) |
@@ -1000,17 +898,8 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       int myw = 0;
       if (on) {
         uint32_t pre = 0;
-#if CPK_DEC_GC
-        GCur gc;
-        gc.g = kGcNone;
-        const uint32_t rel = (uint32_t)(pkw - wbuf);
-#endif
         for (uint32_t q = cb; q < entry;) {
-#if CPK_DEC_GC
-          const GRec r = gc_rec(gc, wbuf, q + rel);
-#else
           const DecRec r = rec_at(pkw, q);
-#endif
           pre += r.nw;
           q += r.len;
         }
@@ -1022,13 +911,21 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       WPH(4)
       // ---- 5: error checks, block map, expansion ------------------------------
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
-      const bool failed = !win_emit<kStream>(pkw, wbuf, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
-                                             enext, lend, gp, glim, ph, dst, st, fin DEC_PH_ARGS);
+      const bool failed = !win_emit<kStream>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
+                                             enext, lend, gp, glim, ph, dst, st, fin, false DEC_PH_ARGS);
       if (failed) break;
       if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
         ow = W;
         e = fin;
         break;
+      }
+      if constexpr (kSerial) {
+        // dense data: ~8 packed bytes per word (0xFF runs); config-2-like
+        // windows take ~3.8 (their ~550 records would be a long serial walk)
+        // (wave-uniform values: kept in scalar registers)
+        if (cool) --cool;
+        else ser = __builtin_amdgcn_readfirstlane((int)(16u * (uint32_t)T < 3u * (enext - e))) != 0;
+        tprev = __builtin_amdgcn_readfirstlane(T);
       }
       ow += T;
       e = enext;
@@ -1043,13 +940,13 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
   }
   WPH_FLUSH(16)
 }
-template <bool kStream>
+template <bool kStream, bool kSerial = false>
 __global__ __launch_bounds__(kDecThreads, kDecWpe) void decode_kernel(
     const uint8_t *__restrict__ packed, uint64_t *__restrict__ in_off,
     const uint64_t *__restrict__ swo, uint32_t n, uint64_t *__restrict__ out,
     int32_t *__restrict__ status, uint32_t *ticket, uint64_t avail, DecStreams sd) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  decode_body<kStream>(smem, packed, in_off, swo, n, out, status, ticket, avail, sd);
+  decode_body<kStream, kSerial>(smem, packed, in_off, swo, n, out, status, ticket, avail, sd);
 }
 
 // ------------------------------------------------------------ messages
@@ -1796,12 +1693,21 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     return CPK_ENOMEM;
   }
   // the kernels' dynamic LDS, above the 64 KiB default for some: set here,
-  // with the context's device current (the attribute is per device)
+  // with the context's device current (the attribute is per device).  The
+  // library is built for gfx950 only (160 KiB of LDS per CU): each request
+  // is checked against that at compile time, so a refused attribute is a
+  // runtime/driver failure, reported as CPK_EDEVICE
+  constexpr uint32_t kGfx950Lds = 160 * 1024;
+  static_assert(cpk::kDecLds <= kGfx950Lds && cpk::kSpLds <= kGfx950Lds && cpk::kSpSmallLds <= kGfx950Lds &&
+                    cpk::kMwLds <= kGfx950Lds && cpk::kSsLds <= kGfx950Lds,
+                "a kernel's dynamic LDS exceeds gfx950's 160 KiB");
   const struct {
     const void *f;
     uint32_t bytes;
   } lds[] = {{(const void *)cpk::decode_kernel<false>, cpk::kDecLds},
              {(const void *)cpk::decode_kernel<true>, cpk::kDecLds},
+             {(const void *)cpk::decode_kernel<false, true>, cpk::kDecLds},
+             {(const void *)cpk::decode_kernel<true, true>, cpk::kDecLds},
              {(const void *)cpk::sp_encode_kernel<true>, cpk::kSpLds},
              {(const void *)cpk::sp_encode_kernel<false>, cpk::kSpLds},
              {(const void *)cpk::sp_small_kernel, cpk::kSpSmallLds},
@@ -2139,7 +2045,10 @@ bool dec_v2(cpk_ctx ctx) { return ctx->decoder == 2; }
 void dec_launch(cpk_ctx ctx, bool stream, unsigned want, const uint8_t *packed, uint64_t *in_off,
                 const uint64_t *swo, uint32_t n, uint64_t *out, int32_t *status, uint64_t avail,
                 cpk::DecStreams sd, hipStream_t s, int which = 0) {
+  // which: 0 the context's choice, 1 the block map, 2 the record index, 3
+  // the block map's dense form (decode_kernel<.., true>)
   const bool v2 = which ? which == 2 : dec_v2(ctx);
+  const bool dense = which == 3;
   const uint32_t lds = v2 ? cpk::kD2Lds : cpk::kDecLds;
   const unsigned per_cu = (unsigned)min(8u, 160u * 1024u / lds);
   unsigned grid = per_cu * (unsigned)ctx->cus;
@@ -2152,9 +2061,15 @@ void dec_launch(cpk_ctx ctx, bool stream, unsigned want, const uint8_t *packed, 
   else if (v2)
     hipLaunchKernelGGL(cpk::decode2_kernel<false>, dim3(grid), dim3(cpk::kD2Threads), lds, s, packed, in_off, swo, n,
                        out, status, tk, avail, sd);
+  else if (stream && dense)
+    hipLaunchKernelGGL((cpk::decode_kernel<true, true>), dim3(grid), dim3(cpk::kDecThreads), lds, s, packed, in_off,
+                       swo, n, out, status, tk, avail, sd);
   else if (stream)
     hipLaunchKernelGGL(cpk::decode_kernel<true>, dim3(grid), dim3(cpk::kDecThreads), lds, s, packed, in_off, swo, n,
                        out, status, tk, avail, sd);
+  else if (dense)
+    hipLaunchKernelGGL((cpk::decode_kernel<false, true>), dim3(grid), dim3(cpk::kDecThreads), lds, s, packed, in_off,
+                       swo, n, out, status, tk, avail, sd);
   else
     hipLaunchKernelGGL(cpk::decode_kernel<false>, dim3(grid), dim3(cpk::kDecThreads), lds, s, packed, in_off, swo, n,
                        out, status, tk, avail, sd);
@@ -2197,7 +2112,7 @@ static int decode_batch_impl(cpk_ctx ctx, const void *d_packed, const uint64_t *
   }
   // by density, decided on the device (dec_gate_kernel): both enqueued, the
   // one not chosen returns at its first instruction
-  uint32_t *skip = ctx->tickets + cpk::kTkGate + 4;
+  uint32_t *skip = ctx->tickets + cpk::kTkGate + 8;  // [3]: block map, record index, dense block map
   hipLaunchKernelGGL(cpk::dec_gate_kernel, dim3(1), dim3(64), 0, s, (const uint64_t *)d_in_off, d_swo, n, skip);
   if (probe && n <= 32) {
     // A few pieces: read their extent back (one sync).  With >= 8 MiB of
@@ -2228,6 +2143,8 @@ static int decode_batch_impl(cpk_ctx ctx, const void *d_packed, const uint64_t *
              cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr, skip}, s, 1);
   dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, in_off, d_swo, n, (uint64_t *)d_out, d_status, 0,
              cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr, skip + 1}, s, 2);
+  dec_launch(ctx, false, (n + 3) / 4, (const uint8_t *)d_packed, in_off, d_swo, n, (uint64_t *)d_out, d_status, 0,
+             cpk::DecStreams{nullptr, nullptr, nullptr, 0, nullptr, skip + 2}, s, 3);
   return hip_ok(hipGetLastError());
 }
 
@@ -2486,9 +2403,12 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
                      (const uint64_t *)mwords, nm, (const uint64_t *)bs0, mwoff);
   hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
                      (const uint64_t *)d_msg_seg_off, nm, (const uint64_t *)bs1, d_msg_seg_off);
+  uint64_t pk[2] = {0, 0};  // the messages' packed range (the decoder's density choice)
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(&h_totals[0], mwoff + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipMemcpyAsync(&h_totals[1], d_msg_seg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(&pk[0], d_msg_off, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(&pk[1], d_msg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return CPK_EDEVICE;
   if (h_totals[0] > out_cap_words || h_totals[1] > seg_cap) return CPK_ENOMEM;
@@ -2502,12 +2422,15 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
       return CPK_EDEVICE;
     // the messages' streams largest first (ord_*: a counting sort by size class)
     ord_launch(mwords, nm, ohist, ord, s);
-    // the stream ends overwrite the words array (no longer needed)
+    // the stream ends overwrite the words array (no longer needed); dense
+    // batches (packed bytes >= 80 % of the words') take the block map's
+    // dense form, as dec_gate_kernel picks it for cpk_decode_batch
+    const bool dense = ctx->decoder == 3 && pk[1] >= pk[0] && 100 * (pk[1] - pk[0]) >= 80 * 8 * h_totals[0];
     dec_launch(ctx, true, (nm + 3) / 4, (const uint8_t *)d_packed, d_seg_in_off, (const uint64_t *)d_seg_word_off,
                (uint32_t)h_totals[1], (uint64_t *)d_out, d_seg_status, 0,
                cpk::DecStreams{mbeg, d_msg_off + 1, d_msg_seg_off, nm, mwords, nullptr,
                                ord},
-               s);
+               s, dense ? 3 : 0);
     hipLaunchKernelGGL(cpk::msg_final_kernel, dim3(tg), dim3(tb), 0, s, d_msg_off, nm,
                        (const uint64_t *)d_msg_seg_off, (const uint64_t *)mwords,
                        (const int32_t *)d_seg_status, d_msg_status);

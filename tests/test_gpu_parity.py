@@ -790,3 +790,74 @@ def test_decode_batch_few_large_pieces_device(ctx, oracle):
             assert st[0] != 0 and np.array_equal(out[8 * int(swo[1]):], data[8 * int(swo[1]):])
         else:
             assert (st == 0).all() and np.array_equal(out, data)
+
+
+@pytest.mark.parametrize("kind", ["runs", "tagged", "mixed"])
+def test_dense_batches_serial_windows(ctx, oracle, kind):
+    """Dense batches (packed >= 80 % of the words) decode in the block map's
+    dense form: windows of few, long records walked by one lane
+    (decode_body<.., kSerial>), the rest in parallel.  Covered: 0xFF runs
+    (the serial walk's case), dense data of tagged words (one zero byte per
+    word: a serial walk passes its record cap and gives the window back,
+    then the cooldown), and both mixed, over pieces of many windows, ragged
+    sizes and a piece ending mid-window; device-resident and host forms,
+    against the oracle."""
+    rng = np.random.default_rng({"runs": 21, "tagged": 22, "mixed": 23}[kind])
+    sizes = [8192, 8191, 300, 16384, 1, 40000, 5000, 0, 8192, 777]
+    parts = []
+    for n in sizes:
+        w = rng.integers(1, 256, size=(n, 8), dtype=np.uint8)
+        if kind == "tagged":
+            w[np.arange(n), rng.integers(0, 8, size=n)] = 0          # L words: a record each
+        elif kind == "mixed":
+            sel = rng.random(n) < 0.5
+            w[np.where(sel)[0], rng.integers(0, 8, size=int(sel.sum()))] = 0
+            w[rng.random(n) < 0.02] = 0
+        else:
+            w[rng.random(n) < 0.03] = 0                              # rare zero words end the runs
+        parts.append(w.reshape(-1))
+    data = np.concatenate(parts)
+    swo = _swo(sizes)
+    pk, off = _check_batch(ctx, oracle, data, swo)
+    assert len(pk) >= 0.8 * len(data)  # (the dense form's batches)
+    # device-resident batch decode (dec_gate_kernel picks the dense form)
+    import torch
+    d_pk = torch.zeros(len(pk) + 64, dtype=torch.uint8, device="cuda")
+    d_pk[: len(pk)] = torch.from_numpy(pk)
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    d_swo = torch.from_numpy(swo.astype(np.int64)).cuda()
+    d_out = torch.zeros(int(swo[-1]) + 1, dtype=torch.int64, device="cuda")
+    d_st = torch.full((len(sizes),), 99, dtype=torch.int32, device="cuda")
+    ctx.decode_batch(d_pk, d_off, d_swo, d_out, d_st)
+    torch.cuda.synchronize()
+    assert (d_st.cpu().numpy() == 0).all()
+    assert d_out.cpu().numpy()[: int(swo[-1])].view(np.uint8).tobytes() == data.tobytes()
+    # corrupted dense pieces (a flipped byte mid-piece, cuts, a trailing
+    # byte): statuses are the oracle's, whichever walk saw the window
+    cases = []
+    p0 = bytes(pk[int(off[0]):int(off[1])])
+    n0 = sizes[0]
+    for k in range(12):
+        b = bytearray(p0)
+        r = k % 4
+        if r == 0:
+            i = int(rng.integers(0, len(b)))
+            b[i] = int(rng.integers(0, 256))
+        elif r == 1:
+            b = b[: int(rng.integers(1, len(b)))]
+        elif r == 2:
+            b += b"\x00"
+        else:
+            i = int(rng.integers(len(b) // 4, len(b) // 2))
+            b[i] = 0xFF
+        cases.append(bytes(b))
+    packed = b"".join(cases)
+    dec, st = ctx.decode_host(np.frombuffer(packed, np.uint8), _swo([len(c) for c in cases]),
+                              _swo([n0] * len(cases)))
+    for i, c in enumerate(cases):
+        ost, out, used = oracle.unpack(c, 8 * n0)
+        if ost == oracle.OK and used != len(c):
+            ost = oracle.ETRAILING
+        assert st[i] == ost, (kind, i, st[i], ost)
+        if ost == oracle.OK:
+            assert dec[8 * n0 * i: 8 * n0 * (i + 1)].tobytes() == out
