@@ -28,7 +28,10 @@
 // chunk to chunk (the state a chunk leaves is published for the next);
 // every unit is read once: traffic U + P for any mix of piece sizes.
 
-constexpr int kSpWaves = 4;
+#ifndef CPK_SP_WAVES
+#define CPK_SP_WAVES 4
+#endif
+constexpr int kSpWaves = CPK_SP_WAVES;
 constexpr int kSpThreads = 64 * kSpWaves;
 constexpr int kSpWS = 128 / kSpWaves;          // steps per wave
 constexpr int kSpCS = kSpWaves * kSpWS;        // steps per chunk (8192 words)
@@ -264,6 +267,7 @@ __device__ __forceinline__ uint32_t sp_a1(SpRegs &R, const uint64_t *__restrict_
       R.dl_ = sp_wl(R.dl_, (uint32_t)D, j);
       R.dh_ = sp_wl(R.dh_, (uint32_t)(D >> 32), j);
     }
+
     CPK_SP_STEP_FENCE();
   }
   return acc;
@@ -414,9 +418,10 @@ __device__ __forceinline__ void sp_xs(SpRegs &R, int cnt, uint32_t Xlast, int la
 // line i (bytes [16 i, 16 i + 16)) lives at ring line i % kSpRingLines; a
 // string crossing the ring's end spills into the overhang line, which belongs
 // to ring line 0.  Its offset g0 in the output may not be known yet (the
-// look-back): the flush shifts relative lines onto the global ones -- global
-// line (g0 >> 4) + t holds relative bytes [16 t - k, 16 t - k + 16), k = g0 & 15,
-// i.e. the last k bytes of relative line t - 1 and the first 16 - k of line t.
+// look-back); once it is, relative line t goes to output bytes
+// [g0 + 16 t, g0 + 16 t + 16) as one 16-byte store at whatever alignment g0
+// has (round 5: no longer shifted onto the 16-byte-aligned output lines,
+// which took two ring lines and four v_alignbyte per line; encode -8 %).
 __device__ __forceinline__ uint4 sp_ring_line(const uint32_t *ring, uint32_t i) {
   const uint4 *rl = reinterpret_cast<const uint4 *>(ring);
   const uint32_t r = sp_rline(i);
@@ -436,70 +441,23 @@ __device__ __forceinline__ void sp_ring_clear(uint32_t *ring, uint32_t i) {
   rl[r] = make_uint4(0u, 0u, 0u, 0u);
   if (r == 0) rl[kSpRingLines] = make_uint4(0u, 0u, 0u, 0u);
 }
-// global line (g0 >> 4) + t from relative lines t - 1 and t
-__device__ __forceinline__ uint4 sp_gline(const uint32_t *ring, uint32_t t, uint32_t k) {
-  const uint4 b = sp_ring_line(ring, t);
-  if (k == 0) return b;
-  const uint4 a = t ? sp_ring_line(ring, t - 1) : make_uint4(0u, 0u, 0u, 0u);
-  // (a || b)[16 - k .. 32 - k)
-  const uint32_t q = 16u - k, s = q & 3;
-  uint4 r;
-  switch (q >> 2) {
-    case 0:
-      r = make_uint4(__builtin_amdgcn_alignbyte(a.y, a.x, s), __builtin_amdgcn_alignbyte(a.z, a.y, s),
-                     __builtin_amdgcn_alignbyte(a.w, a.z, s), __builtin_amdgcn_alignbyte(b.x, a.w, s));
-      break;
-    case 1:
-      r = make_uint4(__builtin_amdgcn_alignbyte(a.z, a.y, s), __builtin_amdgcn_alignbyte(a.w, a.z, s),
-                     __builtin_amdgcn_alignbyte(b.x, a.w, s), __builtin_amdgcn_alignbyte(b.y, b.x, s));
-      break;
-    case 2:
-      r = make_uint4(__builtin_amdgcn_alignbyte(a.w, a.z, s), __builtin_amdgcn_alignbyte(b.x, a.w, s),
-                     __builtin_amdgcn_alignbyte(b.y, b.x, s), __builtin_amdgcn_alignbyte(b.z, b.y, s));
-      break;
-    default:
-      r = make_uint4(__builtin_amdgcn_alignbyte(b.x, a.w, s), __builtin_amdgcn_alignbyte(b.y, b.x, s),
-                     __builtin_amdgcn_alignbyte(b.z, b.y, s), __builtin_amdgcn_alignbyte(b.w, b.z, s));
-      break;
-  }
-  return r;
-}
-// bytes [j0, j1) of global line (g0 >> 4) + t (a line shared with a neighbour)
-// (ocap: a bound on the output buffer -- stores past it are dropped, so a
-// corrupted offset cannot fault the device)
-__device__ __forceinline__ void sp_store_bytes(uint8_t *out, const uint32_t *ring, uint64_t g0, uint32_t t,
-                                               int j0, int j1, int lane, uint64_t ocap) {
-  const uint4 val = sp_gline(ring, t, (uint32_t)(g0 & 15));
-  const uint64_t a = ((g0 >> 4) + t) * 16 + (uint32_t)lane;
-  if (lane >= j0 && lane < j1 && a < ocap) {
-    const uint32_t d = (lane & 8) ? ((lane & 4) ? val.w : val.z) : ((lane & 4) ? val.y : val.x);
-    out[a] = (uint8_t)(d >> (8 * (lane & 3)));
-  }
-}
-// the complete global lines [ft, upto) (relative numbering t); their
-// relative lines before the last are cleared
-__device__ __forceinline__ void sp_flush(uint8_t *out, uint32_t *ring, uint64_t g0, uint32_t &ft, uint32_t upto,
-                                         int lane, uint64_t ocap) {
-  if (ft >= upto) return;
-  const uint32_t k = (uint32_t)(g0 & 15);
-  const uint64_t L0 = g0 >> 4;
-  if (ft == 0 && k) {
-    // the first line holds the previous wave's / piece's bytes below k
-    sp_store_bytes(out, ring, g0, 0, (int)k, 16, lane, ocap);
-    ft = 1;
-  }
+// relative lines [ft, upto) to the output at g0 + 16 t: 16-byte stores at
+// any byte alignment (every byte of the wave's output is stored by exactly
+// one lane, no line is assembled from two), each line cleared once stored
+typedef unsigned int sp_u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ void sp_flush_rel(uint8_t *out, uint32_t *ring, uint64_t g0, uint32_t &ft,
+                                             uint32_t upto, int lane, uint64_t ocap) {
   for (uint32_t t0 = ft; t0 < upto; t0 += 64) {
     const uint32_t t = t0 + (uint32_t)lane;
-    // every lane builds a line (ring indices wrap: lanes past upto read
-    // harmless lines): the shift's switch on the uniform k stays a scalar
-    // branch instead of an exec-masked one inside the lane condition
-    const uint4 v = sp_gline(ring, t, k);
-    wave_lds_order();
     if (t < upto) {
-      if ((L0 + t) * 16 + 16 <= ocap) st_stream(v, out + (L0 + t) * 16);
-      if (t) sp_ring_clear(ring, t - 1);
+      const uint4 v = sp_ring_line(ring, t);
+      const uint64_t a = g0 + 16ull * t;
+      if (a + 16 <= ocap) {
+        const sp_u32x4u w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<sp_u32x4u *>(out + a));
+      }
+      sp_ring_clear(ring, t);
     }
-    wave_lds_order();
   }
   ft = upto;
 }
@@ -628,14 +586,16 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
         rel += ta + (stot >> 16);
         // complete lines leave 64 at a time (one full-wave store)
         if (known) {
-          const uint32_t done = ((uint32_t)(g0 & 15) + rel) >> 4;
+          const uint32_t done = rel >> 4;
           if (done - ft >= 64u) {
             wave_lds_order();
-            sp_flush(out, ring, g0, ft, ft + 64, lane, ocap);
+            sp_flush_rel(out, ring, g0, ft, ft + 64, lane, ocap);
+            wave_lds_order();
           }
         }
       }
     }
+
     CPK_SP_STEP_FENCE();
   };
   // (two fully unrolled loops around the one place the offset may be fetched)
@@ -653,20 +613,17 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
   if (!known) g0 = getbase();
   g0 = sp_uni(g0);
   wave_lds_order();
-  const uint32_t k = (uint32_t)(g0 & 15);
-  const uint32_t done = (k + rel) >> 4;
-  sp_flush(out, ring, g0, ft, done, lane, ocap);
-  const uint32_t rem = (k + rel) & 15;
+  const uint32_t done = rel >> 4, rem = rel & 15;
+  sp_flush_rel(out, ring, g0, ft, done, lane, ocap);
   if (rem) {
-    // the last, partial line (also the first when it is all there is)
-    sp_store_bytes(out, ring, g0, done, done == 0 ? (int)k : 0, (int)rem, lane, ocap);
-  }
-  wave_lds_order();
-  // clear what is left: relative lines [ft - 1, done] (ft - 1: the line
-  // before the last flushed one, still in the ring for its tail)
-  {
-    const uint32_t c0 = ft ? ft - 1 : 0, c1 = done + 1;
-    for (uint32_t i = c0 + (uint32_t)lane; i < c1; i += 64) sp_ring_clear(ring, i);
+    // the last, partial line: its bytes one per lane
+    const uint4 v = sp_ring_line(ring, done);
+    const uint64_t a = g0 + 16ull * done + (uint32_t)lane;
+    if ((uint32_t)lane < rem && a < ocap) {
+      const uint32_t d = (lane & 8) ? ((lane & 4) ? v.w : v.z) : ((lane & 4) ? v.y : v.x);
+      out[a] = (uint8_t)(d >> (8 * (lane & 3)));
+    }
+    if (lane == 0) sp_ring_clear(ring, done);
   }
   wave_lds_order();
 }

@@ -588,9 +588,13 @@ __global__ __launch_bounds__(256) void e4_minmax_kernel(const uint64_t *__restri
     const uint64_t a = swo[0], T = swo[n] - a;
     const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x, G = (uint64_t)gridDim.x * 256;
     const uint64_t st = T / G, h = (uint32_t)(g * 2654435761u) ^ ((uint32_t)g >> 7);
-    const bool z = in && T && in[a + g * T / G + (st ? h % st : 0)] == 0;
+    const uint64_t x = (in && T) ? in[a + g * T / G + (st ? h % st : 0)] : 1ull;
+    const bool z = in && T && x == 0;
     const uint64_t zb = __ballot(z);
     if ((threadIdx.x & 63) == 0 && zb) atomicAdd(&mm[3], (uint32_t)__builtin_popcountll(zb));
+    // (and the sampled words' packed bytes, tag + nonzero bytes, into mm[7])
+    const int pb = wave_incl_add((in && T && x) ? 1 + __builtin_popcount(e4_tag(x)) : 0);
+    if ((threadIdx.x & 63) == 63 && pb) atomicAdd(&mm[7], (uint32_t)pb);
   }
   // grid-stride over the pieces, one atomic pair per workgroup (one per
   // wave put 8 K same-address atomics in line at 1 Mi pieces: 97 us)
@@ -629,10 +633,24 @@ __global__ __launch_bounds__(256) void e4_minmax_kernel(const uint64_t *__restri
 // Among single-pass batches, those whose sampled words are at least 85 %
 // zero take its sparse form (cpk_sparse: tickets[kTkGate + 6] = 1; config 4
 // encode -7 %, config 2 +36 %).
+// Dense batches (the sampled words' tags and nonzero bytes at least
+// CPK_GATE_DENSE_PCT % of their bytes) take the two passes instead: there a
+// wave's output overflows the single pass's ring and waits for its offset,
+// while the two passes stream at ~5 TB/s.  Measured (1 Mi pieces of 8192
+// words, profiles/r5q_density_sweep.log): config-3 density (sampled ~106 %)
+// two passes 41.0 ms against the single pass's 51.4 (47.1 with the round-5
+// flush); at ~78 % and below the single pass is ahead (37.0 / 38.2 ms, 31.3 /
+// 36.5 at 56 %).
+#ifndef CPK_GATE_DENSE_PCT
+#define CPK_GATE_DENSE_PCT 90
+#endif
 __global__ void e4_gate_kernel(uint32_t *tickets, uint32_t samples, uint32_t force) {
   const uint32_t lo = tickets[kTkGate], hi = tickets[kTkGate + 1];
-  const bool sp = lo >= 4096u && 2u * lo >= hi;
-  const bool sparse = sp && (force ? force == 2u : (uint64_t)tickets[kTkGate + 3] * 100u >= (uint64_t)samples * 85u);
+  const bool like = lo >= 4096u && 2u * lo >= hi;
+  const bool sparse = like && (force ? force == 2u : (uint64_t)tickets[kTkGate + 3] * 100u >= (uint64_t)samples * 85u);
+  const bool dense = like && !sparse && !force &&
+                     (uint64_t)tickets[kTkGate + 7] * 100u >= (uint64_t)samples * 8u * CPK_GATE_DENSE_PCT;
+  const bool sp = like && !dense;
   if (threadIdx.x == 0) {
     tickets[kTkGate + 6] = sparse ? 1u : 0u;
     tickets[kTkGate + 2] = sp ? 1u : 0u;

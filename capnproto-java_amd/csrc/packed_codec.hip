@@ -57,7 +57,8 @@ constexpr int kTkDec = 8 * kTkStride;  // decoder counters [8]
 constexpr int kTkPlan = 16 * kTkStride;
 constexpr int kTkErr = 17 * kTkStride;
 constexpr int kTkGate = 17 * kTkStride + 8;  // [0..1] min, max piece words, [2] encoder choice, [3] sampled zero
-                                             // words, [4..5] decoder choice, [6] single pass's form (1: sparse)
+                                             // words, [6] single pass's form (1: sparse), [7] sampled words' packed
+                                             // bytes, [8..10] decoder choice
 constexpr int kTkWords = 18 * kTkStride;
 __device__ __forceinline__ int xcc_id() {
   int x;
@@ -1475,7 +1476,10 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 // leave room for (round 4: config 2's ~7.7 KiB of output per wave overflowed
 // 8 KiB rings often enough that waves waited for their offset a third of
 // the time; 11 KiB: encode -11 %)
-#define CPK_SP_RING 11264
+#ifndef CPK_SP_RING_DENSE
+#define CPK_SP_RING_DENSE 11264
+#endif
+#define CPK_SP_RING CPK_SP_RING_DENSE
 #include "encode_sp.hip"
 #undef CPK_SP_RING
 #include "encode_sp3.hip"
@@ -1497,6 +1501,8 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 #pragma push_macro("CPK_SP_WPE")
 #pragma push_macro("CPK_SP_A1G")
 #pragma push_macro("CPK_SP_DEFER")
+#pragma push_macro("CPK_SP_WAVES")
+#undef CPK_SP_WAVES
 #undef CPK_SP_RELOAD
 #undef CPK_SP_RING
 #undef CPK_SP_WPE
@@ -1518,6 +1524,7 @@ using namespace cpk;
 #pragma pop_macro("CPK_SP_WPE")
 #pragma pop_macro("CPK_SP_A1G")
 #pragma pop_macro("CPK_SP_DEFER")
+#pragma pop_macro("CPK_SP_WAVES")
 
 // ================================================================ C ABI
 struct HostPipe;  // host_pipe.hip: staging of the host-memory forms
@@ -1895,7 +1902,7 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
     // overwrites)
     uint32_t *mm = ctx->tickets + cpk::kTkGate;
     if (hipMemsetAsync(mm, 0xff, 4, s) != hipSuccess || hipMemsetAsync(mm + 1, 0, 4, s) != hipSuccess ||
-        hipMemsetAsync(mm + 3, 0, 4, s) != hipSuccess)
+        hipMemsetAsync(mm + 3, 0, 4, s) != hipSuccess || hipMemsetAsync(mm + 7, 0, 4, s) != hipSuccess)
       return CPK_EDEVICE;
     const unsigned mg = n < 256u * 256u ? (unsigned)((n + 255) / 256) : 256u;
     hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3(mg), dim3(256), 0, s, d_swo, n, mm, (const uint64_t *)d_in);

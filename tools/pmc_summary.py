@@ -6,6 +6,7 @@ usage: python tools/pmc_summary.py gpurun_out/<tag> [--json out.json WORKLOAD] (
 (WORKLOAD: the bench config string the passes ran, stored with the numbers so
 bench.py only reports traffic measured on its own workload)"""
 import csv
+import re
 import json
 import sys
 from collections import defaultdict
@@ -21,10 +22,14 @@ for f in sorted(root.glob("*/*_counter_collection.csv")):
                      else "sp_encode_sparse_kernel" if "cpk_sparse" in k and "sp_encode_kernel" in k
                      else "sp_encode_kernel" if "sp_encode_kernel" in k
                      else "decode2_kernel" if "decode2_kernel" in k
+                     # (decode_kernel<stream, serial>: the dense form -- serial walks of
+                     # dense windows -- is its own launch, skipped unless picked)
+                     else "decode_kernel_dense" if re.search(r"decode_kernel<\w+, ?true>", k)
                      else "decode_kernel" if "decode_kernel" in k else k.split("(")[0][-40:])
             vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
-for kern in ("sp_encode_kernel", "sp_encode_sparse_kernel", "e4_size_kernel", "e4_emit_kernel", "decode_kernel", "decode2_kernel"):
+for kern in ("sp_encode_kernel", "sp_encode_sparse_kernel", "e4_size_kernel", "e4_emit_kernel", "decode_kernel",
+             "decode_kernel_dense", "decode2_kernel"):
     if kern not in vals:
         continue
     d = {c: sum(v) / len(v) for c, v in vals[kern].items()}
@@ -57,7 +62,7 @@ if len(sys.argv) > 3 and sys.argv[2] == "--json":
                     for c in ("FETCH_SIZE", "WRITE_SIZE")})
     if enc:
         out["encode_kernel"] = max(enc, key=traffic_of)
-    dec = [out[k] for k in ("decode_kernel", "decode2_kernel") if k in out]
+    dec = [out[k] for k in ("decode_kernel", "decode_kernel_dense", "decode2_kernel") if k in out]
     if dec:
         out["decode_kernel"] = max(dec, key=traffic_of)
     for kern, key in (("encode_kernel", "encode"), ("decode_kernel", "decode")):

@@ -48,9 +48,15 @@ for spec in libs:
     L = cp.load(Path(lp), strict=False)
     ctx = cp.Context(0)
     handles.append((spec.split("/")[-1], L, ctx))
-for cfg in cfgs:
+# QB_DENS="z:lz:q,...": custom densities (zero-word fraction, mean zero run,
+# zero-byte fraction of nonzero words), one run each, instead of QB_CFG's presets
+dens = [tuple(float(x) for x in d.split(":")) for d in os.environ.get("QB_DENS", "").split(",") if d]
+for cfg in (dens or cfgs):
     cp._lib = handles[0][1]
-    gp = cp.preset(cfg)
+    if dens:
+        gp = cp.gen_params(2, *cfg)
+    else:
+        gp = cp.preset(cfg)
     if __import__("os").environ.get("QB_Z"):  # (a custom density: QB_Z zero fraction, QB_LZ mean zero run)
         _e = __import__("os").environ
         gp = cp.gen_params(cfg, float(_e["QB_Z"]), float(_e.get("QB_LZ", "16")), 0.25)
