@@ -40,10 +40,13 @@ constexpr uint32_t kE4RingDw = kE4RingBytes / 4;
 
 __device__ __forceinline__ uint32_t e4_tag(uint64_t v) {
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-  const uint32_t tl = ((lo & 0x7f7f7f7fu) + 0x7f7f7f7fu) | lo;
-  const uint32_t th = ((hi & 0x7f7f7f7fu) + 0x7f7f7f7fu) | hi;
-  const uint32_t y = ((tl >> 7) & 0x01010101u) | ((th >> 3) & 0x10101010u);
-  return (y | (y >> 7) | (y >> 14) | (y >> 21)) & 0xffu;
+  // bit 7 of each byte: the byte is nonzero (no carry crosses a byte); the
+  // eight flags gathered by two u8 dot products with weights 2^k (9 VALU
+  // instead of the 15 of shifts and ORs: round 5, config 2 encode -2.3 %,
+  // config 4 -14 %)
+  const uint32_t tl = (((lo & 0x7f7f7f7fu) + 0x7f7f7f7fu) | lo) & 0x80808080u;
+  const uint32_t th = (((hi & 0x7f7f7f7fu) + 0x7f7f7f7fu) | hi) & 0x80808080u;
+  return __builtin_amdgcn_udot4(th, 0x80402010u, __builtin_amdgcn_udot4(tl, 0x08040201u, 0u, false), false) >> 7;
 }
 
 // bytes [j0, j1) of global line L from the ring, then clears the ring line

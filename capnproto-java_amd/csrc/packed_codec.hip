@@ -165,15 +165,6 @@ __device__ __forceinline__ uint32_t chunk_div(uint32_t r) {
   return __umul24(r, kM) >> 20;
 }
 
-// nonzero-byte mask of a 32-bit half: bit b set iff byte b != 0
-__device__ __forceinline__ uint32_t nzmask4(uint32_t d) {
-  uint32_t t = (((d & 0x7f7f7f7fu) + 0x7f7f7f7fu) | d) & 0x80808080u;
-  uint32_t x = t >> 7;          // bits 0,8,16,24
-  x |= x >> 7;                  // bits 0,1 8,9 16,17 ...
-  x |= x >> 14;                 // bits 0..3
-  return x & 0xfu;
-}
-
 // LUT entries.  compact: byte j = index of the j-th set bit of m (else 0x0C
 // = zero byte for v_perm).  expand: byte i = popcount(m & ((1<<i)-1)) if bit
 // i is set, else 0x0C.
