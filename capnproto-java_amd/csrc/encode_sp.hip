@@ -49,12 +49,18 @@ static_assert(kSpRing % 16 == 0, "whole lines");
 __device__ __forceinline__ uint32_t sp_rline(uint32_t i) {
   return (kSpRingLines & (kSpRingLines - 1)) == 0 ? (i & (kSpRingLines - 1)) : (i % kSpRingLines);
 }
-constexpr uint32_t kSpRingStride = kSpRing + 16;  // + one overhang line (line 0's spill)
+// overhang lines past the ring's end: a step's strings are laid out from the
+// ring position of its first byte without wrapping, so up to a step's 640
+// bytes + a string's spill land past the end (41 lines; the reader ORs line
+// r < 41 with overhang line r).  Round 5: no per-string wrap (config 2
+// encode -0.6 %, config 4 -1.8 %)
+constexpr uint32_t kSpOvLines = 41;
+constexpr uint32_t kSpRingStride = kSpRing + 16 * kSpOvLines;
 constexpr uint32_t kSpoLut = 0;                                      // u64[256]
 constexpr uint32_t kSpoMsk = 2048;                                   // u64[kSpCS][3]
 constexpr uint32_t kSpoRing = kSpoMsk + kSpCS * 24;                  // per wave
 constexpr uint32_t kSpoScr = kSpoRing + kSpWaves * kSpRingStride;    // u64[32]
-constexpr uint32_t kSpLds = kSpoScr + 32 * 8;                        // 37,632 B (4 waves)
+constexpr uint32_t kSpLds = kSpoScr + 32 * 8;  // 53,056 B (dense form, 11 KiB rings), 24,384 B (sparse form)
 static_assert(kSpWaves <= 16 && kSpWS >= 4 && kSpWS <= 32 && kSpWS % 4 == 0, "wave count");
 static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 // scratch words: [0] ticket, [16..16 + waves) wave bytes, [5] piece offset,
@@ -67,6 +73,7 @@ static_assert(kSpoRing % 16 == 0 && kSpoScr % 16 == 0, "LDS alignment");
 #define CPK_SP_WPE 3  // waves per SIMD the registers must allow (3 workgroups per CU)
 #endif
 constexpr int kSpWpe = CPK_SP_WPE;  // workgroups per CU (the grid: kSpWpe x CUs)
+static_assert(kSpLds * kSpWpe <= 160u * 1024u, "the workgroups per CU must fit its LDS");
 
 // status word per piece: [63:62] flag (1 aggregate, 2 inclusive prefix),
 // [61:46] launch epoch, [45:0] value (a relaxed 8-byte agent-scope granule:
@@ -426,8 +433,8 @@ __device__ __forceinline__ uint4 sp_ring_line(const uint32_t *ring, uint32_t i) 
   const uint4 *rl = reinterpret_cast<const uint4 *>(ring);
   const uint32_t r = sp_rline(i);
   uint4 v = rl[r];
-  if (r == 0) {
-    const uint4 o = rl[kSpRingLines];
+  if (r < kSpOvLines) {
+    const uint4 o = rl[kSpRingLines + r];
     v.x |= o.x;
     v.y |= o.y;
     v.z |= o.z;
@@ -439,7 +446,7 @@ __device__ __forceinline__ void sp_ring_clear(uint32_t *ring, uint32_t i) {
   uint4 *rl = reinterpret_cast<uint4 *>(ring);
   const uint32_t r = sp_rline(i);
   rl[r] = make_uint4(0u, 0u, 0u, 0u);
-  if (r == 0) rl[kSpRingLines] = make_uint4(0u, 0u, 0u, 0u);
+  if (r < kSpOvLines) rl[kSpRingLines + r] = make_uint4(0u, 0u, 0u, 0u);
 }
 // relative lines [ft, upto) to the output at g0 + 16 t: 16-byte stores at
 // any byte alignment (every byte of the wave's output is stored by exactly
@@ -512,7 +519,12 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
     const bool zw = m == 0;
     uint32_t cz = 0, cd = 0;
+#if CPK_SP_HCALL
+    // (the dense form: nearly every step has heads, no branch -- config 2
+    // encode -0.9 %; the sparse form keeps it, +36 % without)
+#else
     if (HC)
+#endif
     {
       // a head's count: words to its run's end, at most 255 (:119-131, :143-164)
       const uint32_t X = (uint32_t)__builtin_amdgcn_readlane((int)R.ox, j);
@@ -546,7 +558,7 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
   // a string OR-ed into the ring at relative byte p (r4 / relq: the ring
   // dword of the step's first byte rel and rel >> 2, wave-uniform -- the
   // ring position without a per-lane modulo: p - rel < 1,284)
-  auto put = [&](uint32_t p, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t nb, uint32_t r4, uint32_t relq)
+  auto put = [&](uint32_t p, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t nb, uint32_t c)
       __attribute__((always_inline)) {
     // the string shifted left by p & 3 bytes over four dwords: one v_perm
     // each, selector bytes [4 - b, 8 - b) of (s_k : s_k-1)
@@ -554,8 +566,7 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, b, 0u);  // (b in every byte)
     const uint32_t d0 = __builtin_amdgcn_perm(s0, 0u, sel), d1 = __builtin_amdgcn_perm(s1, s0, sel);
     const uint32_t d2 = __builtin_amdgcn_perm(s2, s1, sel), d3 = __builtin_amdgcn_perm(0u, s2, sel);
-    uint32_t q = r4 + ((p >> 2) - relq);
-    q = q >= kSpRing4 ? q - kSpRing4 : q;
+    const uint32_t q = (p >> 2) + c;
     uint32_t *rp = ring + q;
     if (nb) {  // (zero-length strings would all hit one address)
       atomicOr(rp, d0);
@@ -580,9 +591,12 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
       const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       if (stot) {
         const uint32_t ta = stot & 0xffffu;
-        const uint32_t relq = rel >> 2, r4 = relq % kSpRing4;
-        put(rel + (incl & 0xffffu) - na, a0, a1, a2, na, r4, relq);
-        put(rel + ta + (incl >> 16) - nb2, b0, b1, b2, nb2, r4, relq);
+        {
+          // (per step, scalar: its first dword's ring position minus that dword)
+          const uint32_t qa = rel >> 2, relb = rel + ta, qb = relb >> 2;
+          put(rel + (incl & 0xffffu) - na, a0, a1, a2, na, qa % kSpRing4 - qa);
+          put(relb + (incl >> 16) - nb2, b0, b1, b2, nb2, qb % kSpRing4 - qb);
+        }
         rel += ta + (stot >> 16);
         // complete lines leave 64 at a time (one full-wave store)
         if (known) {

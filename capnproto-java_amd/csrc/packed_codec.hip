@@ -1471,7 +1471,9 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 #define CPK_SP_RING_DENSE 11264
 #endif
 #define CPK_SP_RING CPK_SP_RING_DENSE
+#define CPK_SP_HCALL 1
 #include "encode_sp.hip"
+#undef CPK_SP_HCALL
 #undef CPK_SP_RING
 #include "encode_sp3.hip"
 #include "decode_v2.hip"
