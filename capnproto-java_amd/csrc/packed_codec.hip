@@ -2403,12 +2403,9 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
                      (const uint64_t *)mwords, nm, (const uint64_t *)bs0, mwoff);
   hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
                      (const uint64_t *)d_msg_seg_off, nm, (const uint64_t *)bs1, d_msg_seg_off);
-  uint64_t pk[2] = {0, 0};  // the messages' packed range (the decoder's density choice)
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(&h_totals[0], mwoff + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipMemcpyAsync(&h_totals[1], d_msg_seg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(&pk[0], d_msg_off, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(&pk[1], d_msg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return CPK_EDEVICE;
   if (h_totals[0] > out_cap_words || h_totals[1] > seg_cap) return CPK_ENOMEM;
@@ -2422,15 +2419,16 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
       return CPK_EDEVICE;
     // the messages' streams largest first (ord_*: a counting sort by size class)
     ord_launch(mwords, nm, ohist, ord, s);
-    // the stream ends overwrite the words array (no longer needed); dense
-    // batches (packed bytes >= 80 % of the words') take the block map's
-    // dense form, as dec_gate_kernel picks it for cpk_decode_batch
-    const bool dense = ctx->decoder == 3 && pk[1] >= pk[0] && 100 * (pk[1] - pk[0]) >= 80 * 8 * h_totals[0];
+    // the stream ends overwrite the words array (no longer needed).  (Dense
+    // message batches stay on the plain block map: its dense form, kept for
+    // cpk_decode_batch, decoded config 3's 256 Ki messages in 49.8-49.9 ms
+    // against 48.0 -- profiles/r5w_c3_decode_forms.txt -- though it won at
+    // 32 Ki messages.)
     dec_launch(ctx, true, (nm + 3) / 4, (const uint8_t *)d_packed, d_seg_in_off, (const uint64_t *)d_seg_word_off,
                (uint32_t)h_totals[1], (uint64_t *)d_out, d_seg_status, 0,
                cpk::DecStreams{mbeg, d_msg_off + 1, d_msg_seg_off, nm, mwords, nullptr,
                                ord},
-               s, dense ? 3 : 0);
+               s, 0);
     hipLaunchKernelGGL(cpk::msg_final_kernel, dim3(tg), dim3(tb), 0, s, d_msg_off, nm,
                        (const uint64_t *)d_msg_seg_off, (const uint64_t *)mwords,
                        (const int32_t *)d_seg_status, d_msg_status);
