@@ -309,12 +309,10 @@ def run_rank(args, rank, world, local):
     # (the batch decoder: the record-index one for sparse batches, packed
     # under 15 % of the words' bytes, else the block map; messages: block map)
     forced_d = os.environ.get("CPK_DECODER", "")[:1]
-    # (and the block map's dense form, decode_kernel<.., true>, for piece
-    # batches packed at >= 80 % of the words' bytes: dense windows walked by
-    # one lane; message batches keep the plain form)
+    # (and the block map's dense form, decode_kernel<.., true>, for batches
+    # packed at >= 80 % of the words' bytes: dense windows walked by one lane)
     dec_kernel = "decode2_kernel" if forced_d == "2" or (forced_d != "1" and mso is None and 100 * P < 15 * U) \
-        else "decode_kernel<dense>" if forced_d not in ("1", "2") and mso is None and 100 * P >= 80 * U \
-        else "decode_kernel"
+        else "decode_kernel<dense>" if forced_d not in ("1", "2") and 100 * P >= 80 * U else "decode_kernel"
     dom_enc = enc_ms > dec_ms
     dom_ms = enc_ms if dom_enc else dec_ms
     achieved = (U + P) / (dom_ms * 1e-3) / 1e9

@@ -76,6 +76,11 @@ __device__ __forceinline__ uint32_t take_ordered(uint32_t *ctr) {
   return (uint32_t)__builtin_amdgcn_readlane((int)t, 0) >> 6;
 }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// a wave-uniform 64-bit value into scalar registers
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+}
 
 // ------------------------------------------------------------ wave scans
 // DPP forms (gfx9 row_shr / row_bcast): no lane-compare masks, no LDS.
@@ -744,12 +749,14 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
           more = false;
           break;
         }
-        if (sd.order) j = sd.order[j];
+        // (the stream's values are wave-uniform: kept in scalar registers,
+        // which leaves the stream form's VGPRs to the windows)
+        if (sd.order) j = (uint32_t)__builtin_amdgcn_readfirstlane((int)sd.order[j]);
         sj = j;
-        snext = sd.sbeg ? (uint32_t)sd.spc[j] : 0u;
-        sende = sd.sbeg ? (uint32_t)sd.spc[j + 1] : n;
-        scur = sd.sbeg ? sd.sbeg[j] : 0;
-        slim = sd.sbeg ? sd.send[j] : avail;
+        snext = sd.sbeg ? (uint32_t)__builtin_amdgcn_readfirstlane((int)sd.spc[j]) : 0u;
+        sende = sd.sbeg ? (uint32_t)__builtin_amdgcn_readfirstlane((int)sd.spc[j + 1]) : n;
+        scur = sd.sbeg ? rfl64(sd.sbeg[j]) : 0;
+        slim = sd.sbeg ? rfl64(sd.send[j]) : avail;
         sfail = CPK_OK;
         if (snext >= sende) sd.send_out[j] = scur;
       }
@@ -757,9 +764,9 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       seg = snext++;
     }
     if (seg >= n) break;
-    const uint64_t w0 = swo[seg];
-    const int W = (int)(swo[seg + 1] - w0);
-    const uint64_t a = kStream ? scur : in_off[seg];
+    const uint64_t w0 = rfl64(swo[seg]);
+    const int W = __builtin_amdgcn_readfirstlane((int)(swo[seg + 1] - w0));
+    const uint64_t a = rfl64(kStream ? scur : in_off[seg]);
     const uint32_t P = kStream ? (uint32_t)min(slim - scur, (uint64_t)0xffffffffu)
                                : (uint32_t)(in_off[seg + 1] - a);
     if (kStream && sfail != CPK_OK) {
@@ -2403,9 +2410,12 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
                      (const uint64_t *)mwords, nm, (const uint64_t *)bs0, mwoff);
   hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
                      (const uint64_t *)d_msg_seg_off, nm, (const uint64_t *)bs1, d_msg_seg_off);
+  uint64_t pk[2] = {0, 0};  // the messages' packed range (the decoder's density choice)
   if (hipGetLastError() != hipSuccess ||
       hipMemcpyAsync(&h_totals[0], mwoff + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipMemcpyAsync(&h_totals[1], d_msg_seg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(&pk[0], d_msg_off, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(&pk[1], d_msg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess)
     return CPK_EDEVICE;
   if (h_totals[0] > out_cap_words || h_totals[1] > seg_cap) return CPK_ENOMEM;
@@ -2419,16 +2429,18 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
       return CPK_EDEVICE;
     // the messages' streams largest first (ord_*: a counting sort by size class)
     ord_launch(mwords, nm, ohist, ord, s);
-    // the stream ends overwrite the words array (no longer needed).  (Dense
-    // message batches stay on the plain block map: its dense form, kept for
-    // cpk_decode_batch, decoded config 3's 256 Ki messages in 49.8-49.9 ms
-    // against 48.0 -- profiles/r5w_c3_decode_forms.txt -- though it won at
-    // 32 Ki messages.)
+    // the stream ends overwrite the words array (no longer needed); dense
+    // batches (packed bytes >= 80 % of the words') take the block map's
+    // dense form, as dec_gate_kernel picks it for cpk_decode_batch (config 3:
+    // 48.0 -> 44.4 ms once the stream form's uniform values sat in scalar
+    // registers -- with 36 B/lane of spills it had been 49.9,
+    // profiles/r5aa_stream_sgpr.txt)
+    const bool dense = ctx->decoder == 3 && pk[1] >= pk[0] && 100 * (pk[1] - pk[0]) >= 80 * 8 * h_totals[0];
     dec_launch(ctx, true, (nm + 3) / 4, (const uint8_t *)d_packed, d_seg_in_off, (const uint64_t *)d_seg_word_off,
                (uint32_t)h_totals[1], (uint64_t *)d_out, d_seg_status, 0,
                cpk::DecStreams{mbeg, d_msg_off + 1, d_msg_seg_off, nm, mwords, nullptr,
                                ord},
-               s, 0);
+               s, dense ? 3 : 0);
     hipLaunchKernelGGL(cpk::msg_final_kernel, dim3(tg), dim3(tb), 0, s, d_msg_off, nm,
                        (const uint64_t *)d_msg_seg_off, (const uint64_t *)mwords,
                        (const int32_t *)d_seg_status, d_msg_status);
