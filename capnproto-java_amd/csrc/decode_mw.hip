@@ -225,9 +225,10 @@ __device__ void decode_stream_mw(uint8_t *smem, const uint8_t *__restrict__ pack
   int sfail = CPK_OK;
   uint32_t tb = 0;  // tag of the next piece's first window
   for (uint32_t seg = p0; seg < p1; ++seg) {
-    const uint64_t w0 = swo[seg];
-    const int W = (int)(swo[seg + 1] - w0);
-    const uint64_t a = scur;
+    // (the piece's values are wave-uniform: scalar registers, not VGPRs)
+    const uint64_t w0 = rfl64(swo[seg]);
+    const int W = __builtin_amdgcn_readfirstlane((int)(swo[seg + 1] - w0));
+    const uint64_t a = rfl64(scur);
     if (sfail != CPK_OK || W == 0) {  // (a read() of nothing consumes nothing)
       if (threadIdx.x == 0) {
         status[seg] = sfail;
@@ -253,13 +254,13 @@ __device__ void decode_stream_mw(uint8_t *smem, const uint8_t *__restrict__ pack
     // start past every wave's)
     if (lane == 0) atomicMax(&ms.rounds, r + 1);
     __syncthreads();
-    tb += ms.rounds * kMwWaves;
-    const int st = ms.tmo ? CPK_EDEVICE : ms.st;
+    tb += (uint32_t)__builtin_amdgcn_readfirstlane((int)ms.rounds) * kMwWaves;
+    const int st = __builtin_amdgcn_readfirstlane(ms.tmo ? CPK_EDEVICE : ms.st);
     if (threadIdx.x == 0) {
       status[seg] = st;
       in_off[seg] = a;
     }
-    if (st == CPK_OK) scur = a + ms.fin;
+    if (st == CPK_OK) scur = a + (uint32_t)__builtin_amdgcn_readfirstlane((int)ms.fin);
     sfail = st;
     __syncthreads();  // (ms read by all before the next piece seeds it)
   }
