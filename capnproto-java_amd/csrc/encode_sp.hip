@@ -518,6 +518,9 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
     const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
     const bool zw = m == 0;
+    // (the step's zero words as a mask: the head-count and byte-count
+    // selects below take scalar mask algebra instead of per-lane selects)
+    const uint64_t ZW = __ballot(zw);
     uint32_t cz = 0, cd = 0;
 #if CPK_SP_HCALL
     // (the dense form: nearly every step has heads, no branch -- config 2
@@ -535,9 +538,8 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
       const uint32_t z_lo = sp_ffbl((uint32_t)e);
       const uint32_t z_hi = sp_ffbl((uint32_t)(e >> 32)) | 32u;  // (ctz < 32: | is +)
       const uint32_t tt = min(min(z_lo, z_hi), min(l64 + X, 255u));
-      const uint32_t cn = sp_sel(0u, tt, HC);
-      cz = zw ? cn : 0u;
-      cd = cn - cz;
+      cz = sp_sel(0u, tt, HC & ZW);   // zero-run heads: the count after the 0x00 tag
+      cd = sp_sel(0u, tt, HC & ~ZW);  // 0xFF heads: the count after the 8 bytes
     }
     // the string: tag, the nonzero bytes, the count after a 0x00 / 0xFF tag
     // (c0 is zero for a zero word); a literal-run member is its 8 bytes
@@ -553,7 +555,7 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     // no bytes: a zero word that is no head -- a zero-run member, or a word
     // past the piece's end (A1 left its tag 0, and it is in no mask): the
     // ZO mask, without its two lane reads
-    nb = sp_sel(zw ? 0u : nb, nb, HC);
+    nb = sp_sel(nb, 0u, ZW & ~HC);
   };
   // a string OR-ed into the ring at relative byte p (r4 / relq: the ring
   // dword of the step's first byte rel and rel >> 2, wave-uniform -- the
