@@ -714,14 +714,16 @@ def test_message_host_forms_all_broken(ctx, oracle, chunk_kb, monkeypatch):
             assert got[i] == []
 
 
-@pytest.mark.parametrize("cfg", [2, 4])
+@pytest.mark.parametrize("cfg", [2, 3, 4])
 @pytest.mark.parametrize("words", [2048, 4095, 4096, 8192, 12288])
 def test_gate_edges_and_sparse_form(ctx, oracle, cfg, words):
     """The device gate's edges (encode_v4.hip, e4_gate_kernel): like-sized
     pieces just under and at the single pass's 4 Ki-word threshold, one
     chunk, and 1.5 chunks (two units each); config-4 data (~90 % zero
     words) sends the single-pass batches to its sparse form
-    (cpk_sparse::sp_encode_kernel), config-2 data to the dense one."""
+    (cpk_sparse::sp_encode_kernel), config-2 data to the dense one, and
+    config-3 data (sampled packed bytes >= 90 % of the words') to the two
+    passes (round 5)."""
     n = max(8, (1 << 22) // words)  # ~32 MiB per batch
     swo = _swo([words] * n)
     _check_batch(ctx, oracle, oracle.generate(oracle.preset(cfg), swo), swo)
