@@ -615,6 +615,36 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
       // flight together)
       uint32_t tag, c1, c9;
       rec_bytes(pkw, q, tag, c1, c9);
+      if constexpr (!kStream) {
+      // one path for every tag: a zero run's word reads its (unused) bytes
+      // and lut[0] selects none; lut[0xff] is the identity for a literal
+      // run's words (no divergent branches per word)
+      uint64_t sel = lut[tag];
+#pragma unroll
+      for (int i = 0; i < kBlk; ++i) {
+        // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
+        // run (tag word, then the counted words), or a tagged word
+        const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
+        const int nw = 1 + (int)((zm & c1) + (fm & c9));
+        const uint32_t rp = (fm && ofs) ? q + 2 + 8u * (uint32_t)ofs : q + 1;
+        const uint64_t raw = read8<kAllIn>(pkw, rp, lend, gp, glim, ph, e);
+        const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
+        const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
+        const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
+        words[i] = (uint64_t)x0 | ((uint64_t)x1 << 32);
+        // past the window's last word: stay put (never stored)
+        if (++ofs == nw && i < wleft) {
+          q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
+          ofs = 0;
+          if (i + 1 < kBlk) {
+            rec_bytes(pkw, q, tag, c1, c9);
+            sel = lut[tag];
+          }
+        }
+      }
+      } else {
+      // (the stream form keeps the branches: its register budget is tighter,
+      // and the one-path form measured 3 % slower there, docs/tuning_log.md r5W)
 #pragma unroll
       for (int i = 0; i < kBlk; ++i) {
         // PackedInputStream.java:84-134 per word: zero run, 0xFF literal
@@ -649,6 +679,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
           ofs = 0;
           if (i + 1 < kBlk) rec_bytes(pkw, q, tag, c1, c9);
         }
+      }
       }
       const int kw = min(kBlk, min(ow + T, W) - wbase);
       uint64_t *d = dst + wbase;
