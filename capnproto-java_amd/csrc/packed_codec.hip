@@ -344,7 +344,7 @@ __device__ __forceinline__ DecRec rec_at(const uint8_t *pkw, uint32_t q) {
 // (tail of a literal run reaching past the window) straight from memory
 // (kAllIn: the caller knows x + 12 <= lend -- every record of the window
 // lies in the loaded bytes -- so no check and no memory path)
-template <bool kAllIn = false>
+template <bool kAllIn = false, bool kLa = true>
 __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32_t lend,
                                          const uint8_t *gpiece, uint32_t glim, uint32_t ph,
                                          uint32_t e) {
@@ -355,9 +355,22 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
   // the 16-byte aligned window buffer.
   const bool inw = kAllIn || x + 12 <= lend;
   const uint32_t xl = inw ? x : e;
-  uint32_t sh = (xl + ph) & 3;
-  const uint32_t *pl = reinterpret_cast<const uint32_t *>(pkw + ((int64_t)xl - sh));  // (signed: xl < sh)
-  uint32_t d0 = pl[0], d1 = pl[1], d2 = pl[2];
+  uint32_t sh, d0, d1, d2;
+  if constexpr (kLa) {
+    // from the LDS byte address itself: its low bits are the phase, its
+    // aligned part the first dword (add, and, and; round 5: config-3
+    // messages decode -1.2 %, the dense piece form +1.8 %: not there)
+    typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+    typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+    const uint32_t la = (uint32_t)(uintptr_t)((lds_cu8 *)pkw) + xl;
+    sh = la & 3;
+    lds_cu32 *pl = (lds_cu32 *)(uintptr_t)(la & ~3u);
+    d0 = pl[0], d1 = pl[1], d2 = pl[2];
+  } else {
+    sh = (xl + ph) & 3;
+    const uint32_t *pl = reinterpret_cast<const uint32_t *>(pkw + ((int64_t)xl - sh));  // (signed: xl < sh)
+    d0 = pl[0], d1 = pl[1], d2 = pl[2];
+  }
   if (!kAllIn && !inw) {
     // address-aligned dwords of the packed buffer, none at or past the
     // readable limit glim (piece-relative: the piece's end rounded up to a
@@ -459,7 +472,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
 // window's first record at piece position e, ow piece words before it
 // (decode_body; decode_piece_mw).  Returns false when a record fails (st
 // set); fin: the end of the record that fills the piece, else 0.
-template <bool kStream>
+template <bool kStream, bool kLa = true>
 __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut, uint32_t *blk, int lane,
                                          uint32_t e, int ow, int W, uint32_t P, int T, bool on,
                                          uint32_t entry, uint32_t S, uint64_t onmask, int o0, int myw,
@@ -627,7 +640,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
         const int nw = 1 + (int)((zm & c1) + (fm & c9));
         const uint32_t rp = (fm && ofs) ? q + 2 + 8u * (uint32_t)ofs : q + 1;
-        const uint64_t raw = read8<kAllIn>(pkw, rp, lend, gp, glim, ph, e);
+        const uint64_t raw = read8<kAllIn, kLa>(pkw, rp, lend, gp, glim, ph, e);
         const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
         const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
         const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
@@ -661,9 +674,9 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
           const uint32_t rn = c9;
           nw = 1 + (int)rn;
           adv = 10 + 8 * rn;
-          x = read8<kAllIn>(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
+          x = read8<kAllIn, kLa>(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
         } else {
-          const uint64_t raw = read8<kAllIn>(pkw, q + 1, lend, gp, glim, ph, e);
+          const uint64_t raw = read8<kAllIn, kLa>(pkw, q + 1, lend, gp, glim, ph, e);
           const uint64_t sel = lut[tag];
           const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
           const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
@@ -730,6 +743,9 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
                                             uint64_t *__restrict__ in_off, const uint64_t *__restrict__ swo,
                                             uint32_t n, uint64_t *__restrict__ out, int32_t *__restrict__ status,
                                             uint32_t *ticket, uint64_t avail, DecStreams sd) {
+  // the expansion's 8-byte reads from LDS byte addresses (read8), but in the
+  // dense piece form, where they measured slower
+  constexpr bool kDecLa = kStream || !kSerial;
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem);
   const int lane = lane_id(), w = wave_id();
   uint8_t *wl = smem + 2048 + w * kDecWaveLds;
@@ -890,7 +906,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
             const int T = readlane(o, 0);
             const uint32_t enext = (uint32_t)readlane((int)q, 0);
             uint32_t fin = 0;
-            const bool failed = !win_emit<kStream>(pkw, lut, blk, lane, e, ow, W, P, T, false, e, e, 0ull, 0,
+            const bool failed = !win_emit<kStream, kDecLa>(pkw, lut, blk, lane, e, ow, W, P, T, false, e, e, 0ull, 0,
                                                    0, enext, lend, gp, glim, ph, dst, st, fin, true DEC_PH_ARGS);
             if (failed) break;  // (cannot happen: no record here is checked)
             ow += T;
@@ -941,7 +957,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       WPH(4)
       // ---- 5: error checks, block map, expansion ------------------------------
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
-      const bool failed = !win_emit<kStream>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
+      const bool failed = !win_emit<kStream, kDecLa>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
                                              enext, lend, gp, glim, ph, dst, st, fin, false DEC_PH_ARGS);
       if (failed) break;
       if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
