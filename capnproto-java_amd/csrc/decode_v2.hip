@@ -368,6 +368,7 @@ __global__ __launch_bounds__(kD2Threads, kD2Wpe) void decode2_kernel(
             const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
             const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
             const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
+            // (nontemporal: plain stores wrote 5 % fewer bytes and took 1.7 % longer)
             if (wv < re) __builtin_nontemporal_store((uint64_t)x0 | ((uint64_t)x1 << 32), &dst_w[wv]);
           }
         }

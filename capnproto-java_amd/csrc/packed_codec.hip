@@ -472,7 +472,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
 // window's first record at piece position e, ow piece words before it
 // (decode_body; decode_piece_mw).  Returns false when a record fails (st
 // set); fin: the end of the record that fills the piece, else 0.
-template <bool kStream, bool kLa = true>
+template <bool kStream, bool kLean = true>
 __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut, uint32_t *blk, int lane,
                                          uint32_t e, int ow, int W, uint32_t P, int T, bool on,
                                          uint32_t entry, uint32_t S, uint64_t onmask, int o0, int myw,
@@ -640,7 +640,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
         const int nw = 1 + (int)((zm & c1) + (fm & c9));
         const uint32_t rp = (fm && ofs) ? q + 2 + 8u * (uint32_t)ofs : q + 1;
-        const uint64_t raw = read8<kAllIn, kLa>(pkw, rp, lend, gp, glim, ph, e);
+        const uint64_t raw = read8<kAllIn, kLean>(pkw, rp, lend, gp, glim, ph, e);
         const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
         const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
         const uint32_t x1 = __builtin_amdgcn_perm(rh, rl, (uint32_t)(sel >> 32));
@@ -674,9 +674,9 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
           const uint32_t rn = c9;
           nw = 1 + (int)rn;
           adv = 10 + 8 * rn;
-          x = read8<kAllIn, kLa>(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
+          x = read8<kAllIn, kLean>(pkw, ofs == 0 ? q + 1 : q + 10 + 8 * (uint32_t)(ofs - 1), lend, gp, glim, ph, e);
         } else {
-          const uint64_t raw = read8<kAllIn, kLa>(pkw, q + 1, lend, gp, glim, ph, e);
+          const uint64_t raw = read8<kAllIn, kLean>(pkw, q + 1, lend, gp, glim, ph, e);
           const uint64_t sel = lut[tag];
           const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
           const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
@@ -704,8 +704,21 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
           v4.y = (uint32_t)(words[i] >> 32);
           v4.z = (uint32_t)words[i + 1];
           v4.w = (uint32_t)(words[i + 1] >> 32);
-          st_stream(v4, d + i);
+          st_stream(v4, d + i);  // (nontemporal: plain stores cut writes 3 % and cost 1.8 % time)
         }
+      }
+      else if (kLean && kw == kBlk && kBlk == 4) {
+        // a full block at an odd word: word 0, words 1-2 as one 16-byte
+        // store, word 3 (no per-word branches; round 5: config 2 decode
+        // -0.6 %, the dense piece form +2.2 %: not there)
+        d[0] = words[0];  // (plain: nontemporal 8-byte stores left partial lines, +6 % HBM writes)
+        uint4 v4;
+        v4.x = (uint32_t)words[1];
+        v4.y = (uint32_t)(words[1] >> 32);
+        v4.z = (uint32_t)words[2];
+        v4.w = (uint32_t)(words[2] >> 32);
+        st_stream(v4, d + 1);
+        d[kBlk - 1] = words[kBlk - 1];
       } else {
 #pragma unroll
         for (int i = 0; i < kBlk; ++i)
@@ -743,9 +756,10 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
                                             uint64_t *__restrict__ in_off, const uint64_t *__restrict__ swo,
                                             uint32_t n, uint64_t *__restrict__ out, int32_t *__restrict__ status,
                                             uint32_t *ticket, uint64_t avail, DecStreams sd) {
-  // the expansion's 8-byte reads from LDS byte addresses (read8), but in the
-  // dense piece form, where they measured slower
-  constexpr bool kDecLa = kStream || !kSerial;
+  // the expansion's lean forms (reads from LDS byte addresses, read8; odd
+  // blocks' stores without branches), but in the dense piece form, where
+  // they measured slower
+  constexpr bool kDecLean = kStream || !kSerial;
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem);
   const int lane = lane_id(), w = wave_id();
   uint8_t *wl = smem + 2048 + w * kDecWaveLds;
@@ -906,7 +920,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
             const int T = readlane(o, 0);
             const uint32_t enext = (uint32_t)readlane((int)q, 0);
             uint32_t fin = 0;
-            const bool failed = !win_emit<kStream, kDecLa>(pkw, lut, blk, lane, e, ow, W, P, T, false, e, e, 0ull, 0,
+            const bool failed = !win_emit<kStream, kDecLean>(pkw, lut, blk, lane, e, ow, W, P, T, false, e, e, 0ull, 0,
                                                    0, enext, lend, gp, glim, ph, dst, st, fin, true DEC_PH_ARGS);
             if (failed) break;  // (cannot happen: no record here is checked)
             ow += T;
@@ -957,7 +971,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       WPH(4)
       // ---- 5: error checks, block map, expansion ------------------------------
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
-      const bool failed = !win_emit<kStream, kDecLa>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
+      const bool failed = !win_emit<kStream, kDecLean>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
                                              enext, lend, gp, glim, ph, dst, st, fin, false DEC_PH_ARGS);
       if (failed) break;
       if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
