@@ -120,7 +120,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
       while (q < wend) {
         const uint32_t r = q - g;
         const uint32_t oo = chunk_div<kDecChunk>(r);
-        if ((visa[oo] >> (r - oo * kDecChunk)) & 1) {
+        if ((visa[oo] >> (q & 63u)) & 1) {  // (win_walks: the bit of q mod 64)
           o = (int)oo;
           break;
         }

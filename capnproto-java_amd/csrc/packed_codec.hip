@@ -274,7 +274,7 @@ constexpr int kRound = CPK_DEC_ROUND;  // output words expanded per round
 #define CPK_DEC_BLK 4
 #endif
 constexpr int kBlk = CPK_DEC_BLK;  // output words per expansion block
-// a lane's visited positions: one bit per chunk byte
+// a lane's visited positions: one bit per chunk byte (bit q mod 64 for position q)
 typedef std::conditional<(kDecChunk <= 32), uint32_t, uint64_t>::type VisMask;
 static_assert(kDecChunk <= 64, "visited mask bits");
 // the visited masks (phases 1-3) and the block map (phase 5) share LDS
@@ -417,7 +417,10 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   if (cb < wend) {
     uint32_t pos = cb;
     while (pos < ce) {
-      vis |= (VisMask)1 << (pos - cb);
+      // (the bit of piece position pos mod 64 -- a rotation of the chunk
+      // offsets, distinct for a 56-byte chunk: the shift takes pos itself,
+      // no subtraction per record; round 5: config 2 decode -0.5 %)
+      vis |= (VisMask)1 << (pos & 63u);
       const DecRec r = rec_at(pkw, pos);
       wt += r.nw;
       pos += r.len;
@@ -432,9 +435,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
     while (S < wend) {
       const uint32_t r = S - e;
       const uint32_t ow_ = chunk_div<kDecChunk>(r);
-      uint32_t base = __umul24(ow_, kDecChunk);
-      asm("" : "+v"(base));  // (else folded into a quarter-rate v_mad_u64_u32)
-      if ((visa[ow_] >> (r - base)) & 1) break;
+      if ((visa[ow_] >> (S & 63u)) & 1) break;  // (bit S mod 64, as above)
       const DecRec rr = rec_at(pkw, S);
       lw += rr.nw;
       S += rr.len;
