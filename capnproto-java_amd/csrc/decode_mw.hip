@@ -103,7 +103,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
     pkw = wbuf + (int64_t)padw - (int64_t)g;
     ph = (padw - g) & 3;
     wave_lds_order();
-    ww = win_walks(pkw, visa, lane, g, wend DEC_PH_ARGS);
+    ww = win_walks<false>(pkw, visa, lane, g, wend DEC_PH_ARGS);
   }
   // ---- the entry (serial over the windows) ----------------------------------
   const uint32_t ein = mw_get(&ms.E[slot], t, &ms.tmo);
@@ -124,7 +124,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
           o = (int)oo;
           break;
         }
-        const DecRec rr = rec_at(pkw, q);
+        const DecRec rr = rec_at<false>(pkw, q);
         sw += rr.nw;
         q += rr.len;
       }
@@ -156,7 +156,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
         const uint32_t from = lane == j ? q : entry;
         uint32_t pre = 0;
         for (uint32_t x = ww.cb; x < from;) {
-          const DecRec r = rec_at(pkw, x);
+          const DecRec r = rec_at<false>(pkw, x);
           pre += r.nw;
           x += r.len;
         }

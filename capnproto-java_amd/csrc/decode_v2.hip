@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kD2Threads, kD2Wpe) void decode2_kernel(
         uint32_t pos = cb;
         while (pos < ce) {
           vis |= (D2Vis)1 << (pos - cb);
-          const DecRec r = rec_at(pkw, pos);
+          const DecRec r = rec_at<!kStream>(pkw, pos);
           wt += r.nw;
           pos += r.len;
         }
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kD2Threads, kD2Wpe) void decode2_kernel(
           const uint32_t r = S - e;
           const uint32_t ow_ = r / kD2Chunk;
           if ((visa[ow_] >> (r - ow_ * kD2Chunk)) & 1) break;
-          const DecRec rr = rec_at(pkw, S);
+          const DecRec rr = rec_at<!kStream>(pkw, S);
           lw += rr.nw;
           ++lr;
           S += rr.len;
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kD2Threads, kD2Wpe) void decode2_kernel(
       if (on) {
         uint32_t pre = 0;
         for (uint32_t q = cb; q < entry;) {
-          const DecRec r = rec_at(pkw, q);
+          const DecRec r = rec_at<!kStream>(pkw, q);
           pre += r.nw;
           q += r.len;
         }

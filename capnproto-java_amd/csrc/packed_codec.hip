@@ -318,10 +318,15 @@ __device__ __forceinline__ int wave_min(int v) {
 // the walks.  (Round 5: reading a count byte only for the tags that have one
 // cut the decoder's LDS cycles 22 % and made it 6 % slower -- the dependent
 // second read and its exec-mask branches, docs/tuning_log.md.)
+template <bool k32 = true>
 __device__ __forceinline__ void rec_bytes(const uint8_t *pkw, uint32_t q, uint32_t &tag, uint32_t &c1, uint32_t &c9) {
   tag = pkw[q];
   c1 = pkw[q + 1];
   c9 = pkw[q + 9];
+  // k32: the tag kept a 32-bit value (hipcc otherwise narrows it to 16-bit
+  // ops: a mask and a separate +1 around every popcount; round 5: config 2
+  // decode -1.0 %, the stream forms +5 %: not there)
+  if constexpr (k32) asm("" : "+v"(tag));
 }
 
 // The record whose tag is at piece position q: its byte length and output
@@ -329,9 +334,10 @@ __device__ __forceinline__ void rec_bytes(const uint8_t *pkw, uint32_t q, uint32
 struct DecRec {
   uint32_t len, nw;
 };
+template <bool k32 = true>
 __device__ __forceinline__ DecRec rec_at(const uint8_t *pkw, uint32_t q) {
   uint32_t tag, c1, c9;
-  rec_bytes(pkw, q, tag, c1, c9);
+  rec_bytes<k32>(pkw, q, tag, c1, c9);
   // masks, not nested selects (hipcc turns those into exec-mask branches)
   const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
   DecRec r;
@@ -407,6 +413,7 @@ struct WinWalk {
   uint32_t cb, S, wt, lw;
   uint64_t R;
 };
+template <bool k32 = true>
 __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, int lane, uint32_t e,
                                              uint32_t wend DEC_PH_PARAMS) {
   // ---- 1: speculative chunk walks --------------------------------------
@@ -421,7 +428,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
       // offsets, distinct for a 56-byte chunk: the shift takes pos itself,
       // no subtraction per record; round 5: config 2 decode -0.5 %)
       vis |= (VisMask)1 << (pos & 63u);
-      const DecRec r = rec_at(pkw, pos);
+      const DecRec r = rec_at<k32>(pkw, pos);
       wt += r.nw;
       pos += r.len;
     }
@@ -436,7 +443,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
       const uint32_t r = S - e;
       const uint32_t ow_ = chunk_div<kDecChunk>(r);
       if ((visa[ow_] >> (S & 63u)) & 1) break;  // (bit S mod 64, as above)
-      const DecRec rr = rec_at(pkw, S);
+      const DecRec rr = rec_at<k32>(pkw, S);
       lw += rr.nw;
       S += rr.len;
     }
@@ -505,7 +512,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
           uint32_t ro = (uint32_t)o0;
           for (uint32_t q = entry; q < S && ro <= (uint32_t)(kRound - kBlk);) {
             uint32_t tag, c1, c9;
-            rec_bytes(pkw, q, tag, c1, c9);
+            rec_bytes<!kStream>(pkw, q, tag, c1, c9);
             const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
             atomicMax(&blk[(ro + kBlk - 1) / kBlk], ((ro + 256u) << 12) | (q - e));
             ro += 1u + (zm & c1) + (fm & c9);
@@ -519,7 +526,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         // do the ones after them)
         for (uint32_t q = entry; q < S && ro <= kRound - kBlk;) {
           uint32_t tag, c1, c9;
-          rec_bytes(pkw, q, tag, c1, c9);
+          rec_bytes<!kStream>(pkw, q, tag, c1, c9);
           const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
           const int nw = 1 + (int)((zm & c1) + (fm & c9));
           if (ro + nw > 0)
@@ -628,7 +635,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
       // word: a literal run's words then need only their own reads, all in
       // flight together)
       uint32_t tag, c1, c9;
-      rec_bytes(pkw, q, tag, c1, c9);
+      rec_bytes<!kStream>(pkw, q, tag, c1, c9);
       if constexpr (!kStream) {
       // one path for every tag: a zero run's word reads its (unused) bytes
       // and lut[0] selects none; lut[0xff] is the identity for a literal
@@ -651,7 +658,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
           q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
           ofs = 0;
           if (i + 1 < kBlk) {
-            rec_bytes(pkw, q, tag, c1, c9);
+            rec_bytes<!kStream>(pkw, q, tag, c1, c9);
             sel = lut[tag];
           }
         }
@@ -691,7 +698,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         if (++ofs == nw && i < wleft) {
           q += adv;
           ofs = 0;
-          if (i + 1 < kBlk) rec_bytes(pkw, q, tag, c1, c9);
+          if (i + 1 < kBlk) rec_bytes<!kStream>(pkw, q, tag, c1, c9);
         }
       }
       }
@@ -907,7 +914,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
           if (lane == 0) {
             const int wr = W - ow;  // words left in the piece
             while (q < wend) {
-              const DecRec r = rec_at(pkw, q);
+              const DecRec r = rec_at<!kStream>(pkw, q);
               if (o + (int)r.nw >= wr || o + (int)r.nw > kRound || ++nrec > kDecSerMax) {
                 ok = 0;
                 break;
@@ -938,7 +945,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
 
       WPH(1)
       // ---- 1-3: speculative walks, chain reachability ------------------------
-      const WinWalk ww = win_walks(pkw, visa, lane, e, wend DEC_PH_ARGS);
+      const WinWalk ww = win_walks<!kStream>(pkw, visa, lane, e, wend DEC_PH_ARGS);
       const uint32_t cb = ww.cb, wt = ww.wt, lw = ww.lw, S = ww.S;
       const uint64_t R = ww.R;
       const uint64_t onmask = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)R, 0)) |
@@ -960,7 +967,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       if (on) {
         uint32_t pre = 0;
         for (uint32_t q = cb; q < entry;) {
-          const DecRec r = rec_at(pkw, q);
+          const DecRec r = rec_at<!kStream>(pkw, q);
           pre += r.nw;
           q += r.len;
         }
