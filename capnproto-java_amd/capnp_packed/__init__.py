@@ -18,6 +18,7 @@ if the HIP library cannot be loaded every entry point raises.
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 import numpy as np
@@ -36,6 +37,7 @@ EXPORTS = [
     "cpk_decode_messages", "cpk_encode_messages", "cpk_encode_messages_host",
     "cpk_decode_messages_host", "cpk_encode_host_gather", "cpk_encode_messages_host_gather",
     "cpk_read_message", "cpk_read_message_host", "cpk_ctx_small_fallbacks",
+    "cpk_encode_batch_cap", "cpk_encode_messages_cap", "cpk_ctx_dense_windows",
 ]
 MSG_HEAD_WORDS, MSG_INFO_WORDS = 257, 517  # CPK_MSG_HEAD_WORDS, CPK_MSG_INFO_WORDS
 
@@ -66,7 +68,9 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    p = Path(path or LIB_PATH)
+    # (CPK_LIB: a variant build for A/B timing and profiling tools, so that no
+    # probe ever overwrites the tree's library)
+    p = Path(path or os.environ.get("CPK_LIB") or LIB_PATH)
     if not p.exists():
         raise ImportError(f"capnp_packed: HIP library {p} not built "
                           "(run python capnproto-java_amd/build_native.py)")
@@ -81,6 +85,8 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_ctx_destroy": ([vp], None),
         "cpk_ctx_device": ([vp], i32),
         "cpk_encode_batch": ([vp, vp, vp, u32, u64, vp, vp, vp], i32),
+        "cpk_encode_batch_cap": ([vp, vp, vp, u32, u64, vp, u64, vp, vp], i32),
+        "cpk_encode_messages_cap": ([vp, vp, vp, u32, vp, u32, u64, vp, u64, vp, vp], i32),
         "cpk_decode_batch": ([vp, vp, vp, vp, u32, vp, vp, vp], i32),
         "cpk_encode_host": ([vp, vp, vp, u32, vp, u64, vp], i32),
         "cpk_encode_host_gather": ([vp, vp, vp, u32, vp, u64, vp], i32),
@@ -91,6 +97,7 @@ def load(path: Path | None = None, strict: bool = True) -> ctypes.CDLL:
         "cpk_count_mismatch": ([vp, vp, vp, u64, vp, vp], i32),
         "cpk_ctx_take_error": ([vp, vp], i32),
         "cpk_ctx_small_fallbacks": ([vp], u64),
+        "cpk_ctx_dense_windows": ([vp, vp, ctypes.POINTER(u64), ctypes.POINTER(u64)], i32),
         "cpk_decode_messages": ([vp, vp, vp, u32, u64, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp], i32),
         "cpk_encode_messages": ([vp, vp, vp, u32, vp, u32, u64, vp, vp, vp], i32),
         "cpk_encode_messages_host": ([vp, vp, vp, u32, vp, u32, vp, u64, vp], i32),
@@ -139,6 +146,9 @@ class Context:
         _check(self._lib.cpk_ctx_create(device, ctypes.byref(h)), "cpk_ctx_create")
         self.handle = h
         self.device = device
+        # (the decoder choice the library read at creation: CPK_DECODER 1 / 2
+        # force one decoder, anything else lets the device pick by density)
+        self.decoder_forced = os.environ.get("CPK_DECODER", "") in ("1", "2")
 
     def close(self):
         if getattr(self, "handle", None):
@@ -166,14 +176,47 @@ class Context:
                                         self._stream(stream))
         _check(rc, "cpk_encode_batch")
 
+    def encode_batch_cap(self, d_in, d_seg_word_off, max_seg_words: int, d_out, out_cap: int,
+                         d_out_off, stream=None):
+        """cpk_encode_batch_cap: as encode_batch, with d_out's byte capacity;
+        packed bytes past it are never stored and take_error() then returns
+        CPK_ENOMEM (ArrayOutputStream.java:40-42)."""
+        n = d_seg_word_off.numel() - 1
+        rc = self._lib.cpk_encode_batch_cap(self.handle, d_in.data_ptr(), d_seg_word_off.data_ptr(), n,
+                                            int(max_seg_words), d_out.data_ptr(), int(out_cap),
+                                            d_out_off.data_ptr(), self._stream(stream))
+        _check(rc, "cpk_encode_batch_cap")
+
+    def encode_messages_cap(self, d_in, d_seg_word_off, d_msg_seg_off, max_seg_words: int, d_out,
+                            out_cap: int, d_out_off, stream=None):
+        """cpk_encode_messages_cap: encode_messages with d_out's byte capacity."""
+        nseg = d_seg_word_off.numel() - 1
+        nm = d_msg_seg_off.numel() - 1
+        rc = self._lib.cpk_encode_messages_cap(self.handle, d_in.data_ptr(), d_seg_word_off.data_ptr(),
+                                               nseg, d_msg_seg_off.data_ptr(), nm, int(max_seg_words),
+                                               d_out.data_ptr(), int(out_cap), d_out_off.data_ptr(),
+                                               self._stream(stream))
+        _check(rc, "cpk_encode_messages_cap")
+
     def take_error(self, stream=None) -> int:
-        """Synchronises `stream`; CPK_EINVAL if an encode since the last call
-        met a piece larger than its max_seg_words hint (output undefined)."""
+        """Synchronises `stream`; CPK_ENOMEM if an encode since the last call
+        would have stored packed bytes past its out_cap (the *_cap forms),
+        CPK_EINVAL if it met a piece larger than its max_seg_words hint
+        (output undefined)."""
         return self._lib.cpk_ctx_take_error(self.handle, self._stream(stream))
 
+    def dense_windows(self, stream=None) -> tuple[int, int]:
+        """(windows walked serially, serial walks given back) by the block
+        map's dense form in the last decode (cpk_ctx_dense_windows)."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._lib.cpk_ctx_dense_windows(self.handle, self._stream(stream), ctypes.byref(a),
+                                               ctypes.byref(b)), "cpk_ctx_dense_windows")
+        return int(a.value), int(b.value)
+
     def small_fallbacks(self) -> int:
-        """One-launch host calls whose completion flag was not seen within
-        5 ms (a stream sync stood in); 0 in normal operation."""
+        """One-launch host calls whose completion flag was still unset after
+        the stream sync that stands in past 5 ms (a lost flag); 0 in normal
+        operation, late launches on a busy GPU included."""
         return int(self._lib.cpk_ctx_small_fallbacks(self.handle))
 
     def decode_batch(self, d_packed, d_in_off, d_seg_word_off, d_out, d_status, stream=None):

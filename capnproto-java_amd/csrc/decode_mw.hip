@@ -113,13 +113,13 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
   uint32_t sw = 0, q = ein;
   int o = -1;
   if (live && ein < wend) {
-    j = (int)chunk_div<kDecChunk>(ein - g);
+    j = (int)chunk_owner(ein - g);
     // lane j walks from the entry to the first position some lane visited
     // (the entry itself, usually) or out of the window
     if (lane == j) {
       while (q < wend) {
         const uint32_t r = q - g;
-        const uint32_t oo = chunk_div<kDecChunk>(r);
+        const uint32_t oo = chunk_owner(r);
         if ((visa[oo] >> (q & 63u)) & 1) {  // (win_walks: the bit of q mod 64)
           o = (int)oo;
           break;
@@ -145,7 +145,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
   int myw = 0, T = 0, o0 = 0;
   if (onmask) {
     wave_lds_order();  // (the walks' reads of visa are done)
-    if (on && S < wend) visa[chunk_div<kDecChunk>(S - g)] = (VisMask)S;
+    if (on && S < wend) visa[chunk_owner(S - g)] = (VisMask)S;
     wave_lds_order();
     if (lane != j) entry = (uint32_t)visa[lane];
     if (on) {

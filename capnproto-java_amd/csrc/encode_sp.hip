@@ -878,13 +878,16 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     const uint64_t *__restrict__ pdesc, const uint64_t *__restrict__ tin, uint32_t n,
     uint8_t *__restrict__ out, uint64_t *__restrict__ out_off, uint64_t *status, uint32_t ep,
     uint32_t *ticket, const uint64_t *__restrict__ utab, const uint64_t *__restrict__ nunits,
-    uint64_t *ustate, uint64_t hint, uint32_t *err, const uint64_t *ocapp, const uint32_t *pick, uint32_t mine) {
+    uint64_t *ustate, uint64_t hint, uint32_t *err, const uint64_t *ocapp, const uint32_t *pick, uint32_t mine,
+    uint64_t ucap) {
   // (pick: the device gate's choice between this form and the other one)
   if (pick && (uint32_t)__builtin_amdgcn_readfirstlane((int)*pick) != mine) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   // a bound on the output buffer's size: sum of 9 w + 1 over the pieces
   // (cpk_packed_bound(w) <= 9 w + 1), + 16
-  const uint64_t ocap = kMsg ? *ocapp : 9 * (swo[n] - swo[0]) + n + 16;
+  // and the caller's capacity (cpk_encode_batch_cap): no line or byte at or
+  // past it is stored
+  const uint64_t ocap = min(kMsg ? *ocapp : 9 * (swo[n] - swo[0]) + n + 16, ucap);
   uint64_t *lut = reinterpret_cast<uint64_t *>(smem + kSpoLut);
   uint64_t *msk = reinterpret_cast<uint64_t *>(smem + kSpoMsk);
   uint64_t *scr = reinterpret_cast<uint64_t *>(smem + kSpoScr);
@@ -952,6 +955,9 @@ __global__ __launch_bounds__(kSpThreads, CPK_SP_WPE) void sp_encode_kernel(
     // kSpDefer steps (or all of them, when they fit the ring)
     auto getoff = [&]() {
       const uint64_t excl = sp_lookback(status, t, ct, ep, err, lane);
+      // (a unit whose bytes pass the caller's capacity: reported; its lines
+      // past the capacity are not stored, ArrayOutputStream.java:40-42)
+      if (lane == 0 && excl + ct > ucap) atomicOr(err, kErrCap);
       if (lane == 0) {
         scr[5] = excl;
         if (c == 0) out_off[p] = excl;

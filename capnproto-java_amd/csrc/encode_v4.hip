@@ -515,7 +515,8 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
 __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint32_t *ticket,
-    const uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip) {
+    const uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip,
+    const uint64_t *__restrict__ sizes, uint64_t ocap, uint32_t *err) {
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint64_t *lut = reinterpret_cast<const uint64_t *>(smem + kE4oLut);
@@ -535,6 +536,12 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     if (W == 0) continue;  // no bytes; no loads (it may sit at the end of the input)
     const uint64_t *src = in + w0;
     const uint64_t obase = out_off[seg];
+    // a piece whose bytes would pass the caller's capacity is not written
+    // (ArrayOutputStream.java:40-42 refuses such a write); reported
+    if (obase + sizes[seg] > ocap) {
+      if (lane == 0) atomicOr(err, kErrCap);
+      continue;
+    }
     uint64_t rpos = obase, fl = obase >> 4;
     // the boundaries of every step come from the size pass (bvbuf); past
     // the piece every word is a boundary.  Words: this group of four steps
@@ -647,11 +654,23 @@ __global__ __launch_bounds__(256) void e4_minmax_kernel(const uint64_t *__restri
 #ifndef CPK_GATE_DENSE_PCT
 #define CPK_GATE_DENSE_PCT 90
 #endif
-__global__ void e4_gate_kernel(uint32_t *tickets, uint32_t samples, uint32_t force) {
+// Batches with one piece far larger than the rest (a piece of over one
+// 8192-word unit and at least 1/2048 of the batch's words: e.g. a single
+// message's segments, DefaultAllocator doubling them) take the single pass
+// too: the two passes give a piece one wave, which then runs alone long
+// after the chip has finished the rest (a 4 MiB segment: ~5 ms per write,
+// profiles/r6b_pbb.log), where the single pass splits it into units.  (At
+// 2048 the single pass's cost on mixed sizes, ~2.4x the two passes' per
+// word, equals one wave's time on the piece at ~5,000x less than the chip's
+// rate.)
+__global__ void e4_gate_kernel(uint32_t *tickets, uint32_t samples, uint32_t force, const uint64_t *swo,
+                               uint32_t n) {
   const uint32_t lo = tickets[kTkGate], hi = tickets[kTkGate + 1];
-  const bool like = lo >= 4096u && 2u * lo >= hi;
+  const uint64_t total = swo[n] - swo[0];
+  const bool big = hi > 8192u && (uint64_t)hi * 2048u >= total;
+  const bool like = (lo >= 4096u && 2u * lo >= hi) || big;
   const bool sparse = like && (force ? force == 2u : (uint64_t)tickets[kTkGate + 3] * 100u >= (uint64_t)samples * 85u);
-  const bool dense = like && !sparse && !force &&
+  const bool dense = like && !big && !sparse && !force &&
                      (uint64_t)tickets[kTkGate + 7] * 100u >= (uint64_t)samples * 8u * CPK_GATE_DENSE_PCT;
   const bool sp = like && !dense;
   if (threadIdx.x == 0) {

@@ -70,6 +70,14 @@ class ArrayOutputStream {
     return n;
   }
   size_t position() const { return pos_; }
+  // getWriteBuffer (ArrayOutputStream.java:47-49): the free part of the
+  // backing buffer, filled in place by a caller that then advances past it
+  uint8_t *writeBuffer() { return buf_ + pos_; }
+  size_t remaining() const { return cap_ - pos_; }
+  void advance(size_t n) {
+    if (cap_ - pos_ < n) throw IOException("backing buffer was not large enough");
+    pos_ += n;
+  }
 
  private:
   uint8_t *buf_;
@@ -184,6 +192,17 @@ inline int readMessageBytes(Gpu &gpu, const uint8_t *p, size_t avail, uint64_t l
   }
 }
 
+// A message read into one reusable word buffer, its segments views of it:
+// what Serialize.read hands MessageReader -- slices of one ByteBuffer
+// holding every segment (Serialize.java:164-177) -- without a vector per
+// segment per call.  Reused across reads: its buffers only grow.
+struct MessageView {
+  std::vector<uint64_t> words, info;
+  size_t segmentCount() const { return (size_t)info[2]; }
+  const uint8_t *segment(size_t i) const { return (const uint8_t *)(words.data() + info[4 + i]); }
+  size_t segmentBytes(size_t i) const { return 8 * (size_t)(info[5 + i] - info[4 + i]); }
+};
+
 inline std::vector<std::vector<uint8_t>> segmentsOf(const std::vector<uint64_t> &words,
                                                     const std::vector<uint64_t> &info) {
   std::vector<std::vector<uint8_t>> segs;
@@ -265,6 +284,47 @@ struct SerializePacked {
           "SerializePacked.write");
     out.resize(off[n + 1]);
     return out;
+  }
+
+  // SerializePacked.write into the caller's ArrayOutputStream: the packed
+  // bytes land in its backing buffer in place (getWriteBuffer,
+  // ArrayOutputStream.java:47-49), nothing allocated per call; a message
+  // that does not fit is the reference's IOException (:40-42).  Returns the
+  // bytes written.
+  static size_t write(Gpu &gpu, const std::vector<std::vector<uint8_t>> &segs, ArrayOutputStream &out) {
+    const size_t n = segs.size();
+    thread_local std::vector<uint8_t> table;
+    thread_local std::vector<const void *> pieces;
+    thread_local std::vector<uint64_t> swo, off;
+    const size_t table_ints = (n + 2) & ~size_t(1);
+    table.assign(4 * table_ints, 0);
+    const uint32_t v = (uint32_t)n - 1;
+    std::memcpy(table.data(), &v, 4);
+    pieces.assign(1, table.data());
+    swo.assign(1, 0);
+    swo.push_back(table.size() / 8);
+    for (size_t i = 0; i < n; ++i) {
+      if (segs[i].size() % 8) throw std::invalid_argument("segment not word-aligned");
+      const uint32_t w = (uint32_t)(segs[i].size() / 8);
+      std::memcpy(table.data() + 4 * (i + 1), &w, 4);
+      pieces.push_back(segs[i].empty() ? nullptr : segs[i].data());
+      swo.push_back(swo.back() + w);
+    }
+    off.resize(n + 2);
+    check(cpk_encode_host_gather(gpu.get(), pieces.data(), swo.data(), (uint32_t)n + 1, out.writeBuffer(),
+                                 out.remaining(), off.data()),
+          "SerializePacked.write");
+    out.advance(off[n + 1]);
+    return off[n + 1];
+  }
+
+  // SerializePacked.read into a reusable MessageView (its segments views of
+  // one word buffer, as Serialize.read slices one ByteBuffer).
+  static void read(Gpu &gpu, ArrayInputStream &in, MessageView &msg, uint64_t traversal_limit_words = 8ull << 20) {
+    in.requireData();
+    check(readMessageBytes(gpu, in.data(), in.remaining(), traversal_limit_words, msg.words, msg.info),
+          "SerializePacked.read");
+    in.advance(msg.info[1]);
   }
 
   // Serialize.read (Serialize.java:119-178) over PackedInputStream: the

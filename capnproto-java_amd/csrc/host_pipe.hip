@@ -200,19 +200,25 @@ int small_encode(cpk_ctx ctx, uint64_t np, uint64_t words, Lay lay, void *h_out,
   if (rc) return rc;
   HostSlot &s = p->slot[0];
   uint64_t *desc = s.pin_meta, *off = desc + 2 * np;
+  TrClock tc(ctx);
   lay((uint64_t *)s.pin_in, desc);
+  tc.mark(kTrWIn);
   const uint64_t seq = small_arm(ctx, off + np + 1);
   cpk::SpSmallArgs da = {};
   if (np <= cpk::kSpArgPieces) memcpy(da.d, desc, 16 * np);
   hipLaunchKernelGGL(cpk::sp_small_kernel, dim3(1), dim3(cpk::kSpThreads), cpk::kSpSmallLds, p->sk,
                      (const uint64_t *)s.pin_in, (const uint64_t *)desc, (uint32_t)np, (uint8_t *)s.pin_out, off,
                      ocap, ctx->tickets + cpk::kTkErr, off + np + 1, seq, da);
-  if (hipGetLastError() != hipSuccess || small_wait(ctx, p->sk, off + np + 1, seq)) return CPK_EDEVICE;
+  if (hipGetLastError() != hipSuccess) return CPK_EDEVICE;
+  tc.mark(kTrWLaunch);
+  if (small_wait(ctx, p->sk, off + np + 1, seq)) return CPK_EDEVICE;
+  tc.mark(kTrWWait);
   const uint64_t P = off[np];
   if (P > ocap) return CPK_EDEVICE;
   if (P > h_out_cap) return CPK_ENOMEM;
   memcpy(h_out, s.pin_out, P);
   for (uint64_t j = 0; j <= np; ++j) h_out_off[j] = off_base + off[j];
+  tc.mark(kTrWOut);
   return CPK_OK;
 }
 
@@ -341,6 +347,7 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
   uint8_t *dst = (uint8_t *)h_out;
   uint64_t base = 0;          // output bytes so far
   const size_t K = cs.size();
+  TrClock tc(ctx);
   // one large chunk (e.g. a single big piece): nothing to overlap it with,
   // so its own transfers are pipelined in 16 MiB chunks instead
   const bool one = K == 1 && cs[0].in_len >= 2 * kPipeChunk;
@@ -362,6 +369,7 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
           break;
         }
       }
+      tc.mark(kTrWIn);
       if (hipMemcpyAsync(s.d_meta, s.pin_meta, (nk + 1) * 8ull, hipMemcpyHostToDevice, p->sh) ||
           hipEventRecord(s.eh, p->sh) || hipStreamWaitEvent(p->sk, s.eh, 0) ||
           (k >= 2 && hipStreamWaitEvent(p->sk, s.ed, 0))) {  // (d_out free: chunk k-2's D2H)
@@ -377,6 +385,7 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
         rc = CPK_EDEVICE;
         break;
       }
+      tc.mark(kTrWLaunch);
     }
     if (k >= 1 && k - 1 < K) {  // chunk k-1: offsets, then its D2H
       const HostChunk &c = cs[k - 1];
@@ -386,6 +395,7 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
         rc = CPK_EDEVICE;
         break;
       }
+      tc.mark(kTrWWait);
       const uint64_t *off = s.pin_meta + nk + 1;
       const uint64_t P = off[nk];
       if (P > c.out_cap) {  // (cannot happen: a piece over its hint)
@@ -421,8 +431,10 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
         rc = CPK_EDEVICE;
         break;
       }
+      tc.mark(kTrWWait);
       const uint64_t o0 = h_out_off[c.i0], o1 = h_out_off[c.i1];
       par_copy(dst + o0, s.pin_out, o1 - o0);
+      tc.mark(kTrWOut);
     }
   }
   if (rc) {
@@ -430,7 +442,9 @@ int encode_host_impl(cpk_ctx ctx, CopyIn copy_in, const uint64_t *h_swo, uint32_
     return rc;
   }
   // (a piece over its hint cannot occur: each chunk's hint is its largest piece)
-  return cpk_ctx_take_error(ctx, p->sk);
+  rc = cpk_ctx_take_error(ctx, p->sk);
+  tc.mark(kTrWWait);
+  return rc;
 }
 
 }  // namespace

@@ -56,6 +56,9 @@ constexpr int kTkEnc = 0;              // encoder counters [8]
 constexpr int kTkDec = 8 * kTkStride;  // decoder counters [8]
 constexpr int kTkPlan = 16 * kTkStride;
 constexpr int kTkErr = 17 * kTkStride;
+// bits of the error word (cpk_ctx_take_error): a piece over its size hint, a
+// timed-out cross-workgroup wait, packed bytes past the caller's capacity
+constexpr uint32_t kErrHint = 1u, kErrWait = 4u, kErrCap = 8u;
 constexpr int kTkGate = 17 * kTkStride + 8;  // [0..1] min, max piece words, [2] encoder choice, [3] sampled zero
                                              // words, [6] single pass's form (1: sparse), [7] sampled words' packed
                                              // bytes, [8..10] decoder choice
@@ -253,7 +256,10 @@ __device__ __forceinline__ uint64_t ld_status(uint64_t *p) {
 constexpr int kDecThreads = 256;               // 4 independent waves
 // workgroups per CU the register budget is sized for (= the LDS limit:
 // 72 VGPRs; at 8 the stream form spilled, messages decode +10 %)
-constexpr int kDecWpe = 7;
+#ifndef CPK_DEC_WPE
+#define CPK_DEC_WPE 7
+#endif
+constexpr int kDecWpe = CPK_DEC_WPE;
 // Lane chunks C of 56 bytes (3.5 KiB windows, 7 workgroups per CU by LDS):
 // measured against 40 / 48 / 60 / 64 at 131,072 pieces with the max-map
 // block map, 56 is fastest on configs 2-4 (against 48: 4.29 -> 4.13 ms,
@@ -274,9 +280,32 @@ constexpr int kRound = CPK_DEC_ROUND;  // output words expanded per round
 #define CPK_DEC_BLK 4
 #endif
 constexpr int kBlk = CPK_DEC_BLK;  // output words per expansion block
-// a lane's visited positions: one bit per chunk byte (bit q mod 64 for position q)
-typedef std::conditional<(kDecChunk <= 32), uint32_t, uint64_t>::type VisMask;
+// a lane's visited positions: one bit per chunk byte (bit q mod 64 for
+// position q: the walks index it by the position itself, so it is 64 bits
+// whatever the chunk size)
+typedef uint64_t VisMask;
+static_assert(sizeof(VisMask) == 8, "visited bits are set at position mod 64");
 static_assert(kDecChunk <= 64, "visited mask bits");
+// Lane chunk starts: lane l at kDecChunk * l, plus kDecSkew bytes for the
+// lanes with bit 4 set (16-31, 48-63).  A 56-byte chunk is a 14-dword stride,
+// so lanes l and l + 16 of a half-wave start their walks on the same LDS bank
+// ((a/4) mod 32 for ds_read_u8 / b32); a one-dword skew puts the 32 starts
+// of a half-wave on 32 distinct banks (chunks 15 and 47 grow to 60 bytes,
+// 31 and 63 shrink to 52)
+#ifndef CPK_DEC_SKEW
+#define CPK_DEC_SKEW 0
+#endif
+constexpr uint32_t kDecSkew = CPK_DEC_SKEW;
+static_assert(kDecChunk + kDecSkew <= 64 && kDecSkew < kDecChunk, "visited mask bits");
+__device__ __forceinline__ uint32_t chunk_start(int l) {
+  return kDecChunk * (uint32_t)l + (kDecSkew & (0u - (((uint32_t)l >> 4) & 1u)));
+}
+// the lane whose chunk holds window position r (< kWin)
+__device__ __forceinline__ uint32_t chunk_owner(uint32_t r) {
+  uint32_t o = chunk_div<kDecChunk>(r);
+  if constexpr (kDecSkew != 0) o -= ((o >> 4) & 1u) & (uint32_t)(r - kDecChunk * o < kDecSkew);
+  return o;
+}
 // the visited masks (phases 1-3) and the block map (phase 5) share LDS
 constexpr uint32_t kDecWaveLds = kWinBuf + (4 * (kRound / kBlk) > 64 * sizeof(VisMask)
                                                 ? 4 * (kRound / kBlk)
@@ -300,6 +329,12 @@ constexpr uint32_t kDecChkReach = (kWin + 2064);
 constexpr uint32_t kDecSerMax = CPK_DEC_SER_MAX, kDecSerCool = 32;
 static_assert(kDecChkReach >= kWin + 2050, "a window's last record must fall inside the checked reach");
 constexpr int kWinLinesPerLane = (int)((kWin + 15 + kDecLook + 15) / 16 + 63) / 64;
+// the batch decoder's next window in registers during this one's block map
+// and expansion (CPK_DEC_PF=1; A/B knob)
+#ifndef CPK_DEC_PF
+#define CPK_DEC_PF 0
+#endif
+constexpr bool kDecPf = CPK_DEC_PF != 0;
 constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;  // 21,760 at 56-byte chunks
 
 __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
@@ -417,8 +452,8 @@ template <bool k32 = true>
 __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, int lane, uint32_t e,
                                              uint32_t wend DEC_PH_PARAMS) {
   // ---- 1: speculative chunk walks --------------------------------------
-  const uint32_t cb = e + kDecChunk * lane;
-  const uint32_t ce = min(cb + kDecChunk, wend);
+  const uint32_t cb = e + chunk_start(lane);
+  const uint32_t ce = min(e + chunk_start(lane + 1), wend);
   VisMask vis = 0;
   uint32_t X = cb, wt = 0;  // wt: output words of the walk
   if (cb < wend) {
@@ -441,7 +476,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   if (cb < wend) {
     while (S < wend) {
       const uint32_t r = S - e;
-      const uint32_t ow_ = chunk_div<kDecChunk>(r);
+      const uint32_t ow_ = chunk_owner(r);
       if ((visa[ow_] >> (S & 63u)) & 1) break;  // (bit S mod 64, as above)
       const DecRec rr = rec_at<k32>(pkw, S);
       lw += rr.nw;
@@ -450,7 +485,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   }
   WPH(2)
   // ---- 3: reachability over lanes --------------------------------------
-  int nx = (cb < wend && S < wend) ? (int)chunk_div<kDecChunk>(S - e) : 64;
+  int nx = (cb < wend && S < wend) ? (int)chunk_owner(S - e) : 64;
   uint64_t R = 1ull << lane;
   {
 #pragma unroll
@@ -790,6 +825,8 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
   uint32_t cool = 0;  // windows before the next serial attempt after one gave up
   int tprev = 0;      // the last window's words (a window near the piece's end stays parallel:
                       // in a stream the bytes do not say where the piece ends)
+  uint32_t nser = 0, nback = 0;  // (dense form: windows walked serially / serial walks given back,
+                                 // into ticket[1] / [2] at the end: cpk_ctx_dense_windows)
 
   for (uint32_t sidx = 0;; ++sidx) {
     // every branch below is on wave-uniform (SGPR) values: the compiler
@@ -850,6 +887,11 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
     uint32_t e = 0;  // true tag position (piece-relative)
     int ow = 0;      // output words produced
     if (W == 0) st = (P == 0 || kStream) ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
+    // (kDecPf: the next window's lines, loaded into registers while this
+    // window's block map and expansion run; pf: they are in flight)
+    constexpr bool kPf = kDecPf && !kStream && !kSerial;
+    uint4 pfl[kPf ? kWinLinesPerLane : 1];
+    bool pf = false;
     while (W != 0) {
       // the window's start and the words so far are wave-uniform: say so
       // (the loop's exits made the compiler keep them in VGPRs and run the
@@ -873,10 +915,15 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       // one memory latency per window instead of one per line
       {
         uint4 l[kWinLinesPerLane];
+        if (kPf && pf) {
 #pragma unroll
-        for (int j = 0; j < kWinLinesPerLane; ++j) {
-          const uint32_t L = lane + 64 * j;
-          l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
+          for (int j = 0; j < kWinLinesPerLane; ++j) l[j] = pfl[kPf ? j : 0];
+        } else {
+#pragma unroll
+          for (int j = 0; j < kWinLinesPerLane; ++j) {
+            const uint32_t L = lane + 64 * j;
+            l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
+          }
         }
 #pragma unroll
         for (int j = 0; j < kWinLinesPerLane; ++j) {
@@ -934,12 +981,14 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
             ow += T;
             e = enext;
             tprev = T;
+            nser = (uint32_t)__builtin_amdgcn_readfirstlane((int)nser + 1);  // (scalar registers)
             continue;
           }
           // too many records (dense but tagged words, e.g. one zero byte per
           // word): the parallel path, and no serial walk for a while
           ser = false;
           cool = kDecSerCool;
+          nback = (uint32_t)__builtin_amdgcn_readfirstlane((int)nback + 1);
         }
       }
 
@@ -954,7 +1003,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
           (uint32_t)__builtin_amdgcn_readlane((int)S, 63 - __builtin_clzll(onmask));
       // each on-path lane hands its landing point to its successor
       wave_lds_order();  // (phase 2's reads of visa are done)
-      if (((onmask >> lane) & 1) && S < wend) visa[chunk_div<kDecChunk>(S - e)] = (VisMask)S;
+      if (((onmask >> lane) & 1) && S < wend) visa[chunk_owner(S - e)] = (VisMask)S;
       wave_lds_order();
       const uint32_t entry = lane == 0 ? e : (uint32_t)visa[lane];
       const bool on = (onmask >> lane) & 1;
@@ -976,6 +1025,21 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       const int inc = wave_incl_add(myw);
       const int T = readlane(inc, 63);
       const int o0 = inc - myw;  // window-relative output of this lane's first record
+      if constexpr (kPf) {
+        // the next window (the piece goes on past this one: its start enext
+        // and bytes are known) loaded now, consumed at its start
+        pf = ow + T < W && enext < P;
+        if (pf) {
+          const uint32_t padn = (uint32_t)((a + enext) & 15);
+          const uint32_t nlines = (min(enext + kWin + kDecLook, P) - (enext - padn) + 15) >> 4;
+          const uint4 *nsrc = reinterpret_cast<const uint4 *>(gp - padn + enext);
+#pragma unroll
+          for (int j = 0; j < kWinLinesPerLane; ++j) {
+            const uint32_t L = lane + 64 * j;
+            pfl[j] = L < nlines ? nsrc[L] : make_uint4(0u, 0u, 0u, 0u);
+          }
+        }
+      }
       WPH(4)
       // ---- 5: error checks, block map, expansion ------------------------------
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
@@ -1005,6 +1069,11 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       sfail = st;
       if (seg + 1 == sende) sd.send_out[sj] = scur;
     }
+  }
+  if constexpr (kSerial) {
+    // (wave-uniform counts, one atomic each per wave and launch)
+    if (lane == 0 && nser) atomicAdd(&ticket[1], nser);
+    if (lane == 0 && nback) atomicAdd(&ticket[2], nback);
   }
   WPH_FLUSH(16)
 }
@@ -1465,12 +1534,19 @@ __global__ void msg_interleave_kernel(const uint64_t *__restrict__ mseg, uint32_
 __global__ void msg_table_emit_kernel(const uint64_t *__restrict__ swo,
                                       const uint64_t *__restrict__ mseg, uint32_t nm,
                                       const uint64_t *__restrict__ poff, uint64_t *__restrict__ soff,
-                                      uint8_t *__restrict__ out) {
+                                      uint8_t *__restrict__ out, const uint64_t *__restrict__ tsize,
+                                      uint64_t ocap, uint32_t *err) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= nm) return;
   const uint64_t s0 = mseg[m], s1 = mseg[m + 1];
   const uint64_t *c = poff + s0 + m;
   for (uint64_t s = s0; s < s1; ++s) soff[s] = c[1 + s - s0];
+  // (the caller's output capacity: a table that would pass it is not
+  // written, ArrayOutputStream.java:40-42)
+  if (c[0] + tsize[m] > ocap) {
+    atomicOr(err, kErrCap);
+    return;
+  }
   uint8_t *o = out + c[0];
   const uint32_t count = (uint32_t)(s1 - s0);
   serial_pack(table_words(count), [&](uint32_t k) { return table_word(swo, s0, count, k); },
@@ -1621,9 +1697,33 @@ struct cpk_ctx_s {
   uint64_t *fl_buf;       // cpk_decode_batch of a few large pieces: boundaries found [33] (lazy)
   uint8_t *rm_copy;       // cpk_read_message_host, one-wave path: the packed bytes on the device (lazy)
   uint64_t small_seq;     // the one-launch host paths' completion flag values (small_wait)
-  uint64_t small_fallbacks;  // small_wait calls that fell back to a stream sync (lost flags)
+  uint64_t small_fallbacks;  // small_wait calls whose flag was unset even after a stream sync (lost flags)
+  uint64_t small_timeouts;   // small_wait calls that waited past 5 ms (late launches included)
   uint64_t *sp_units;     // single pass, pieces over one chunk: unit counts | starts | block sums | unit table
   uint64_t sp_units_cap;  //   u64 entries
+  // CPK_HOST_TRACE=1 (read at creation): host wall time of the one-message
+  // host paths (cpk_encode_host[_gather], cpk_read_message_host) by phase,
+  // summed per context and printed to stderr by cpk_ctx_destroy
+  uint64_t rm_mw_max;     // cpk_read_message[_host]: streams under it by one workgroup (<= kRmMwMax)
+  bool trace;
+  double tr_us[8];
+  uint64_t tr_n[8];
+};
+// the phases (write: staging in, enqueues, waits, staging out; read: same)
+enum { kTrWIn, kTrWLaunch, kTrWWait, kTrWOut, kTrRIn, kTrRLaunch, kTrRWait, kTrROut };
+struct TrClock {
+  cpk_ctx c;
+  std::chrono::steady_clock::time_point t;
+  explicit TrClock(cpk_ctx ctx) : c(ctx) {
+    if (c->trace) t = std::chrono::steady_clock::now();
+  }
+  void mark(int k) {
+    if (!c->trace) return;
+    const auto n = std::chrono::steady_clock::now();
+    c->tr_us[k] += std::chrono::duration<double, std::micro>(n - t).count();
+    ++c->tr_n[k];
+    t = n;
+  }
 };
 
 namespace {
@@ -1690,11 +1790,16 @@ static int small_wait(cpk_ctx ctx, hipStream_t s, const uint64_t *flag, uint64_t
     __builtin_ia32_pause();
     if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
   }
-  // counted (cpk_ctx_small_fallbacks): a lost flag would otherwise only cost
-  // 5 ms per call and pass every test
-  ++ctx->small_fallbacks;
+  // A late launch (a busy GPU, queueing behind other streams, the first
+  // module load) also gets here: the stream synchronisation decides.  Only a
+  // flag still unset after it -- a kernel that completed without writing it,
+  // a device-side bug -- is counted (cpk_ctx_small_fallbacks); a lost flag
+  // would otherwise only cost 5 ms per call and pass every test.
+  ++ctx->small_timeouts;
   if (hipStreamSynchronize(s) != hipSuccess) return 1;
-  return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? 0 : 1;
+  if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return 0;
+  ++ctx->small_fallbacks;
+  return 1;
 }
 #include "host_pipe.hip"
 
@@ -1760,6 +1865,11 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     // CPK_DECODER=1 selects the block-map decoder, 2 the record-index one
     const char *d = getenv("CPK_DECODER");
     c->decoder = (d && d[0] == '2') ? 2 : (d && d[0] == '1') ? 1 : 3;
+    const char *t = getenv("CPK_HOST_TRACE");
+    c->trace = t && t[0] == '1';
+    // (CPK_RM_MW_MAX_KB: A/B of the one-workgroup reader's upper bound)
+    const char *m = getenv("CPK_RM_MW_MAX_KB");
+    c->rm_mw_max = m ? (uint64_t)atoll(m) << 10 : 0;
   }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
@@ -1803,6 +1913,14 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
 void cpk_ctx_destroy(cpk_ctx ctx) {
   if (!ctx) return;
   DeviceGuard g(ctx->device);
+  if (ctx->trace) {
+    static const char *nm[8] = {"write staging in", "write enqueue", "write wait", "write staging out",
+                                "read staging in", "read enqueue", "read wait", "read staging out"};
+    for (int k = 0; k < 8; ++k)
+      if (ctx->tr_n[k])
+        fprintf(stderr, "cpk host trace: %-18s %8llu marks %12.1f us total\n", nm[k],
+                (unsigned long long)ctx->tr_n[k], ctx->tr_us[k]);
+  }
   if (ctx->status) hipFree(ctx->status);
   if (ctx->tickets) hipFree(ctx->tickets);
   if (ctx->e4_bv) hipFree(ctx->e4_bv);
@@ -1819,6 +1937,18 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
 
 int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
 uint64_t cpk_ctx_small_fallbacks(cpk_ctx ctx) { return ctx ? ctx->small_fallbacks : 0; }
+int cpk_ctx_dense_windows(cpk_ctx ctx, void *stream, uint64_t *serial, uint64_t *given_back) {
+  if (!ctx || !serial || !given_back) return CPK_EINVAL;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t c[2] = {0, 0};
+  if (hipMemcpyAsync(c, ctx->tickets + cpk::kTkDec + 1, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return CPK_EDEVICE;
+  *serial = c[0];
+  *given_back = c[1];
+  return CPK_OK;
+}
 
 // Single-pass encoder (encode_sp.hip): one launch, the look-back words
 // epoch-tagged (cleared only when the epoch wraps or the array grows).  Work
@@ -1840,7 +1970,7 @@ static bool sp_takes(cpk_ctx ctx, uint32_t n, uint64_t max_seg_words) {
 // chunk (0: every piece is one unit)
 int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64_t *pdesc,
               const uint64_t *tin, uint32_t n, uint64_t hint, void *d_out, uint64_t *d_out_off,
-              hipStream_t s, bool gated = false, uint64_t units = 0) {
+              hipStream_t s, bool gated = false, uint64_t units = 0, uint64_t out_cap = ~0ull) {
   const uint64_t ucap = units ? units : n;  // look-back words (+ as many run-state words)
   bool fresh = false;
   if (2 * ucap > ctx->sp_cap) {
@@ -1894,19 +2024,19 @@ int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64
     hipLaunchKernelGGL(cpk::sp_encode_kernel<true>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
                        ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
-                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr, pick, 0u);
+                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr, pick, 0u, out_cap);
   else
     hipLaunchKernelGGL(cpk::sp_encode_kernel<false>, dim3(grid), dim3(cpk::kSpThreads), cpk::kSpLds, s,
                        (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out, d_out_off,
                        ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate, hint,
-                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr, pick, 0u);
+                       ctx->tickets + cpk::kTkErr, tin ? tin - 1 : (const uint64_t *)nullptr, pick, 0u, out_cap);
   if (gated && !pdesc) {
     unsigned g2 = (unsigned)(cpk_sparse::kSpWpe * ctx->cus);
     if (g2 > ucap) g2 = (unsigned)ucap;
     hipLaunchKernelGGL(cpk_sparse::sp_encode_kernel<false>, dim3(g2), dim3(cpk_sparse::kSpThreads),
                        cpk_sparse::kSpLds, s, (const uint64_t *)d_in, d_swo, pdesc, tin, n, (uint8_t *)d_out,
                        d_out_off, ctx->sp_status, ctx->sp_epoch, ctx->tickets + cpk::kTkPlan, utab, nunits, ustate,
-                       hint, ctx->tickets + cpk::kTkErr, (const uint64_t *)nullptr, pick, 1u);
+                       hint, ctx->tickets + cpk::kTkErr, (const uint64_t *)nullptr, pick, 1u, out_cap);
   }
   return hip_ok(hipGetLastError());
 }
@@ -1955,7 +2085,7 @@ static int e4_rows(cpk_ctx ctx, const uint64_t *d_swo, uint32_t n, uint64_t hint
 // per piece from the hint, or packed by word offset when there is no hint (the
 // batch's word count is then read back, synchronising the stream).
 int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, uint64_t hint,
-              void *d_out, uint64_t *d_out_off, hipStream_t s, bool gate = false) {
+              void *d_out, uint64_t *d_out_off, hipStream_t s, bool gate = false, uint64_t out_cap = ~0ull) {
   const uint32_t nb = (uint32_t)((n + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
   int rc = ensure_status(ctx, (uint64_t)n + nb + 1);
   if (rc) return rc;
@@ -1975,7 +2105,8 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
       return CPK_EDEVICE;
     const unsigned mg = n < 256u * 256u ? (unsigned)((n + 255) / 256) : 256u;
     hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3(mg), dim3(256), 0, s, d_swo, n, mm, (const uint64_t *)d_in);
-    hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets, mg * 256u, (uint32_t)ctx->sp_form);
+    hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets, mg * 256u, (uint32_t)ctx->sp_form,
+                       d_swo, n);
   }
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (n + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (n + cpk::kE4Waves - 1) / cpk::kE4Waves;
@@ -1991,13 +2122,20 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
   hipLaunchKernelGGL(cpk::e4_emit_kernel, dim3(grid), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
                      (const uint64_t *)d_in, d_swo, n, (const uint64_t *)d_out_off,
                      (uint8_t *)d_out, ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv,
-                     stride, gate ? (const uint32_t *)(ctx->tickets + cpk::kTkGate + 2) : (const uint32_t *)nullptr);
+                     stride, gate ? (const uint32_t *)(ctx->tickets + cpk::kTkGate + 2) : (const uint32_t *)nullptr,
+                     (const uint64_t *)sizes, out_cap, ctx->tickets + cpk::kTkErr);
   return hip_ok(hipGetLastError());
 }
 
 int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t nseg,
                         const uint64_t *d_msg_seg_off, uint32_t nm, uint64_t max_seg_words,
                         void *d_out, uint64_t *d_out_off, void *stream) {
+  return cpk_encode_messages_cap(ctx, d_in, d_swo, nseg, d_msg_seg_off, nm, max_seg_words, d_out, ~0ull,
+                                 d_out_off, stream);
+}
+int cpk_encode_messages_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t nseg,
+                            const uint64_t *d_msg_seg_off, uint32_t nm, uint64_t max_seg_words,
+                            void *d_out, uint64_t out_cap, uint64_t *d_out_off, void *stream) {
   if (!ctx || !d_out_off || (nm && !d_msg_seg_off) || (nseg && !d_swo)) return CPK_EINVAL;
   if (((uintptr_t)d_out & 15) || ((uintptr_t)d_in & 7)) return CPK_EINVAL;
   if (max_seg_words == 0) return CPK_EINVAL;  // (a bound is needed for the step rows)
@@ -2028,7 +2166,8 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
     // (tables are at most 257 words: the segments' hint bounds the units)
     const uint64_t ub = sp_unit_bound(np, max_seg_words);
     if (ub > 0xffffffffull) return CPK_EUNSUPPORTED;
-    return sp_launch(ctx, d_in, nullptr, pdesc, tbuf, (uint32_t)np, max_seg_words, d_out, d_out_off, s, false, ub);
+    return sp_launch(ctx, d_in, nullptr, pdesc, tbuf, (uint32_t)np, max_seg_words, d_out, d_out_off, s, false, ub,
+                     out_cap);
   }
   const uint32_t nb = (uint32_t)((np + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
   // scratch: segment sizes | table sizes | message-order sizes | segment offsets | block sums
@@ -2057,22 +2196,30 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, ui
   hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
                      (const uint64_t *)comb, (uint32_t)np, (const uint64_t *)bsum, d_out_off);
   hipLaunchKernelGGL(cpk::msg_table_emit_kernel, dim3(tg), dim3(tb), 0, s, d_swo, d_msg_seg_off, nm,
-                     (const uint64_t *)d_out_off, soff, (uint8_t *)d_out);
+                     (const uint64_t *)d_out_off, soff, (uint8_t *)d_out, (const uint64_t *)tsize, out_cap,
+                     ctx->tickets + cpk::kTkErr);
   if (nseg)
     hipLaunchKernelGGL(cpk::e4_emit_kernel, dim3(grid), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
                        (const uint64_t *)d_in, d_swo, nseg, (const uint64_t *)soff, (uint8_t *)d_out,
-                       ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv, stride, (const uint32_t *)nullptr);
+                       ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv, stride, (const uint32_t *)nullptr,
+                       (const uint64_t *)ssize, out_cap, ctx->tickets + cpk::kTkErr);
   return hip_ok(hipGetLastError());
 }
 
 int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n,
                      uint64_t max_seg_words, void *d_out, uint64_t *d_out_off, void *stream) {
+  return cpk_encode_batch_cap(ctx, d_in, d_swo, n, max_seg_words, d_out, ~0ull, d_out_off, stream);
+}
+int cpk_encode_batch_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n,
+                         uint64_t max_seg_words, void *d_out, uint64_t out_cap, uint64_t *d_out_off,
+                         void *stream) {
   if (!ctx || (!d_swo && n) || !d_out_off) return CPK_EINVAL;
   if (((uintptr_t)d_out & 15) || ((uintptr_t)d_in & 7)) return CPK_EINVAL;
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return hip_ok(hipMemsetAsync(d_out_off, 0, 8, s));
-  if (!sp_takes(ctx, n, max_seg_words)) return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s);
+  if (!sp_takes(ctx, n, max_seg_words))
+    return e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s, false, out_cap);
   if (ctx->encoder == 0) {
     // (forced single pass: pieces of any size, several units for a large one)
     uint64_t hint = max_seg_words;
@@ -2087,14 +2234,15 @@ int cpk_encode_batch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint3
     uint64_t ub = sp_unit_bound(n, hint);
     if (hint > 64ull * cpk::kSpCS && !max_seg_words) ub = n + hint / (64ull * cpk::kSpCS) + 1;
     if (ub > 0xffffffffull) return CPK_EUNSUPPORTED;
-    return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s, false, ub);
+    return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s, false, ub,
+                     out_cap);
   }
   // by piece size: both enqueued, the device picks one (e4_gate_kernel);
   // pieces over one chunk go to the single pass as several units
-  int rc = e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s, true);
+  int rc = e4_encode(ctx, d_in, d_swo, n, max_seg_words, d_out, d_out_off, s, true, out_cap);
   if (rc) return rc;
   return sp_launch(ctx, d_in, d_swo, nullptr, nullptr, n, max_seg_words, d_out, d_out_off, s, true,
-                   sp_unit_bound(n, max_seg_words));
+                   sp_unit_bound(n, max_seg_words), out_cap);
 }
 
 int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
@@ -2106,9 +2254,12 @@ int cpk_ctx_take_error(cpk_ctx ctx, void *stream) {
       hipStreamSynchronize(s) != hipSuccess)
     return CPK_EDEVICE;
   if (e && hipMemsetAsync(ctx->tickets + cpk::kTkErr, 0, 4, s) != hipSuccess) return CPK_EDEVICE;
-  // bit 0: a piece over its size hint; bit 2: a cross-workgroup wait timed
-  // out (cannot happen by design: every wave it waits on is resident)
-  return e ? ((e & 4u) ? CPK_EDEVICE : CPK_EINVAL) : CPK_OK;
+  // kErrHint: a piece over its size hint; kErrWait: a cross-workgroup wait
+  // timed out (cannot happen by design: every wave it waits on is resident);
+  // kErrCap: packed bytes would have passed the caller's output capacity
+  // (nothing was written there: ArrayOutputStream.java:40-42 -> IOException)
+  if (!e) return CPK_OK;
+  return (e & cpk::kErrWait) ? CPK_EDEVICE : (e & cpk::kErrCap) ? CPK_ENOMEM : CPK_EINVAL;
 }
 
 // one launch of the configured decoder (grid: as many workgroups per CU as
@@ -2240,6 +2391,9 @@ constexpr uint64_t kRmSsMin = 64 * 1024;  // cpk_read_message
 // parallel block path 206)
 constexpr uint64_t kRmMwMin = 6 * 1024;
 constexpr uint64_t kRmMwMax = 512 * 1024;
+uint64_t rm_mw_max(cpk_ctx ctx) {
+  return ctx->rm_mw_max && ctx->rm_mw_max < kRmMwMax ? ctx->rm_mw_max : kRmMwMax;
+}
 
 // the bytes a stream of `words` words may take: 10 per word at most
 uint64_t ss_reach(uint64_t avail, uint64_t words) {
@@ -2394,7 +2548,7 @@ static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, 
   // (a lower bar than cpk_decode_stream's: a message's one-wave decode is
   //  ~0.5 GB/s, the parallel path ~250 us of fixed cost: even at 64 KiB)
   const bool one = getenv("CPK_STREAM_ONE_WAVE") != nullptr;
-  if (!one && !dec_v2(ctx) && reach >= kRmMwMin && reach < kRmMwMax) {
+  if (!one && !dec_v2(ctx) && reach >= kRmMwMin && reach < rm_mw_max(ctx)) {
     // (the host path: pinned bytes, copied to the device in the kernel)
     if (info_mirror && !ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmMwMax + 128) != hipSuccess)
       return CPK_ENOMEM;
@@ -2579,12 +2733,14 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   if (rc) return rc;
   HostSlot &sl = p->slot[0];
   uint64_t *info = sl.pin_meta;
-  if (R < kRmMwMax && !getenv("CPK_NO_SMALL")) {
+  TrClock tc(ctx);
+  if (R < rm_mw_max(ctx) && !getenv("CPK_NO_SMALL")) {
     // the one-wave range: the kernels read the packed bytes from the pinned
     // slot and write the words and the info row into pinned memory in place
     // -- no DMA either way, one sync
     memcpy(sl.pin_in, h_packed, R);
     memset((uint8_t *)sl.pin_in + R, 0, 64);
+    tc.mark(kTrRIn);
     const uint64_t seq = small_arm(ctx, info + kRmInfo);
     bool flagged = false;
     rc = read_message_impl(ctx, sl.pin_in, R, traversal_limit_words, sl.pin_out, out_cap_words, nullptr, p->sk,
@@ -2593,7 +2749,9 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
       pipe_drain(p);
       return rc;
     }
+    tc.mark(kTrRLaunch);
     if (flagged ? small_wait(ctx, p->sk, info + kRmInfo, seq) : hipStreamSynchronize(p->sk)) return CPK_EDEVICE;
+    tc.mark(kTrRWait);
     const int st = (int)(int64_t)info[0];
     const uint32_t count = (uint32_t)info[2];
     for (int i = 0; i < 4; ++i) h_info[i] = info[i];
@@ -2601,6 +2759,7 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
     const uint64_t w0 = info[4], words = info[4 + count] - w0;
     for (uint32_t i = 0; i <= count; ++i) h_info[4 + i] = info[4 + i] - w0;
     if (words) memcpy(h_out, (const uint64_t *)sl.pin_out + w0, words * 8);
+    tc.mark(kTrROut);
     return CPK_OK;
   }
   // (the bytes chunk by chunk, DMA under the host copy; then the decoder's
@@ -2609,14 +2768,16 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   if (h2d_pipelined(sl.d_in, sl.pin_in, h_packed, R, p->sk) ||
       hipMemcpyAsync((uint8_t *)sl.d_in + R, (uint8_t *)sl.pin_in + R, 64, hipMemcpyHostToDevice, p->sk))
     return CPK_EDEVICE;
+  tc.mark(kTrRIn);
   rc = cpk_read_message(ctx, sl.d_in, R, traversal_limit_words, sl.d_out, out_cap_words, sl.d_meta, p->sk);
   if (rc) {
     pipe_drain(p);
     return rc;
   }
-  if (hipMemcpyAsync(info, sl.d_meta, kRmInfo * 8ull, hipMemcpyDeviceToHost, p->sk) ||
-      hipStreamSynchronize(p->sk))
-    return CPK_EDEVICE;
+  if (hipMemcpyAsync(info, sl.d_meta, kRmInfo * 8ull, hipMemcpyDeviceToHost, p->sk)) return CPK_EDEVICE;
+  tc.mark(kTrRLaunch);
+  if (hipStreamSynchronize(p->sk)) return CPK_EDEVICE;
+  tc.mark(kTrRWait);
   const int st = (int)(int64_t)info[0];
   const uint32_t count = (uint32_t)info[2];
   h_info[0] = info[0];
@@ -2630,6 +2791,7 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   // (the words chunk by chunk: each chunk's copy-out under the next's DMA)
   if (words && d2h_pipelined(h_out, sl.pin_out, (uint64_t *)sl.d_out + w0, words * 8, p->sk, sl.eh, sl.ed))
     return CPK_EDEVICE;
+  tc.mark(kTrROut);
   return CPK_OK;
 }
 

@@ -82,11 +82,17 @@ uint64_t cpk_batch_packed_capacity(const uint64_t *h_seg_word_off, uint32_t n);
 int cpk_ctx_create(int device, cpk_ctx *out);
 void cpk_ctx_destroy(cpk_ctx ctx);
 int cpk_ctx_device(cpk_ctx ctx);
-/* Times a one-launch host path (small messages) gave up spinning on its
- * kernel's pinned completion flag after 5 ms and fell back to a stream
- * synchronisation since the context was created.  Zero in normal operation:
- * a count that grows means a lost completion flag (a device-side bug). */
+/* Times a one-launch host path (small messages) found its kernel's pinned
+ * completion flag unset even after the stream synchronisation it falls back
+ * to when the flag has not turned within 5 ms (a late launch on a busy GPU
+ * only takes that fallback and is not counted).  Zero in normal operation: a
+ * count that grows means a lost completion flag (a device-side bug). */
 uint64_t cpk_ctx_small_fallbacks(cpk_ctx ctx);
+/* Diagnostics of the last batch / message decode on this context (synchronises
+ * `stream`): windows the dense block-map form walked with one lane along the
+ * true chain, and serial walks it gave back to the parallel walks (too many
+ * records); both 0 when another decoder form took the batch. */
+int cpk_ctx_dense_windows(cpk_ctx ctx, void *stream, uint64_t *serial, uint64_t *given_back);
 
 /* Batch encode of n pieces, device-resident (replaces n calls of
  * PackedOutputStream.write, PackedOutputStream.java:35-205).  Pieces of any
@@ -137,9 +143,27 @@ int cpk_encode_messages(cpk_ctx ctx, const void *d_in, const uint64_t *d_seg_wor
                         uint32_t nseg, const uint64_t *d_msg_seg_off, uint32_t nm,
                         uint64_t max_seg_words, void *d_out, uint64_t *d_out_off, void *stream);
 
-/* Synchronises `stream` and returns CPK_EINVAL if an encode issued since the
- * last call met a piece larger than its max_seg_words bound, else CPK_OK
- * (clears the flag).  The host forms below check it themselves. */
+/* The same two calls with the byte capacity of d_out (the reference's sink
+ * refuses a write that does not fit: ArrayOutputStream.write throws
+ * IOException, ArrayOutputStream.java:36-44).  A piece whose packed bytes
+ * would pass out_cap is reported -- cpk_ctx_take_error returns CPK_ENOMEM --
+ * and no byte at or past d_out + out_cap is ever stored; pieces wholly below
+ * it are written as usual (the bytes of the piece that crosses it are
+ * undefined).  cpk_encode_batch / cpk_encode_messages are these calls with
+ * out_cap = UINT64_MAX: they trust the documented capacity. */
+int cpk_encode_batch_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_seg_word_off,
+                         uint32_t n, uint64_t max_seg_words, void *d_out, uint64_t out_cap,
+                         uint64_t *d_out_off, void *stream);
+int cpk_encode_messages_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_seg_word_off,
+                            uint32_t nseg, const uint64_t *d_msg_seg_off, uint32_t nm,
+                            uint64_t max_seg_words, void *d_out, uint64_t out_cap,
+                            uint64_t *d_out_off, void *stream);
+
+/* Synchronises `stream` and returns the first problem an encode issued since
+ * the last call met (and clears it): CPK_ENOMEM if packed bytes would have
+ * passed an out_cap (the *_cap forms), CPK_EINVAL if a piece was larger than
+ * its max_seg_words bound, else CPK_OK.  The host forms below check it
+ * themselves. */
 int cpk_ctx_take_error(cpk_ctx ctx, void *stream);
 
 /* Batch decode of n pieces, device-resident (replaces n calls of

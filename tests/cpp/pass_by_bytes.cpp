@@ -84,10 +84,16 @@ static bool cpu_read(const std::vector<uint8_t> &buf, size_t len, std::vector<ui
 int main(int argc, char **argv) {
   const size_t max_kib = argc > 1 ? (size_t)atol(argv[1]) : 4096;
   const int iters = argc > 2 ? atoi(argv[2]) : 50;
-  capnp_amd::Gpu gpu(0);
   std::printf("# passByBytes (TestCase.java:80-123): per iteration 2 x SerializePacked.write + 2 x read\n");
-  std::printf("# msg_bytes  segs  packed_bytes  gpu_packed_us  packed_cpu_us  gpu/cpu\n");
+  std::printf("# gpu_alloc: the facade returning fresh vectors (packed bytes, then copied into the\n"
+              "#   request buffer; one vector per segment read back); gpu_owned: packed in place into the\n"
+              "#   caller's ArrayOutputStream, segments read as views of one reused buffer\n"
+              "#   (MessageView), split into its write and read calls; cpu: the C codec (one thread)\n");
+  std::printf("# msg_bytes  segs  packed_bytes  gpu_alloc_us  gpu_owned_us  (write_us  read_us)  packed_cpu_us"
+              "  alloc/cpu  owned/cpu\n");
   for (size_t kib = 1; kib <= max_kib; kib *= 2) {
+    // (a context per size: with CPK_HOST_TRACE=1 each prints its phases on destruction)
+    capnp_amd::Gpu gpu(0);
     const size_t bytes = kib * 1024;
     const Segs req = make_message(bytes, 7 + (uint32_t)kib), resp = make_message(bytes, 99 + (uint32_t)kib);
     const size_t cap = cpko_packed_bound(bytes / 8 + 520) + 64;
@@ -119,6 +125,39 @@ int main(int argc, char **argv) {
         if (back.size() != m->size()) std::abort();
       }
     };
+    capnp_amd::MessageView view;
+    double t_w = 0, t_r = 0;
+    auto owned_iter = [&]() {
+      for (const Segs *m : {&req, &resp}) {
+        std::vector<uint8_t> &buf = m == &req ? reqbuf : respbuf;
+        capnp_amd::ArrayOutputStream w(buf.data(), buf.size());
+        const double a = now();
+        capnp_amd::SerializePacked::write(gpu, *m, w);
+        const double b = now();
+        capnp_amd::ArrayInputStream in(buf.data(), w.position());
+        capnp_amd::SerializePacked::read(gpu, in, view);
+        t_w += b - a;
+        t_r += now() - b;
+        if (view.segmentCount() != m->size()) std::abort();
+      }
+    };
+    // (parity of the in-place forms once: the C codec's bytes, the segments back)
+    {
+      capnp_amd::ArrayOutputStream w(reqbuf.data(), reqbuf.size());
+      const size_t k = capnp_amd::SerializePacked::write(gpu, req, w);
+      std::vector<uint8_t> ref(reqbuf.size());
+      if (k != plen || cpu_write(req, ref) != plen || std::memcmp(ref.data(), reqbuf.data(), plen) != 0) {
+        std::printf("MISMATCH owned write %zu\n", bytes);
+        return 1;
+      }
+      capnp_amd::ArrayInputStream in(reqbuf.data(), k);
+      capnp_amd::SerializePacked::read(gpu, in, view);
+      for (size_t i = 0; i < req.size(); ++i)
+        if (view.segmentBytes(i) != req[i].size() || std::memcmp(view.segment(i), req[i].data(), req[i].size())) {
+          std::printf("MISMATCH owned read %zu\n", bytes);
+          return 1;
+        }
+    }
     auto cpu_iter = [&]() {
       for (const Segs *m : {&req, &resp}) {
         std::vector<uint8_t> &buf = m == &req ? reqbuf : respbuf;
@@ -127,15 +166,21 @@ int main(int argc, char **argv) {
       }
     };
     gpu_iter();
+    owned_iter();
     cpu_iter();
+    t_w = t_r = 0;
     const int it = std::max(3, (int)(iters * 64 / std::max<size_t>(kib, 64)));
     double t0 = now();
     for (int i = 0; i < it; ++i) gpu_iter();
     const double tg = (now() - t0) / it;
     t0 = now();
+    for (int i = 0; i < it; ++i) owned_iter();
+    const double to = (now() - t0) / it;
+    t0 = now();
     for (int i = 0; i < it; ++i) cpu_iter();
     const double tc = (now() - t0) / it;
-    std::printf("%10zu  %4zu  %12zu  %13.1f  %13.1f  %7.2f\n", bytes, req.size(), plen, tg * 1e6, tc * 1e6, tg / tc);
+    std::printf("%10zu  %4zu  %12zu  %12.1f  %12.1f  (%8.1f  %7.1f)  %13.1f  %9.2f  %9.2f\n", bytes, req.size(), plen,
+                tg * 1e6, to * 1e6, t_w / it * 1e6, t_r / it * 1e6, tc * 1e6, tg / tc, to / tc);
     std::fflush(stdout);
   }
   return 0;

@@ -834,6 +834,16 @@ def test_dense_batches_serial_windows(ctx, oracle, kind):
     torch.cuda.synchronize()
     assert (d_st.cpu().numpy() == 0).all()
     assert d_out.cpu().numpy()[: int(swo[-1])].view(np.uint8).tobytes() == data.tobytes()
+    # the serial walk really ran (and, on tagged words, gave windows back):
+    # a change to its heuristics must not quietly turn it off
+    if not ctx.decoder_forced:
+        ser, back = ctx.dense_windows()
+        if kind == "runs":
+            assert ser > 0, (ser, back)
+        elif kind == "tagged":
+            assert back > 0, (ser, back)
+        else:
+            assert ser + back > 0, (ser, back)
     # corrupted dense pieces (a flipped byte mid-piece, cuts, a trailing
     # byte): statuses are the oracle's, whichever walk saw the window
     cases = []

@@ -190,7 +190,8 @@ def test_small_host_paths_back_to_back(ctx, oracle):
         assert st == 0 and got == segs and used == len(pk), k
         packed, _ = ctx.encode_messages_host([segs])
         assert bytes(packed) == pk, k
-    # every call saw its kernel's completion flag (no 5 ms stream-sync fallback)
+    # no call lost its kernel's completion flag (a late launch may take the
+    # 5 ms stream-sync fallback on a busy box; that is not counted)
     assert ctx.small_fallbacks() == f0
 
 
