@@ -196,7 +196,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
   uint32_t fin = 0;
   const bool ok = win_emit<true>(pkw, lut, blk, lane, ein, ow, W, P, T, on, entry, S, onmask, o0, myw, enext,
                                  lend, gp, (uint32_t)(((a + P + 15) & ~15ull) - a), ph, dst, st,
-                                 fin, false DEC_PH_ARGS);
+                                 fin, false, ~0u, 0 DEC_PH_ARGS);
   if (!ok) end_piece(st, 0);
   else if (fills && fin) end_piece(CPK_OK, fin);
   else if (chk && lane == 0) mw_put(&ms.O[nslot], t + 1, (uint32_t)(ow + T));

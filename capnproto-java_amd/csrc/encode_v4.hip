@@ -229,13 +229,15 @@ __device__ __forceinline__ uint32_t e4_next_piece(uint32_t *ticket, int &xq, int
 __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     uint64_t *__restrict__ sizes, uint32_t *ticket, uint64_t hint, uint32_t *err,
-    uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip) {
+    uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip, const uint32_t *order) {
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;  // (the single pass took the batch)
   const int lane = lane_id();
   int xq = xcc_id(), dry = 0;
   for (;;) {
-    const uint32_t seg = e4_next_piece(ticket, xq, dry, n);
-    if (seg >= n) break;
+    const uint32_t tk = e4_next_piece(ticket, xq, dry, n);
+    if (tk >= n) break;
+    // (order: the pieces largest first)
+    const uint32_t seg = order ? (uint32_t)__builtin_amdgcn_readfirstlane((int)order[tk]) : tk;
     const uint64_t w0 = swo[seg];
     const uint64_t W = swo[seg + 1] - w0;
     if (((hint && W > hint) || W >= (1ull << 31)) && lane == 0) atomicOr(err, 1u);
@@ -516,7 +518,7 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint32_t *ticket,
     const uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip,
-    const uint64_t *__restrict__ sizes, uint64_t ocap, uint32_t *err) {
+    const uint64_t *__restrict__ sizes, uint64_t ocap, uint32_t *err, const uint32_t *order) {
   if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint64_t *lut = reinterpret_cast<const uint64_t *>(smem + kE4oLut);
@@ -529,8 +531,9 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
   __syncthreads();
   int xq = xcc_id(), dry = 0;
   for (;;) {
-    const uint32_t seg = e4_next_piece(ticket, xq, dry, n);
-    if (seg >= n) break;
+    const uint32_t tk = e4_next_piece(ticket, xq, dry, n);
+    if (tk >= n) break;
+    const uint32_t seg = order ? (uint32_t)__builtin_amdgcn_readfirstlane((int)order[tk]) : tk;
     const uint64_t w0 = swo[seg];
     const uint64_t W = swo[seg + 1] - w0;
     if (W == 0) continue;  // no bytes; no loads (it may sit at the end of the input)

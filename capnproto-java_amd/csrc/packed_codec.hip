@@ -297,6 +297,10 @@ static_assert(kDecChunk <= 64, "visited mask bits");
 #endif
 constexpr uint32_t kDecSkew = CPK_DEC_SKEW;
 static_assert(kDecChunk + kDecSkew <= 64 && kDecSkew < kDecChunk, "visited mask bits");
+// the chunk walk as two walks per lane (CPK_DEC_2W=1; A/B knob)
+#ifndef CPK_DEC_2W
+#define CPK_DEC_2W 0
+#endif
 __device__ __forceinline__ uint32_t chunk_start(int l) {
   return kDecChunk * (uint32_t)l + (kDecSkew & (0u - (((uint32_t)l >> 4) & 1u)));
 }
@@ -335,7 +339,18 @@ constexpr int kWinLinesPerLane = (int)((kWin + 15 + kDecLook + 15) / 16 + 63) / 
 #define CPK_DEC_PF 0
 #endif
 constexpr bool kDecPf = CPK_DEC_PF != 0;
-constexpr uint32_t kDecLds = 2048 + 4 * kDecWaveLds;  // 21,760 at 56-byte chunks
+// LUT | 4 waves' windows and block maps | 4 waves' dense-form counters
+constexpr uint32_t kDecCntOff = 2048 + 4 * kDecWaveLds;
+// The dense form's window counters (cpk_ctx_dense_windows): compiled into
+// the diagnostics build only (libcapnp_packed_hip_diag.so, build_native.py).
+// Any code in the serial path changes the dense forms' register allocation
+// (spills): with the counters, config-3 message decode +2 % (round 6,
+// profiles/r6f_*).
+#ifndef CPK_DEC_CNT
+#define CPK_DEC_CNT 0
+#endif
+constexpr bool kDecCnt = CPK_DEC_CNT != 0;
+constexpr uint32_t kDecLds = kDecCntOff + 32;  // 22,624 at 56-byte chunks
 
 __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
 #pragma unroll
@@ -447,6 +462,7 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
 struct WinWalk {
   uint32_t cb, S, wt, lw;
   uint64_t R;
+  uint32_t pm, wm;  // (two walks: where A landed on B's chain, A's words before it; ~0u: none)
 };
 template <bool k32 = true>
 __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, int lane, uint32_t e,
@@ -456,6 +472,68 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   const uint32_t ce = min(e + chunk_start(lane + 1), wend);
   VisMask vis = 0;
   uint32_t X = cb, wt = 0;  // wt: output words of the walk
+  uint32_t pm = ~0u, wm = 0;
+#if CPK_DEC_2W
+  if (cb < wend) {
+    // Two dependent walks per lane, so that each lane has two LDS round trips
+    // in flight: A from cb over the chunk's first half, B from its middle cm
+    // over the second, in lockstep.  Then A walks on until it lands on a
+    // position B visited -- from there the two coincide (the chain is a
+    // function of the position) -- or leaves the chunk, while B' walks B
+    // again from cm over the positions before A's (B's words before the
+    // landing point).  The result (visited positions, exit, words) is the
+    // single walk's from cb exactly: A's positions before the landing point,
+    // B's from it on.
+    const uint32_t cm = min(cb + kDecChunk / 2, ce);
+    uint32_t pa = cb, pb = cm, wb = 0;
+    VisMask vb = 0;
+    while (pa < cm || pb < ce) {
+      const bool ga = pa < cm, gb = pb < ce;
+      // (both records' bytes read before either is used; an idle chain reads
+      // at cb, always loaded)
+      const DecRec ra = rec_at<k32>(pkw, ga ? pa : cb);
+      const DecRec rb = rec_at<k32>(pkw, gb ? pb : cb);
+      if (ga) {
+        vis |= (VisMask)1 << (pa & 63u);
+        wt += ra.nw;
+        pa += ra.len;
+      }
+      if (gb) {
+        vb |= (VisMask)1 << (pb & 63u);
+        wb += rb.nw;
+        pb += rb.len;
+      }
+    }
+    uint32_t pb2 = cm, wb2 = 0;
+    for (;;) {
+      const bool la = pa < ce && !((vb >> (pa & 63u)) & 1);  // A walks on
+      const bool lb = pb2 < pa && pa < ce;                    // B' catches up (p >= pa)
+      if (!la && !lb) break;
+      const DecRec ra = rec_at<k32>(pkw, la ? pa : cb);
+      const DecRec rb = rec_at<k32>(pkw, lb ? pb2 : cb);
+      if (la) {
+        vis |= (VisMask)1 << (pa & 63u);
+        wt += ra.nw;
+        pa += ra.len;
+      }
+      if (lb) {
+        wb2 += rb.nw;
+        pb2 += rb.len;
+      }
+    }
+    if (pa < ce) {
+      // landed at p = pa: B's positions [p, ce) (bits p mod 64 on, rotated)
+      const uint32_t L = ce - pa;  // 1..kDecChunk + kDecSkew < 64
+      vis |= __builtin_rotateleft64((1ull << L) - 1, pa & 63u) & vb;
+      pm = pa;
+      wm = wt;
+      wt += wb - wb2;
+      X = pb;
+    } else {
+      X = pa;
+    }
+  }
+#else
   if (cb < wend) {
     uint32_t pos = cb;
     while (pos < ce) {
@@ -469,6 +547,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
     }
     X = pos;
   }
+#endif
   visa[lane] = vis;
   wave_lds_order();
   // ---- 2: walk on until landing on a visited position -------------------
@@ -506,6 +585,8 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   ww.wt = wt;
   ww.lw = lw;
   ww.R = R;
+  ww.pm = pm;
+  ww.wm = wm;
   return ww;
 }
 
@@ -521,7 +602,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
                                          uint32_t entry, uint32_t S, uint64_t onmask, int o0, int myw,
                                          uint32_t enext, uint32_t lend, const uint8_t *gp, uint32_t glim,
                                          uint32_t ph, uint64_t *dst, int &st, uint32_t &fin,
-                                         bool premapped DEC_PH_PARAMS) {
+                                         bool premapped, uint32_t pm, int omid DEC_PH_PARAMS) {
   bool failed = false;
   fin = 0;
   // errors and the filling record can only occur in a window reaching the
@@ -544,6 +625,35 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         // round 0 (usually the window's only one): every record's output
         // is at or past the round's start, so it always marks a block
         if (on) {
+#if CPK_DEC_2W >= 2
+          // two walks: [entry, pm) and [pm, S) (pm: where the chunk walk's
+          // first half landed on its second's chain, omid its output), in
+          // lockstep -- two LDS round trips in flight per lane
+          const bool split = pm != ~0u && entry < pm;
+          const uint32_t e1 = split ? pm : S;
+          uint32_t q1 = entry, q2 = split ? pm : S;
+          uint32_t r1 = (uint32_t)o0, r2 = (uint32_t)omid;
+          constexpr uint32_t kLast = (uint32_t)(kRound - kBlk);
+          for (;;) {
+            const bool g1 = q1 < e1 && r1 <= kLast, g2 = q2 < S && r2 <= kLast;
+            if (!g1 && !g2) break;
+            uint32_t t1, a1, b1, t2, a2, b2;
+            rec_bytes<!kStream>(pkw, g1 ? q1 : e, t1, a1, b1);
+            rec_bytes<!kStream>(pkw, g2 ? q2 : e, t2, a2, b2);
+            if (g1) {
+              const uint32_t zm = 0u - (uint32_t)(t1 == 0), fm = 0u - (uint32_t)(t1 == 0xffu);
+              atomicMax(&blk[(r1 + kBlk - 1) / kBlk], ((r1 + 256u) << 12) | (q1 - e));
+              r1 += 1u + (zm & a1) + (fm & b1);
+              q1 += 1 + __builtin_popcount(t1) + (zm & 1u) + (fm & (8u * b1 + 1u));
+            }
+            if (g2) {
+              const uint32_t zm = 0u - (uint32_t)(t2 == 0), fm = 0u - (uint32_t)(t2 == 0xffu);
+              atomicMax(&blk[(r2 + kBlk - 1) / kBlk], ((r2 + 256u) << 12) | (q2 - e));
+              r2 += 1u + (zm & a2) + (fm & b2);
+              q2 += 1 + __builtin_popcount(t2) + (zm & 1u) + (fm & (8u * b2 + 1u));
+            }
+          }
+#else
           uint32_t ro = (uint32_t)o0;
           for (uint32_t q = entry; q < S && ro <= (uint32_t)(kRound - kBlk);) {
             uint32_t tag, c1, c9;
@@ -553,6 +663,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
             ro += 1u + (zm & c1) + (fm & c9);
             q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
           }
+#endif
         }
       } else
       if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
@@ -811,6 +922,8 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
   VisMask *visa = reinterpret_cast<VisMask *>(blk);  // [64], over the block map
   if (sd.skip && __builtin_amdgcn_readfirstlane(*sd.skip)) return;
   fill_luts(lut, true);
+  if (kSerial && kDecCnt && threadIdx.x == 0)  // (the dense form's counters, below)
+    reinterpret_cast<uint64_t *>(smem + kDecCntOff)[0] = 0ull;
   __syncthreads();  // the only block-wide barrier: LUT ready
   // (one stream: its one ticket is item 0 of counter 0 -- start there, and
   // a wave that does not get it leaves at once instead of trying the other
@@ -825,8 +938,11 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
   uint32_t cool = 0;  // windows before the next serial attempt after one gave up
   int tprev = 0;      // the last window's words (a window near the piece's end stays parallel:
                       // in a stream the bytes do not say where the piece ends)
-  uint32_t nser = 0, nback = 0;  // (dense form: windows walked serially / serial walks given back,
-                                 // into ticket[1] / [2] at the end: cpk_ctx_dense_windows)
+  // (dense form: windows walked serially / serial walks given back, counted
+  // per workgroup at a fixed LDS address -- anything live across the window
+  // loop costs the dense forms spills -- and added to ticket[1] / [2] at the
+  // end: cpk_ctx_dense_windows)
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + kDecCntOff);
 
   for (uint32_t sidx = 0;; ++sidx) {
     // every branch below is on wave-uniform (SGPR) values: the compiler
@@ -976,19 +1092,19 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
             const uint32_t enext = (uint32_t)readlane((int)q, 0);
             uint32_t fin = 0;
             const bool failed = !win_emit<kStream, kDecLean>(pkw, lut, blk, lane, e, ow, W, P, T, false, e, e, 0ull, 0,
-                                                   0, enext, lend, gp, glim, ph, dst, st, fin, true DEC_PH_ARGS);
+                                                   0, enext, lend, gp, glim, ph, dst, st, fin, true, ~0u, 0 DEC_PH_ARGS);
             if (failed) break;  // (cannot happen: no record here is checked)
             ow += T;
             e = enext;
             tprev = T;
-            nser = (uint32_t)__builtin_amdgcn_readfirstlane((int)nser + 1);  // (scalar registers)
+            if (kDecCnt && lane == 0) atomicAdd(&cnt[0], 1u);
             continue;
           }
           // too many records (dense but tagged words, e.g. one zero byte per
           // word): the parallel path, and no serial walk for a while
           ser = false;
           cool = kDecSerCool;
-          nback = (uint32_t)__builtin_amdgcn_readfirstlane((int)nback + 1);
+          if (kDecCnt && lane == 0) atomicAdd(&cnt[1], 1u);
         }
       }
 
@@ -1013,8 +1129,8 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       // visited) plus the landing walk: the walk's words minus those before
       // entry (usually one or two records of a false start)
       int myw = 0;
+      uint32_t pre = 0;
       if (on) {
-        uint32_t pre = 0;
         for (uint32_t q = cb; q < entry;) {
           const DecRec r = rec_at<!kStream>(pkw, q);
           pre += r.nw;
@@ -1025,6 +1141,8 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       const int inc = wave_incl_add(myw);
       const int T = readlane(inc, 63);
       const int o0 = inc - myw;  // window-relative output of this lane's first record
+      // (two-walk map: the output of the chunk walk's landing point pm)
+      const int omid = o0 + (int)(ww.wm - pre);
       if constexpr (kPf) {
         // the next window (the piece goes on past this one: its start enext
         // and bytes are known) loaded now, consumed at its start
@@ -1044,7 +1162,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       // ---- 5: error checks, block map, expansion ------------------------------
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
       const bool failed = !win_emit<kStream, kDecLean>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
-                                             enext, lend, gp, glim, ph, dst, st, fin, false DEC_PH_ARGS);
+                                             enext, lend, gp, glim, ph, dst, st, fin, false, ww.pm, omid DEC_PH_ARGS);
       if (failed) break;
       if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
         ow = W;
@@ -1070,10 +1188,14 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       if (seg + 1 == sende) sd.send_out[sj] = scur;
     }
   }
-  if constexpr (kSerial) {
-    // (wave-uniform counts, one atomic each per wave and launch)
-    if (lane == 0 && nser) atomicAdd(&ticket[1], nser);
-    if (lane == 0 && nback) atomicAdd(&ticket[2], nback);
+  if constexpr (kSerial && kDecCnt) {
+    // (each wave hands on what the workgroup has counted so far, its own
+    // counts included: every count is taken by its own wave's exchange)
+    if (lane == 0) {
+      const uint32_t a = atomicExch(&cnt[0], 0u), b = atomicExch(&cnt[1], 0u);
+      if (a) atomicAdd(&ticket[1], a);
+      if (b) atomicAdd(&ticket[2], b);
+    }
   }
   WPH_FLUSH(16)
 }
@@ -1191,12 +1313,17 @@ constexpr int kOrdClasses = 64;
 __device__ __forceinline__ uint32_t ord_class(uint64_t w) {
   return (uint32_t)(kOrdClasses - 1) - (w ? 64u - (uint32_t)__builtin_clzll(w) : 0u);
 }
-__global__ void ord_hist_kernel(const uint64_t *__restrict__ words, uint32_t n, uint32_t *hist) {
+// (item i's words: words[i], or swo[i + 1] - swo[i] when swo is given)
+__device__ __forceinline__ uint64_t ord_words(const uint64_t *words, const uint64_t *swo, uint32_t i) {
+  return swo ? swo[i + 1] - swo[i] : words[i];
+}
+__global__ void ord_hist_kernel(const uint64_t *__restrict__ words, uint32_t n, uint32_t *hist,
+                                const uint64_t *__restrict__ swo) {
   __shared__ uint32_t h[kOrdClasses];
   if (threadIdx.x < kOrdClasses) h[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) atomicAdd(&h[ord_class(words[i])], 1u);
+  if (i < n) atomicAdd(&h[ord_class(ord_words(words, swo, i))], 1u);
   __syncthreads();
   if (threadIdx.x < kOrdClasses && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
 }
@@ -1212,12 +1339,12 @@ __global__ void ord_scan_kernel(uint32_t *hist) {
 // (a block reserves its range in each class with one global atomic: with a
 // few classes and 256 Ki messages, one atomic per message took 1.5 ms)
 __global__ void ord_scatter_kernel(const uint64_t *__restrict__ words, uint32_t n, uint32_t *cursor,
-                                   uint32_t *__restrict__ order) {
+                                   uint32_t *__restrict__ order, const uint64_t *__restrict__ swo) {
   __shared__ uint32_t cnt[kOrdClasses], base[kOrdClasses];
   if (threadIdx.x < kOrdClasses) cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = i < n ? ord_class(words[i]) : 0u;
+  const uint32_t c = i < n ? ord_class(ord_words(words, swo, i)) : 0u;
   const uint32_t r = i < n ? atomicAdd(&cnt[c], 1u) : 0u;
   __syncthreads();
   if (threadIdx.x < kOrdClasses && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
@@ -1705,6 +1832,7 @@ struct cpk_ctx_s {
   // host paths (cpk_encode_host[_gather], cpk_read_message_host) by phase,
   // summed per context and printed to stderr by cpk_ctx_destroy
   uint64_t rm_mw_max;     // cpk_read_message[_host]: streams under it by one workgroup (<= kRmMwMax)
+  bool e4_order;          // cpk_encode_messages' two passes: segments largest first (CPK_E4_ORDER=0: off)
   bool trace;
   double tr_us[8];
   uint64_t tr_n[8];
@@ -1744,12 +1872,13 @@ struct DeviceGuard {
 
 // order[0..n) = 0..n-1 by size class, largest first (cpk::ord_*); hist:
 // kOrdClasses u32 of scratch
-void ord_launch(const uint64_t *words, uint32_t n, uint32_t *hist, uint32_t *order, hipStream_t s) {
+void ord_launch(const uint64_t *words, uint32_t n, uint32_t *hist, uint32_t *order, hipStream_t s,
+                const uint64_t *swo = nullptr) {
   const unsigned tb = 256, tg = (n + tb - 1) / tb;
   (void)hipMemsetAsync(hist, 0, 4 * cpk::kOrdClasses, s);
-  hipLaunchKernelGGL(cpk::ord_hist_kernel, dim3(tg), dim3(tb), 0, s, words, n, hist);
+  hipLaunchKernelGGL(cpk::ord_hist_kernel, dim3(tg), dim3(tb), 0, s, words, n, hist, swo);
   hipLaunchKernelGGL(cpk::ord_scan_kernel, dim3(1), dim3(64), 0, s, hist);
-  hipLaunchKernelGGL(cpk::ord_scatter_kernel, dim3(tg), dim3(tb), 0, s, words, n, hist, order);
+  hipLaunchKernelGGL(cpk::ord_scatter_kernel, dim3(tg), dim3(tb), 0, s, words, n, hist, order, swo);
 }
 
 int ensure_status(cpk_ctx ctx, uint64_t n) {
@@ -1870,6 +1999,8 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     // (CPK_RM_MW_MAX_KB: A/B of the one-workgroup reader's upper bound)
     const char *m = getenv("CPK_RM_MW_MAX_KB");
     c->rm_mw_max = m ? (uint64_t)atoll(m) << 10 : 0;
+    const char *o = getenv("CPK_E4_ORDER");
+    c->e4_order = !(o && o[0] == '0');
   }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
@@ -1939,6 +2070,7 @@ int cpk_ctx_device(cpk_ctx ctx) { return ctx ? ctx->device : -1; }
 uint64_t cpk_ctx_small_fallbacks(cpk_ctx ctx) { return ctx ? ctx->small_fallbacks : 0; }
 int cpk_ctx_dense_windows(cpk_ctx ctx, void *stream, uint64_t *serial, uint64_t *given_back) {
   if (!ctx || !serial || !given_back) return CPK_EINVAL;
+  if (!cpk::kDecCnt) return CPK_EUNSUPPORTED;  // (counted by the diagnostics build only)
   DeviceGuard g(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   uint32_t c[2] = {0, 0};
@@ -2113,7 +2245,8 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
   hipLaunchKernelGGL(cpk::e4_size_kernel, dim3(grid), dim3(cpk::kE4Threads), 0, s,
                      (const uint64_t *)d_in, d_swo, n, sizes, ctx->tickets + cpk::kTkEnc, hint,
                      ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride,
-                     gate ? (const uint32_t *)(ctx->tickets + cpk::kTkGate + 2) : (const uint32_t *)nullptr);
+                     gate ? (const uint32_t *)(ctx->tickets + cpk::kTkGate + 2) : (const uint32_t *)nullptr,
+                     (const uint32_t *)nullptr);
   hipLaunchKernelGGL(cpk::e4_scan_reduce, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
                      (const uint64_t *)sizes, n, bsum);
   hipLaunchKernelGGL(cpk::e4_scan_top, dim3(1), dim3(cpk::kE4ScanThreads), 0, s, bsum, nb);
@@ -2123,7 +2256,7 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
                      (const uint64_t *)d_in, d_swo, n, (const uint64_t *)d_out_off,
                      (uint8_t *)d_out, ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv,
                      stride, gate ? (const uint32_t *)(ctx->tickets + cpk::kTkGate + 2) : (const uint32_t *)nullptr,
-                     (const uint64_t *)sizes, out_cap, ctx->tickets + cpk::kTkErr);
+                     (const uint64_t *)sizes, out_cap, ctx->tickets + cpk::kTkErr, (const uint32_t *)nullptr);
   return hip_ok(hipGetLastError());
 }
 
@@ -2170,11 +2303,13 @@ int cpk_encode_messages_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo
                      out_cap);
   }
   const uint32_t nb = (uint32_t)((np + cpk::kE4ScanBlock - 1) / cpk::kE4ScanBlock);
-  // scratch: segment sizes | table sizes | message-order sizes | segment offsets | block sums
-  int rc = ensure_status(ctx, (uint64_t)nseg + nm + np + nseg + nb + 1);
+  // scratch: segment sizes | table sizes | message-order sizes | segment offsets | block sums |
+  // the segments largest first (u32) | their class counts (u32)
+  int rc = ensure_status(ctx, (uint64_t)nseg + nm + np + nseg + nb + 1 + nseg / 2 + 1 + cpk::kOrdClasses / 2);
   if (rc) return rc;
   uint64_t *ssize = ctx->status, *tsize = ssize + nseg, *comb = tsize + nm, *soff = comb + np;
   uint64_t *bsum = soff + nseg;
+  uint32_t *sord = reinterpret_cast<uint32_t *>(bsum + nb + 1), *shist = sord + nseg + (nseg & 1);
   uint64_t stride;
   rc = e4_rows(ctx, d_swo, nseg, max_seg_words, s, stride);
   if (rc) return rc;
@@ -2182,10 +2317,18 @@ int cpk_encode_messages_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo
   const unsigned tb = 256, tg = (nm + tb - 1) / tb;
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (nseg + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (nseg + cpk::kE4Waves - 1) / cpk::kE4Waves;
+  // (segments largest first, both passes: a wave takes a whole segment, and a
+  // 256 KiB one taken last kept the rest of the chip idle behind it)
+  const uint32_t *order = nullptr;
+  if (nseg && ctx->e4_order) {
+    ord_launch(nullptr, nseg, shist, sord, s, d_swo);
+    order = sord;
+  }
   if (nseg)
     hipLaunchKernelGGL(cpk::e4_size_kernel, dim3(grid), dim3(cpk::kE4Threads), 0, s,
                        (const uint64_t *)d_in, d_swo, nseg, ssize, ctx->tickets + cpk::kTkEnc,
-                       max_seg_words, ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride, (const uint32_t *)nullptr);
+                       max_seg_words, ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride, (const uint32_t *)nullptr,
+                       order);
   hipLaunchKernelGGL(cpk::msg_table_size_kernel, dim3(tg), dim3(tb), 0, s, d_swo, d_msg_seg_off, nm,
                      tsize);
   hipLaunchKernelGGL(cpk::msg_interleave_kernel, dim3(tg), dim3(tb), 0, s, d_msg_seg_off, nm,
@@ -2202,7 +2345,7 @@ int cpk_encode_messages_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo
     hipLaunchKernelGGL(cpk::e4_emit_kernel, dim3(grid), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
                        (const uint64_t *)d_in, d_swo, nseg, (const uint64_t *)soff, (uint8_t *)d_out,
                        ctx->tickets + cpk::kTkDec, (const uint64_t *)ctx->e4_bv, stride, (const uint32_t *)nullptr,
-                       (const uint64_t *)ssize, out_cap, ctx->tickets + cpk::kTkErr);
+                       (const uint64_t *)ssize, out_cap, ctx->tickets + cpk::kTkErr, order);
   return hip_ok(hipGetLastError());
 }
 
@@ -2391,8 +2534,15 @@ constexpr uint64_t kRmSsMin = 64 * 1024;  // cpk_read_message
 // parallel block path 206)
 constexpr uint64_t kRmMwMin = 6 * 1024;
 constexpr uint64_t kRmMwMax = 512 * 1024;
-uint64_t rm_mw_max(cpk_ctx ctx) {
-  return ctx->rm_mw_max && ctx->rm_mw_max < kRmMwMax ? ctx->rm_mw_max : kRmMwMax;
+// From host memory the workgroup reads the packed bytes straight from pinned
+// memory (PCIe round trips per window) and the block path stages them by
+// DMA: the block path is ahead from 128 KiB there (passByBytes replay, 512
+// KiB messages: 806 us per iteration against 940 at 256 KiB and 1,190 at
+// 512 KiB, profiles/r6c_pass_by_bytes_mw*.txt)
+constexpr uint64_t kRmMwMaxHost = 128 * 1024;
+uint64_t rm_mw_max(cpk_ctx ctx, bool host) {
+  const uint64_t d = host ? kRmMwMaxHost : kRmMwMax;
+  return ctx->rm_mw_max && ctx->rm_mw_max < kRmMwMax ? ctx->rm_mw_max : d;
 }
 
 // the bytes a stream of `words` words may take: 10 per word at most
@@ -2548,7 +2698,7 @@ static int read_message_impl(cpk_ctx ctx, const void *d_packed, uint64_t avail, 
   // (a lower bar than cpk_decode_stream's: a message's one-wave decode is
   //  ~0.5 GB/s, the parallel path ~250 us of fixed cost: even at 64 KiB)
   const bool one = getenv("CPK_STREAM_ONE_WAVE") != nullptr;
-  if (!one && !dec_v2(ctx) && reach >= kRmMwMin && reach < rm_mw_max(ctx)) {
+  if (!one && !dec_v2(ctx) && reach >= kRmMwMin && reach < rm_mw_max(ctx, info_mirror != nullptr)) {
     // (the host path: pinned bytes, copied to the device in the kernel)
     if (info_mirror && !ctx->rm_copy && hipMalloc(&ctx->rm_copy, kRmMwMax + 128) != hipSuccess)
       return CPK_ENOMEM;
@@ -2734,7 +2884,7 @@ int cpk_read_message_host(cpk_ctx ctx, const void *h_packed, uint64_t avail, uin
   HostSlot &sl = p->slot[0];
   uint64_t *info = sl.pin_meta;
   TrClock tc(ctx);
-  if (R < rm_mw_max(ctx) && !getenv("CPK_NO_SMALL")) {
+  if (R < rm_mw_max(ctx, true) && !getenv("CPK_NO_SMALL")) {
     // the one-wave range: the kernels read the packed bytes from the pinned
     // slot and write the words and the info row into pinned memory in place
     // -- no DMA either way, one sync

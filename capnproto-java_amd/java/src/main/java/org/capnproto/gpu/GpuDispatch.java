@@ -50,10 +50,10 @@ public final class GpuDispatch {
         Boolean.getBoolean("org.capnproto.gpu") || "1".equals(System.getenv("CAPNP_GPU"));
 
     /** Messages below these many unpacked bytes take the reference's CPU
-     *  codec (defaults: the write and read crossovers measured in
-     *  INTEGRATION.md, tests/cpp/threshold_probe.cpp). */
-    public static final long DEFAULT_MIN_WRITE_BYTES = 128L << 10;
-    public static final long DEFAULT_MIN_READ_BYTES = 512L << 10;
+     *  codec (defaults: the write and read crossovers of the multi-segment
+     *  passByBytes replay, INTEGRATION.md, tests/cpp/pass_by_bytes.cpp). */
+    public static final long DEFAULT_MIN_WRITE_BYTES = 1L << 20;
+    public static final long DEFAULT_MIN_READ_BYTES = 2L << 20;
     public static final long MIN_WRITE_BYTES =
         threshold("minWriteBytes", "CAPNP_GPU_MIN_WRITE_BYTES", DEFAULT_MIN_WRITE_BYTES);
     public static final long MIN_READ_BYTES =

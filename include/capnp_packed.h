@@ -91,7 +91,9 @@ uint64_t cpk_ctx_small_fallbacks(cpk_ctx ctx);
 /* Diagnostics of the last batch / message decode on this context (synchronises
  * `stream`): windows the dense block-map form walked with one lane along the
  * true chain, and serial walks it gave back to the parallel walks (too many
- * records); both 0 when another decoder form took the batch. */
+ * records); both 0 when another decoder form took the batch.  Counted only by
+ * the diagnostics build (libcapnp_packed_hip_diag.so: the counters cost the
+ * dense forms ~2 %); the product library returns CPK_EUNSUPPORTED. */
 int cpk_ctx_dense_windows(cpk_ctx ctx, void *stream, uint64_t *serial, uint64_t *given_back);
 
 /* Batch encode of n pieces, device-resident (replaces n calls of

@@ -835,9 +835,25 @@ def test_dense_batches_serial_windows(ctx, oracle, kind):
     assert (d_st.cpu().numpy() == 0).all()
     assert d_out.cpu().numpy()[: int(swo[-1])].view(np.uint8).tobytes() == data.tobytes()
     # the serial walk really ran (and, on tagged words, gave windows back):
-    # a change to its heuristics must not quietly turn it off
+    # a change to its heuristics must not quietly turn it off.  Counted by
+    # the diagnostics build (the same sources with -DCPK_DEC_CNT=1; the
+    # counters cost the product's dense forms ~2 %), in a child process
     if not ctx.decoder_forced:
-        ser, back = ctx.dense_windows()
+        import subprocess
+        import sys
+        import tempfile
+        repo = Path(__file__).resolve().parents[1]
+        diag = repo / "capnproto-java_amd" / "lib" / "libcapnp_packed_hip_diag.so"
+        assert diag.exists(), "diagnostics library not built (build_native.build_diag)"
+        with tempfile.TemporaryDirectory() as td:
+            for k, v in (("pk", pk), ("off", off), ("swo", swo), ("data", data)):
+                np.save(Path(td) / f"{k}.npy", v)
+            import os
+            r = subprocess.run([sys.executable, str(repo / "tests" / "_dense_windows_probe.py"), td],
+                               capture_output=True, text=True, timeout=120,
+                               env=dict(os.environ, CPK_LIB=str(diag)))
+        assert r.returncode == 0, r.stdout + r.stderr
+        ser, back = (int(x) for x in r.stdout.split("dense_windows")[1].split())
         if kind == "runs":
             assert ser > 0, (ser, back)
         elif kind == "tagged":

@@ -196,12 +196,20 @@ def test_small_host_paths_back_to_back(ctx, oracle):
 
 
 def test_read_message_mid_size_workgroup_path(ctx, oracle):
-    """Streams of 6-512 KiB take the one-launch workgroup decoder
-    (decode_mw.hip: a piece's windows spread over 16 waves, entries chained
-    between them): clean messages of 1-9 segments (empty ones included) with
-    the next message behind them, cuts anywhere (ETRUNC), byte flips
-    (status, segments and bytes consumed equal the oracle's Serialize.read)
-    and both dense and sparse data."""
+    """Streams of 6-128 KiB from host memory (6-512 KiB device-resident) take
+    the one-launch workgroup decoder (decode_mw.hip: a piece's windows spread
+    over 16 waves, entries chained between them): clean messages of 1-9
+    segments (empty ones included) with the next message behind them, cuts
+    anywhere (ETRUNC), byte flips (status, segments and bytes consumed equal
+    the oracle's Serialize.read) and both dense and sparse data.  Host
+    streams of 128-512 KiB, which now take the block path, are also read
+    through a context whose workgroup bound is 512 KiB (CPK_RM_MW_MAX_KB)."""
+    import capnp_packed as cp
+    os.environ["CPK_RM_MW_MAX_KB"] = "512"
+    try:
+        ctx512 = cp.Context(0)
+    finally:
+        os.environ.pop("CPK_RM_MW_MAX_KB")
     rng = np.random.default_rng(14)
     for cfg_probs in ((.4, .3, .2, .1), (.05, .05, .1, .8), (.9, .05, .03, .02)):
         for sizes in ([3000], [8192 * 4], [0, 5000, 0, 12000], [int(x) for x in rng.integers(0, 6000, size=9)],
@@ -212,6 +220,11 @@ def test_read_message_mid_size_workgroup_path(ctx, oracle):
             _, nxt = _msg(rng, oracle, [7, 0, 3])
             st, got, used = _check(ctx, oracle, pk + nxt)
             assert st == 0 and got == segs and used == len(pk)
+            if len(pk) >= 128 * 1024:
+                st, got, used = _check(ctx512, oracle, pk + nxt)
+                assert st == 0 and got == segs and used == len(pk)
+                for cut in (len(pk) // 2, len(pk) - 1):
+                    assert _check(ctx512, oracle, pk[:cut])[0] == -2, cut
             for cut in sorted(set([1, 8, 9, 17, len(pk) // 3, len(pk) // 2, len(pk) - 1] +
                                   [int(c) for c in rng.integers(1, len(pk), size=12)])):
                 st, _, _ = _check(ctx, oracle, pk[:cut])
