@@ -297,6 +297,14 @@ static_assert(kDecChunk <= 64, "visited mask bits");
 #endif
 constexpr uint32_t kDecSkew = CPK_DEC_SKEW;
 static_assert(kDecChunk + kDecSkew <= 64 && kDecSkew < kDecChunk, "visited mask bits");
+// the expansion's 8-byte reads as two aligned ds_read_b64 (CPK_DEC_R64=1; A/B knob)
+#ifndef CPK_DEC_R64
+#define CPK_DEC_R64 0
+#endif
+// zero-run words' (unused) expansion reads at one address (CPK_DEC_ZB=1; A/B knob)
+#ifndef CPK_DEC_ZB
+#define CPK_DEC_ZB 0
+#endif
 // the chunk walk as two walks per lane (CPK_DEC_2W=1; A/B knob)
 #ifndef CPK_DEC_2W
 #define CPK_DEC_2W 0
@@ -420,8 +428,24 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
     typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
     const uint32_t la = (uint32_t)(uintptr_t)((lds_cu8 *)pkw) + xl;
     sh = la & 3;
+#if CPK_DEC_R64
+    // two aligned 8-byte reads (ds_read_b64: 2 LDS cycles each, banks over
+    // 64 dwords) instead of three dword reads (banks over 32); the second
+    // address opaque, so they are not merged into a ds_read2_b64 (8 cycles)
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) const u32x2 lds_cu2;
+    const uint32_t a8 = la & ~7u;
+    uint32_t a8b = a8 + 8;
+    asm("" : "+v"(a8b));
+    const u32x2 q0 = *(lds_cu2 *)(uintptr_t)a8, q1 = *(lds_cu2 *)(uintptr_t)a8b;
+    const bool h4 = (la & 4) != 0;
+    d0 = h4 ? q0.y : q0.x;
+    d1 = h4 ? q1.x : q0.y;
+    d2 = h4 ? q1.y : q1.x;
+#else
     lds_cu32 *pl = (lds_cu32 *)(uintptr_t)(la & ~3u);
     d0 = pl[0], d1 = pl[1], d2 = pl[2];
+#endif
   } else {
     sh = (xl + ph) & 3;
     const uint32_t *pl = reinterpret_cast<const uint32_t *>(pkw + ((int64_t)xl - sh));  // (signed: xl < sh)
@@ -793,7 +817,13 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         // run (tag word, then the counted words), or a tagged word
         const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
         const int nw = 1 + (int)((zm & c1) + (fm & c9));
+#if CPK_DEC_ZB
+        // (a zero run's words read the window's first bytes: every such lane
+        // of the instruction the same address -- a broadcast, no bank conflict)
+        const uint32_t rp = zm ? e : ((fm && ofs) ? q + 2 + 8u * (uint32_t)ofs : q + 1);
+#else
         const uint32_t rp = (fm && ofs) ? q + 2 + 8u * (uint32_t)ofs : q + 1;
+#endif
         const uint64_t raw = read8<kAllIn, kLean>(pkw, rp, lend, gp, glim, ph, e);
         const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
         const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
