@@ -113,13 +113,13 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
   uint32_t sw = 0, q = ein;
   int o = -1;
   if (live && ein < wend) {
-    j = (int)chunk_owner(ein - g);
+    j = (int)chunk_div<kDecChunk>(ein - g);
     // lane j walks from the entry to the first position some lane visited
     // (the entry itself, usually) or out of the window
     if (lane == j) {
       while (q < wend) {
         const uint32_t r = q - g;
-        const uint32_t oo = chunk_owner(r);
+        const uint32_t oo = chunk_div<kDecChunk>(r);
         if ((visa[oo] >> (q & 63u)) & 1) {  // (win_walks: the bit of q mod 64)
           o = (int)oo;
           break;
@@ -145,7 +145,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
   int myw = 0, T = 0, o0 = 0;
   if (onmask) {
     wave_lds_order();  // (the walks' reads of visa are done)
-    if (on && S < wend) visa[chunk_owner(S - g)] = (VisMask)S;
+    if (on && S < wend) visa[chunk_div<kDecChunk>(S - g)] = (VisMask)S;
     wave_lds_order();
     if (lane != j) entry = (uint32_t)visa[lane];
     if (on) {
@@ -196,7 +196,7 @@ __device__ __forceinline__ bool mw_window(uint8_t *wl, const uint64_t *lut, MwSh
   uint32_t fin = 0;
   const bool ok = win_emit<true>(pkw, lut, blk, lane, ein, ow, W, P, T, on, entry, S, onmask, o0, myw, enext,
                                  lend, gp, (uint32_t)(((a + P + 15) & ~15ull) - a), ph, dst, st,
-                                 fin, false, ~0u, 0 DEC_PH_ARGS);
+                                 fin, false DEC_PH_ARGS);
   if (!ok) end_piece(st, 0);
   else if (fills && fin) end_piece(CPK_OK, fin);
   else if (chk && lane == 0) mw_put(&ms.O[nslot], t + 1, (uint32_t)(ow + T));

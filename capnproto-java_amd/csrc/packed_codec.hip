@@ -286,38 +286,6 @@ constexpr int kBlk = CPK_DEC_BLK;  // output words per expansion block
 typedef uint64_t VisMask;
 static_assert(sizeof(VisMask) == 8, "visited bits are set at position mod 64");
 static_assert(kDecChunk <= 64, "visited mask bits");
-// Lane chunk starts: lane l at kDecChunk * l, plus kDecSkew bytes for the
-// lanes with bit 4 set (16-31, 48-63).  A 56-byte chunk is a 14-dword stride,
-// so lanes l and l + 16 of a half-wave start their walks on the same LDS bank
-// ((a/4) mod 32 for ds_read_u8 / b32); a one-dword skew puts the 32 starts
-// of a half-wave on 32 distinct banks (chunks 15 and 47 grow to 60 bytes,
-// 31 and 63 shrink to 52)
-#ifndef CPK_DEC_SKEW
-#define CPK_DEC_SKEW 0
-#endif
-constexpr uint32_t kDecSkew = CPK_DEC_SKEW;
-static_assert(kDecChunk + kDecSkew <= 64 && kDecSkew < kDecChunk, "visited mask bits");
-// the expansion's 8-byte reads as two aligned ds_read_b64 (CPK_DEC_R64=1; A/B knob)
-#ifndef CPK_DEC_R64
-#define CPK_DEC_R64 0
-#endif
-// zero-run words' (unused) expansion reads at one address (CPK_DEC_ZB=1; A/B knob)
-#ifndef CPK_DEC_ZB
-#define CPK_DEC_ZB 0
-#endif
-// the chunk walk as two walks per lane (CPK_DEC_2W=1; A/B knob)
-#ifndef CPK_DEC_2W
-#define CPK_DEC_2W 0
-#endif
-__device__ __forceinline__ uint32_t chunk_start(int l) {
-  return kDecChunk * (uint32_t)l + (kDecSkew & (0u - (((uint32_t)l >> 4) & 1u)));
-}
-// the lane whose chunk holds window position r (< kWin)
-__device__ __forceinline__ uint32_t chunk_owner(uint32_t r) {
-  uint32_t o = chunk_div<kDecChunk>(r);
-  if constexpr (kDecSkew != 0) o -= ((o >> 4) & 1u) & (uint32_t)(r - kDecChunk * o < kDecSkew);
-  return o;
-}
 // the visited masks (phases 1-3) and the block map (phase 5) share LDS
 constexpr uint32_t kDecWaveLds = kWinBuf + (4 * (kRound / kBlk) > 64 * sizeof(VisMask)
                                                 ? 4 * (kRound / kBlk)
@@ -341,12 +309,6 @@ constexpr uint32_t kDecChkReach = (kWin + 2064);
 constexpr uint32_t kDecSerMax = CPK_DEC_SER_MAX, kDecSerCool = 32;
 static_assert(kDecChkReach >= kWin + 2050, "a window's last record must fall inside the checked reach");
 constexpr int kWinLinesPerLane = (int)((kWin + 15 + kDecLook + 15) / 16 + 63) / 64;
-// the batch decoder's next window in registers during this one's block map
-// and expansion (CPK_DEC_PF=1; A/B knob)
-#ifndef CPK_DEC_PF
-#define CPK_DEC_PF 0
-#endif
-constexpr bool kDecPf = CPK_DEC_PF != 0;
 // LUT | 4 waves' windows and block maps | 4 waves' dense-form counters
 constexpr uint32_t kDecCntOff = 2048 + 4 * kDecWaveLds;
 // The dense form's window counters (cpk_ctx_dense_windows): compiled into
@@ -428,24 +390,8 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
     typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
     const uint32_t la = (uint32_t)(uintptr_t)((lds_cu8 *)pkw) + xl;
     sh = la & 3;
-#if CPK_DEC_R64
-    // two aligned 8-byte reads (ds_read_b64: 2 LDS cycles each, banks over
-    // 64 dwords) instead of three dword reads (banks over 32); the second
-    // address opaque, so they are not merged into a ds_read2_b64 (8 cycles)
-    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-    typedef __attribute__((address_space(3))) const u32x2 lds_cu2;
-    const uint32_t a8 = la & ~7u;
-    uint32_t a8b = a8 + 8;
-    asm("" : "+v"(a8b));
-    const u32x2 q0 = *(lds_cu2 *)(uintptr_t)a8, q1 = *(lds_cu2 *)(uintptr_t)a8b;
-    const bool h4 = (la & 4) != 0;
-    d0 = h4 ? q0.y : q0.x;
-    d1 = h4 ? q1.x : q0.y;
-    d2 = h4 ? q1.y : q1.x;
-#else
     lds_cu32 *pl = (lds_cu32 *)(uintptr_t)(la & ~3u);
     d0 = pl[0], d1 = pl[1], d2 = pl[2];
-#endif
   } else {
     sh = (xl + ph) & 3;
     const uint32_t *pl = reinterpret_cast<const uint32_t *>(pkw + ((int64_t)xl - sh));  // (signed: xl < sh)
@@ -486,78 +432,15 @@ __device__ __forceinline__ uint64_t read8(const uint8_t *pkw, uint32_t x, uint32
 struct WinWalk {
   uint32_t cb, S, wt, lw;
   uint64_t R;
-  uint32_t pm, wm;  // (two walks: where A landed on B's chain, A's words before it; ~0u: none)
 };
 template <bool k32 = true>
 __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, int lane, uint32_t e,
                                              uint32_t wend DEC_PH_PARAMS) {
   // ---- 1: speculative chunk walks --------------------------------------
-  const uint32_t cb = e + chunk_start(lane);
-  const uint32_t ce = min(e + chunk_start(lane + 1), wend);
+  const uint32_t cb = e + kDecChunk * lane;
+  const uint32_t ce = min(cb + kDecChunk, wend);
   VisMask vis = 0;
   uint32_t X = cb, wt = 0;  // wt: output words of the walk
-  uint32_t pm = ~0u, wm = 0;
-#if CPK_DEC_2W
-  if (cb < wend) {
-    // Two dependent walks per lane, so that each lane has two LDS round trips
-    // in flight: A from cb over the chunk's first half, B from its middle cm
-    // over the second, in lockstep.  Then A walks on until it lands on a
-    // position B visited -- from there the two coincide (the chain is a
-    // function of the position) -- or leaves the chunk, while B' walks B
-    // again from cm over the positions before A's (B's words before the
-    // landing point).  The result (visited positions, exit, words) is the
-    // single walk's from cb exactly: A's positions before the landing point,
-    // B's from it on.
-    const uint32_t cm = min(cb + kDecChunk / 2, ce);
-    uint32_t pa = cb, pb = cm, wb = 0;
-    VisMask vb = 0;
-    while (pa < cm || pb < ce) {
-      const bool ga = pa < cm, gb = pb < ce;
-      // (both records' bytes read before either is used; an idle chain reads
-      // at cb, always loaded)
-      const DecRec ra = rec_at<k32>(pkw, ga ? pa : cb);
-      const DecRec rb = rec_at<k32>(pkw, gb ? pb : cb);
-      if (ga) {
-        vis |= (VisMask)1 << (pa & 63u);
-        wt += ra.nw;
-        pa += ra.len;
-      }
-      if (gb) {
-        vb |= (VisMask)1 << (pb & 63u);
-        wb += rb.nw;
-        pb += rb.len;
-      }
-    }
-    uint32_t pb2 = cm, wb2 = 0;
-    for (;;) {
-      const bool la = pa < ce && !((vb >> (pa & 63u)) & 1);  // A walks on
-      const bool lb = pb2 < pa && pa < ce;                    // B' catches up (p >= pa)
-      if (!la && !lb) break;
-      const DecRec ra = rec_at<k32>(pkw, la ? pa : cb);
-      const DecRec rb = rec_at<k32>(pkw, lb ? pb2 : cb);
-      if (la) {
-        vis |= (VisMask)1 << (pa & 63u);
-        wt += ra.nw;
-        pa += ra.len;
-      }
-      if (lb) {
-        wb2 += rb.nw;
-        pb2 += rb.len;
-      }
-    }
-    if (pa < ce) {
-      // landed at p = pa: B's positions [p, ce) (bits p mod 64 on, rotated)
-      const uint32_t L = ce - pa;  // 1..kDecChunk + kDecSkew < 64
-      vis |= __builtin_rotateleft64((1ull << L) - 1, pa & 63u) & vb;
-      pm = pa;
-      wm = wt;
-      wt += wb - wb2;
-      X = pb;
-    } else {
-      X = pa;
-    }
-  }
-#else
   if (cb < wend) {
     uint32_t pos = cb;
     while (pos < ce) {
@@ -571,7 +454,6 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
     }
     X = pos;
   }
-#endif
   visa[lane] = vis;
   wave_lds_order();
   // ---- 2: walk on until landing on a visited position -------------------
@@ -579,7 +461,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   if (cb < wend) {
     while (S < wend) {
       const uint32_t r = S - e;
-      const uint32_t ow_ = chunk_owner(r);
+      const uint32_t ow_ = chunk_div<kDecChunk>(r);
       if ((visa[ow_] >> (S & 63u)) & 1) break;  // (bit S mod 64, as above)
       const DecRec rr = rec_at<k32>(pkw, S);
       lw += rr.nw;
@@ -588,7 +470,7 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   }
   WPH(2)
   // ---- 3: reachability over lanes --------------------------------------
-  int nx = (cb < wend && S < wend) ? (int)chunk_owner(S - e) : 64;
+  int nx = (cb < wend && S < wend) ? (int)chunk_div<kDecChunk>(S - e) : 64;
   uint64_t R = 1ull << lane;
   {
 #pragma unroll
@@ -609,8 +491,6 @@ __device__ __forceinline__ WinWalk win_walks(const uint8_t *pkw, VisMask *visa, 
   ww.wt = wt;
   ww.lw = lw;
   ww.R = R;
-  ww.pm = pm;
-  ww.wm = wm;
   return ww;
 }
 
@@ -626,7 +506,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
                                          uint32_t entry, uint32_t S, uint64_t onmask, int o0, int myw,
                                          uint32_t enext, uint32_t lend, const uint8_t *gp, uint32_t glim,
                                          uint32_t ph, uint64_t *dst, int &st, uint32_t &fin,
-                                         bool premapped, uint32_t pm, int omid DEC_PH_PARAMS) {
+                                         bool premapped DEC_PH_PARAMS) {
   bool failed = false;
   fin = 0;
   // errors and the filling record can only occur in a window reaching the
@@ -649,35 +529,6 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         // round 0 (usually the window's only one): every record's output
         // is at or past the round's start, so it always marks a block
         if (on) {
-#if CPK_DEC_2W >= 2
-          // two walks: [entry, pm) and [pm, S) (pm: where the chunk walk's
-          // first half landed on its second's chain, omid its output), in
-          // lockstep -- two LDS round trips in flight per lane
-          const bool split = pm != ~0u && entry < pm;
-          const uint32_t e1 = split ? pm : S;
-          uint32_t q1 = entry, q2 = split ? pm : S;
-          uint32_t r1 = (uint32_t)o0, r2 = (uint32_t)omid;
-          constexpr uint32_t kLast = (uint32_t)(kRound - kBlk);
-          for (;;) {
-            const bool g1 = q1 < e1 && r1 <= kLast, g2 = q2 < S && r2 <= kLast;
-            if (!g1 && !g2) break;
-            uint32_t t1, a1, b1, t2, a2, b2;
-            rec_bytes<!kStream>(pkw, g1 ? q1 : e, t1, a1, b1);
-            rec_bytes<!kStream>(pkw, g2 ? q2 : e, t2, a2, b2);
-            if (g1) {
-              const uint32_t zm = 0u - (uint32_t)(t1 == 0), fm = 0u - (uint32_t)(t1 == 0xffu);
-              atomicMax(&blk[(r1 + kBlk - 1) / kBlk], ((r1 + 256u) << 12) | (q1 - e));
-              r1 += 1u + (zm & a1) + (fm & b1);
-              q1 += 1 + __builtin_popcount(t1) + (zm & 1u) + (fm & (8u * b1 + 1u));
-            }
-            if (g2) {
-              const uint32_t zm = 0u - (uint32_t)(t2 == 0), fm = 0u - (uint32_t)(t2 == 0xffu);
-              atomicMax(&blk[(r2 + kBlk - 1) / kBlk], ((r2 + 256u) << 12) | (q2 - e));
-              r2 += 1u + (zm & a2) + (fm & b2);
-              q2 += 1 + __builtin_popcount(t2) + (zm & 1u) + (fm & (8u * b2 + 1u));
-            }
-          }
-#else
           uint32_t ro = (uint32_t)o0;
           for (uint32_t q = entry; q < S && ro <= (uint32_t)(kRound - kBlk);) {
             uint32_t tag, c1, c9;
@@ -687,7 +538,6 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
             ro += 1u + (zm & c1) + (fm & c9);
             q += 1 + __builtin_popcount(tag) + (zm & 1u) + (fm & (8u * c9 + 1u));
           }
-#endif
         }
       } else
       if (on && (rb == 0 || (o0 < rb + kRound && o0 + myw > rb))) {
@@ -817,13 +667,7 @@ __device__ __forceinline__ bool win_emit(const uint8_t *pkw, const uint64_t *lut
         // run (tag word, then the counted words), or a tagged word
         const uint32_t zm = 0u - (uint32_t)(tag == 0), fm = 0u - (uint32_t)(tag == 0xffu);
         const int nw = 1 + (int)((zm & c1) + (fm & c9));
-#if CPK_DEC_ZB
-        // (a zero run's words read the window's first bytes: every such lane
-        // of the instruction the same address -- a broadcast, no bank conflict)
-        const uint32_t rp = zm ? e : ((fm && ofs) ? q + 2 + 8u * (uint32_t)ofs : q + 1);
-#else
         const uint32_t rp = (fm && ofs) ? q + 2 + 8u * (uint32_t)ofs : q + 1;
-#endif
         const uint64_t raw = read8<kAllIn, kLean>(pkw, rp, lend, gp, glim, ph, e);
         const uint32_t rl = (uint32_t)raw, rh = (uint32_t)(raw >> 32);
         const uint32_t x0 = __builtin_amdgcn_perm(rh, rl, (uint32_t)sel);
@@ -1033,11 +877,6 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
     uint32_t e = 0;  // true tag position (piece-relative)
     int ow = 0;      // output words produced
     if (W == 0) st = (P == 0 || kStream) ? CPK_OK : CPK_ETRAILING;  // read() of 0 bytes
-    // (kDecPf: the next window's lines, loaded into registers while this
-    // window's block map and expansion run; pf: they are in flight)
-    constexpr bool kPf = kDecPf && !kStream && !kSerial;
-    uint4 pfl[kPf ? kWinLinesPerLane : 1];
-    bool pf = false;
     while (W != 0) {
       // the window's start and the words so far are wave-uniform: say so
       // (the loop's exits made the compiler keep them in VGPRs and run the
@@ -1061,15 +900,10 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       // one memory latency per window instead of one per line
       {
         uint4 l[kWinLinesPerLane];
-        if (kPf && pf) {
 #pragma unroll
-          for (int j = 0; j < kWinLinesPerLane; ++j) l[j] = pfl[kPf ? j : 0];
-        } else {
-#pragma unroll
-          for (int j = 0; j < kWinLinesPerLane; ++j) {
-            const uint32_t L = lane + 64 * j;
-            l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
-          }
+        for (int j = 0; j < kWinLinesPerLane; ++j) {
+          const uint32_t L = lane + 64 * j;
+          l[j] = L < lines ? gsrc[L] : make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
         for (int j = 0; j < kWinLinesPerLane; ++j) {
@@ -1122,7 +956,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
             const uint32_t enext = (uint32_t)readlane((int)q, 0);
             uint32_t fin = 0;
             const bool failed = !win_emit<kStream, kDecLean>(pkw, lut, blk, lane, e, ow, W, P, T, false, e, e, 0ull, 0,
-                                                   0, enext, lend, gp, glim, ph, dst, st, fin, true, ~0u, 0 DEC_PH_ARGS);
+                                                   0, enext, lend, gp, glim, ph, dst, st, fin, true DEC_PH_ARGS);
             if (failed) break;  // (cannot happen: no record here is checked)
             ow += T;
             e = enext;
@@ -1149,7 +983,7 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
           (uint32_t)__builtin_amdgcn_readlane((int)S, 63 - __builtin_clzll(onmask));
       // each on-path lane hands its landing point to its successor
       wave_lds_order();  // (phase 2's reads of visa are done)
-      if (((onmask >> lane) & 1) && S < wend) visa[chunk_owner(S - e)] = (VisMask)S;
+      if (((onmask >> lane) & 1) && S < wend) visa[chunk_div<kDecChunk>(S - e)] = (VisMask)S;
       wave_lds_order();
       const uint32_t entry = lane == 0 ? e : (uint32_t)visa[lane];
       const bool on = (onmask >> lane) & 1;
@@ -1159,8 +993,8 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       // visited) plus the landing walk: the walk's words minus those before
       // entry (usually one or two records of a false start)
       int myw = 0;
-      uint32_t pre = 0;
       if (on) {
+        uint32_t pre = 0;
         for (uint32_t q = cb; q < entry;) {
           const DecRec r = rec_at<!kStream>(pkw, q);
           pre += r.nw;
@@ -1171,28 +1005,11 @@ __device__ __forceinline__ void decode_body(uint8_t *smem, const uint8_t *__rest
       const int inc = wave_incl_add(myw);
       const int T = readlane(inc, 63);
       const int o0 = inc - myw;  // window-relative output of this lane's first record
-      // (two-walk map: the output of the chunk walk's landing point pm)
-      const int omid = o0 + (int)(ww.wm - pre);
-      if constexpr (kPf) {
-        // the next window (the piece goes on past this one: its start enext
-        // and bytes are known) loaded now, consumed at its start
-        pf = ow + T < W && enext < P;
-        if (pf) {
-          const uint32_t padn = (uint32_t)((a + enext) & 15);
-          const uint32_t nlines = (min(enext + kWin + kDecLook, P) - (enext - padn) + 15) >> 4;
-          const uint4 *nsrc = reinterpret_cast<const uint4 *>(gp - padn + enext);
-#pragma unroll
-          for (int j = 0; j < kWinLinesPerLane; ++j) {
-            const uint32_t L = lane + 64 * j;
-            pfl[j] = L < nlines ? nsrc[L] : make_uint4(0u, 0u, 0u, 0u);
-          }
-        }
-      }
       WPH(4)
       // ---- 5: error checks, block map, expansion ------------------------------
       uint32_t fin = 0;  // end of the record that fills the piece (if any)
       const bool failed = !win_emit<kStream, kDecLean>(pkw, lut, blk, lane, e, ow, W, P, T, on, entry, S, onmask, o0, myw,
-                                             enext, lend, gp, glim, ph, dst, st, fin, false, ww.pm, omid DEC_PH_ARGS);
+                                             enext, lend, gp, glim, ph, dst, st, fin, false DEC_PH_ARGS);
       if (failed) break;
       if (ow + T >= W && fin) {  // the piece is full: next piece starts at fin
         ow = W;

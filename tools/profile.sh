@@ -25,5 +25,7 @@ run write 300 --pmc WRITE_SIZE
 if [ $SQ = 1 ]; then
   run sq1 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
   run sq2 300 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_BUSY_CYCLES
+  # (the effective clock: GRBM_GUI_ACTIVE / 8 XCDs / kernel time, MI355X_MICROARCH.md DVFS)
+  run sq3 300 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES
 fi
 echo "profile done"
