@@ -1628,14 +1628,32 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 #undef CPK_SP_A1G
 #undef CPK_SP_DEFER
 #define CPK_SP_RELOAD 1
+// (CPK_SPARSE_RING / _WPE / _A1G: A/B knobs for the form's ring, workgroups
+// per CU and A1 load groups)
+#ifdef CPK_SPARSE_RING
+#define CPK_SP_RING CPK_SPARSE_RING
+#else
 #define CPK_SP_RING 4096
+#endif
+#ifdef CPK_SPARSE_WPE
+#define CPK_SP_WPE CPK_SPARSE_WPE
+#else
 #define CPK_SP_WPE 6
+#endif
+#ifdef CPK_SPARSE_A1G
+#define CPK_SP_A1G CPK_SPARSE_A1G
+#else
 #define CPK_SP_A1G 4
+#endif
 #define CPK_SP_OWN_ROLES 1
+#ifdef CPK_SPARSE_HCALL
+#define CPK_SP_HCALL 1
+#endif
 namespace cpk_sparse {
 using namespace cpk;
 #include "encode_sp.hip"
 }  // namespace cpk_sparse
+#undef CPK_SP_HCALL
 #undef CPK_SP_OWN_ROLES
 #undef CPK_SP_DEFER
 #pragma pop_macro("CPK_SP_RELOAD")

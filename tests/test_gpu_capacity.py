@@ -62,15 +62,18 @@ def test_encode_batch_capacity(ctx, oracle, cfg, short):
                   lambda d_pk, c, d_off: ctx.encode_batch_cap(d_in, d_swo, 8192, d_pk, c, d_off))
 
 
+@pytest.mark.parametrize("nmsg", [60, 300])
 @pytest.mark.parametrize("short", [0, 1, "half"])
-def test_encode_messages_capacity(ctx, oracle, short):
-    """Message batches (tables built on the device): 300 messages of mixed
-    segments; the table pieces are refused like the segments."""
+def test_encode_messages_capacity(ctx, oracle, short, nmsg):
+    """Message batches (tables built on the device): 60 messages (at most
+    1,024 pieces: the single pass with the tables' descriptors) and 300
+    (the two passes) of mixed segments; the table pieces are refused like
+    the segments."""
     import torch
     import capnp_packed as cp
-    rng = np.random.default_rng(77)
+    rng = np.random.default_rng(77 + nmsg)
     msgs = []
-    for i in range(300):
+    for i in range(nmsg):
         nseg = int(rng.choice([1, 2, 3, 4, 9]))
         sizes = [int(rng.choice([0, 1, 17, 300, 2000, 9000])) for _ in range(nseg)]
         msgs.append([(rng.integers(0, 256, size=8 * s, dtype=np.uint8)
