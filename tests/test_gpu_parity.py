@@ -729,6 +729,20 @@ def test_gate_edges_and_sparse_form(ctx, oracle, cfg, words):
     _check_batch(ctx, oracle, oracle.generate(oracle.preset(cfg), swo), swo)
 
 
+@pytest.mark.parametrize("cfg", [2, 3, 4])
+def test_gate_big_piece_takes_single_pass(ctx, oracle, cfg):
+    """A batch with one piece over a unit and at least 1/2048 of the words
+    (a single message's segments, the last as large as all before it) goes
+    to the single pass whatever its density (round 6: the two passes would
+    give that piece one wave) -- dense (config 3), config-2 and sparse data,
+    the big piece first, in the middle and last."""
+    for order in range(3):
+        sizes = [17, 300, 4096, 1, 9000]
+        sizes.insert([0, 3, 5][order], 70000 + order)
+        swo = _swo(sizes)
+        _check_batch(ctx, oracle, oracle.generate(oracle.preset(cfg), swo), swo)
+
+
 def test_decode_host_few_large_pieces(ctx, oracle):
     """cpk_decode_host with a few large pieces (>= 8 MiB of words each on
     average) decodes them as one stream in parallel and keeps that result
