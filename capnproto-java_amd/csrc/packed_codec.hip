@@ -1697,7 +1697,8 @@ struct cpk_ctx_s {
   // host paths (cpk_encode_host[_gather], cpk_read_message_host) by phase,
   // summed per context and printed to stderr by cpk_ctx_destroy
   uint64_t rm_mw_max;     // cpk_read_message[_host]: streams under it by one workgroup (<= kRmMwMax)
-  bool e4_order;          // cpk_encode_messages' two passes: segments largest first (CPK_E4_ORDER=0: off)
+  int e4_order;           // cpk_encode_messages' two passes, segments largest first: 1 both passes,
+                          // 2 the emit pass only, 0 neither (CPK_E4_ORDER)
   bool trace;
   double tr_us[8];
   uint64_t tr_n[8];
@@ -1865,7 +1866,7 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     const char *m = getenv("CPK_RM_MW_MAX_KB");
     c->rm_mw_max = m ? (uint64_t)atoll(m) << 10 : 0;
     const char *o = getenv("CPK_E4_ORDER");
-    c->e4_order = !(o && o[0] == '0');
+    c->e4_order = o ? atoi(o) : 1;
   }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
@@ -2189,11 +2190,12 @@ int cpk_encode_messages_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo
     ord_launch(nullptr, nseg, shist, sord, s, d_swo);
     order = sord;
   }
+  const uint32_t *size_order = ctx->e4_order == 1 ? order : nullptr;
   if (nseg)
     hipLaunchKernelGGL(cpk::e4_size_kernel, dim3(grid), dim3(cpk::kE4Threads), 0, s,
                        (const uint64_t *)d_in, d_swo, nseg, ssize, ctx->tickets + cpk::kTkEnc,
                        max_seg_words, ctx->tickets + cpk::kTkErr, ctx->e4_bv, stride, (const uint32_t *)nullptr,
-                       order);
+                       size_order);
   hipLaunchKernelGGL(cpk::msg_table_size_kernel, dim3(tg), dim3(tb), 0, s, d_swo, d_msg_seg_off, nm,
                      tsize);
   hipLaunchKernelGGL(cpk::msg_interleave_kernel, dim3(tg), dim3(tb), 0, s, d_msg_seg_off, nm,
