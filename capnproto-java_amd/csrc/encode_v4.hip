@@ -226,18 +226,25 @@ __device__ __forceinline__ uint32_t e4_next_piece(uint32_t *ticket, int &xq, int
 }
 
 // ---- pass 1: packed size of every piece --------------------------------------
-// Piece seg's packed size (valid in lane 63) and its step rows in bvbuf.
-// kNt: the words' loads nontemporal (the two passes: U is read again only by
-// the emit pass, long after); the fused encoder keeps them cacheable.
-template <bool kNt>
-__device__ __forceinline__ uint64_t e4_size_piece(const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo,
-                                                  uint32_t seg, uint64_t hint, uint32_t *err,
-                                                  uint64_t *__restrict__ bvbuf, uint64_t stride, int lane) {
-  {
+__global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
+    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
+    uint64_t *__restrict__ sizes, uint32_t *ticket, uint64_t hint, uint32_t *err,
+    uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip, const uint32_t *order) {
+  if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;  // (the single pass took the batch)
+  const int lane = lane_id();
+  int xq = xcc_id(), dry = 0;
+  for (;;) {
+    const uint32_t tk = e4_next_piece(ticket, xq, dry, n);
+    if (tk >= n) break;
+    // (order: the pieces largest first)
+    const uint32_t seg = order ? (uint32_t)__builtin_amdgcn_readfirstlane((int)order[tk]) : tk;
     const uint64_t w0 = swo[seg];
     const uint64_t W = swo[seg + 1] - w0;
     if (((hint && W > hint) || W >= (1ull << 31)) && lane == 0) atomicOr(err, 1u);
-    if (W == 0) return 0;  // an empty piece: no bytes (and no loads: it may sit at the end)
+    if (W == 0) {  // an empty piece: no bytes (and no loads: it may sit at the end)
+      if (lane == 0) sizes[seg] = 0;
+      continue;
+    }
     const uint64_t *src = in + w0;
     // this piece's step rows in bvbuf: `stride` rows per piece when the
     // size hint bounds them, else packed by word offset (disjoint: a piece
@@ -266,12 +273,10 @@ __device__ __forceinline__ uint64_t e4_size_piece(const uint64_t *__restrict__ i
     // branches around them); words past the end are masked by `valid`
     const uint32_t kl = W32 - 1;
 #pragma unroll
-    for (int j = 0; j < PF; ++j) v[j] = kNt ? E4_SLD(src + min(((uint32_t)j << 6) + lane, kl))
-                                            : E4_LD2(src + min(((uint32_t)j << 6) + lane, kl));
+    for (int j = 0; j < PF; ++j) v[j] = E4_SLD(src + min(((uint32_t)j << 6) + lane, kl));
     for (uint32_t s0 = 0; s0 < nsteps; s0 += PF) {
 #pragma unroll
-      for (int j = 0; j < PF; ++j) vn[j] = kNt ? E4_SLD(src + min(((s0 + PF + j) << 6) + lane, kl))
-                                               : E4_LD2(src + min(((s0 + PF + j) << 6) + lane, kl));
+      for (int j = 0; j < PF; ++j) vn[j] = E4_SLD(src + min(((s0 + PF + j) << 6) + lane, kl));
 #pragma unroll
       for (int j = 0; j < PF; ++j) {
         const uint32_t k = ((s0 + j) << 6) + lane;
@@ -346,24 +351,7 @@ __device__ __forceinline__ uint64_t e4_size_piece(const uint64_t *__restrict__ i
     // wave sum in two 16-bit halves (a piece's packed size may pass 2^31)
     const uint32_t thi = (uint32_t)wave_incl_add((int)(acc >> 16));
     const uint32_t tlo = (uint32_t)wave_incl_add((int)(acc & 0xffffu));
-    return ((uint64_t)thi << 16) + tlo + bytes;
-  }
-}
-
-__global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_size_kernel(
-    const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
-    uint64_t *__restrict__ sizes, uint32_t *ticket, uint64_t hint, uint32_t *err,
-    uint64_t *__restrict__ bvbuf, uint64_t stride, const uint32_t *skip, const uint32_t *order) {
-  if (skip && __builtin_amdgcn_readfirstlane(*skip)) return;  // (the single pass took the batch)
-  const int lane = lane_id();
-  int xq = xcc_id(), dry = 0;
-  for (;;) {
-    const uint32_t tk = e4_next_piece(ticket, xq, dry, n);
-    if (tk >= n) break;
-    // (order: the pieces largest first)
-    const uint32_t seg = order ? (uint32_t)__builtin_amdgcn_readfirstlane((int)order[tk]) : tk;
-    const uint64_t sz = e4_size_piece<true>(in, swo, seg, hint, err, bvbuf, stride, lane);
-    if (lane == 63) sizes[seg] = sz;
+    if (lane == 63) sizes[seg] = ((uint64_t)thi << 16) + tlo + bytes;
   }
 }
 
@@ -526,70 +514,6 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
   }
 }
 
-// a step row: a plain (scalar) load, or (kCoh) an agent-scope load that
-// bypasses the vector L1 and never goes through the scalar cache, which
-// does not see this launch's vector stores
-template <bool kCoh>
-__device__ __forceinline__ uint64_t e4_row(const uint64_t *p) {
-  return kCoh ? rfl64(ld_status(const_cast<uint64_t *>(p))) : *p;
-}
-
-// Piece seg's packed bytes at out + obase (a piece of at least one word).
-// kCoh: the step rows read past the vector L1 (the fused encoder wrote them
-// earlier in the same launch; the two passes read them in the next kernel).
-template <bool kCoh>
-__device__ __forceinline__ void e4_emit_piece(const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo,
-                                              uint32_t seg, uint64_t obase, uint8_t *__restrict__ out,
-                                              const uint64_t *__restrict__ bvbuf, uint64_t stride,
-                                              const uint64_t *lut, uint32_t *ring, int lane) {
-  {
-    const uint64_t w0 = swo[seg];
-    const uint64_t W = swo[seg + 1] - w0;
-    const uint64_t *src = in + w0;
-    uint64_t rpos = obase, fl = obase >> 4;
-    // the boundaries of every step come from the size pass (bvbuf); past
-    // the piece every word is a boundary.  Words: this group of four steps
-    // and the next one's loads in flight.
-    const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;  // (pieces < 2^31 words)
-    if (stride && nsteps > stride) return;  // over the size hint: reported, output undefined
-    const uint64_t *bvp = bvbuf + 3 * (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
-    // steps of loads in flight ahead of the emit (2 and 8 measured 1-2 %
-    // slower, r4AL_ab.log)
-    constexpr int EPF = 4;
-    uint64_t vc[EPF], vl[EPF];
-    const uint32_t kl = W32 - 1;  // loads clamped, not predicated
-#pragma unroll
-    for (int j = 0; j < EPF; ++j) vc[j] = E4_LD2(src + min(((uint32_t)j << 6) + lane, kl));
-    for (uint32_t s0 = 0; s0 < nsteps; s0 += EPF) {
-#pragma unroll
-      for (int j = 0; j < EPF; ++j) vl[j] = E4_LD2(src + min(((s0 + EPF + j) << 6) + lane, kl));
-      uint64_t bv[EPF + 4], mem[EPF], hc[EPF];
-#pragma unroll
-      for (int j = 0; j < EPF + 4; ++j) bv[j] = s0 + j < nsteps ? e4_row<kCoh>(bvp + 3 * (s0 + j)) : ~0ull;
-#pragma unroll
-      for (int j = 0; j < EPF; ++j) {
-        mem[j] = s0 + j < nsteps ? e4_row<kCoh>(bvp + 3 * (s0 + j) + 1) : 0ull;
-        hc[j] = s0 + j < nsteps ? e4_row<kCoh>(bvp + 3 * (s0 + j) + 2) : 0ull;
-      }
-#pragma unroll
-      for (int j = 0; j < EPF; ++j) {
-        if (s0 + j < nsteps)
-          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W32, bv[j], bv[j + 1], bv[j + 2], bv[j + 3],
-                       bv[j + 4], mem[j], hc[j], lane, lut, ring, out, rpos, fl, obase);
-      }
-#pragma unroll
-      for (int j = 0; j < EPF; ++j) vc[j] = vl[j];
-    }
-    wave_lds_order();
-    e4_flush(out, ring, fl, rpos >> 4, obase, lane);
-    // the piece's last, partial line
-    if (rpos > fl * 16) {
-      const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
-      e4_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane);
-    }
-  }
-}
-
 __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     const uint64_t *__restrict__ in, const uint64_t *__restrict__ swo, uint32_t n,
     const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out, uint32_t *ticket,
@@ -610,7 +534,10 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     const uint32_t tk = e4_next_piece(ticket, xq, dry, n);
     if (tk >= n) break;
     const uint32_t seg = order ? (uint32_t)__builtin_amdgcn_readfirstlane((int)order[tk]) : tk;
-    if (swo[seg + 1] == swo[seg]) continue;  // no bytes; no loads (it may sit at the end of the input)
+    const uint64_t w0 = swo[seg];
+    const uint64_t W = swo[seg + 1] - w0;
+    if (W == 0) continue;  // no bytes; no loads (it may sit at the end of the input)
+    const uint64_t *src = in + w0;
     const uint64_t obase = out_off[seg];
     // a piece whose bytes would pass the caller's capacity is not written
     // (ArrayOutputStream.java:40-42 refuses such a write); reported
@@ -618,7 +545,47 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
       if (lane == 0) atomicOr(err, kErrCap);
       continue;
     }
-    e4_emit_piece<false>(in, swo, seg, obase, out, bvbuf, stride, lut, ring, lane);
+    uint64_t rpos = obase, fl = obase >> 4;
+    // the boundaries of every step come from the size pass (bvbuf); past
+    // the piece every word is a boundary.  Words: this group of four steps
+    // and the next one's loads in flight.
+    const uint32_t W32 = (uint32_t)W, nsteps = (W32 + 63) >> 6;  // (pieces < 2^31 words)
+    if (stride && nsteps > stride) continue;  // over the size hint: reported, output undefined
+    const uint64_t *bvp = bvbuf + 3 * (stride ? (uint64_t)seg * stride : (w0 - swo[0]) / 64 + seg);
+    // steps of loads in flight ahead of the emit (2 and 8 measured 1-2 %
+    // slower, r4AL_ab.log)
+    constexpr int EPF = 4;
+    uint64_t vc[EPF], vl[EPF];
+    const uint32_t kl = W32 - 1;  // loads clamped, not predicated
+#pragma unroll
+    for (int j = 0; j < EPF; ++j) vc[j] = E4_LD2(src + min(((uint32_t)j << 6) + lane, kl));
+    for (uint32_t s0 = 0; s0 < nsteps; s0 += EPF) {
+#pragma unroll
+      for (int j = 0; j < EPF; ++j) vl[j] = E4_LD2(src + min(((s0 + EPF + j) << 6) + lane, kl));
+      uint64_t bv[EPF + 4], mem[EPF], hc[EPF];
+#pragma unroll
+      for (int j = 0; j < EPF + 4; ++j) bv[j] = s0 + j < nsteps ? bvp[3 * (s0 + j)] : ~0ull;
+#pragma unroll
+      for (int j = 0; j < EPF; ++j) {
+        mem[j] = s0 + j < nsteps ? bvp[3 * (s0 + j) + 1] : 0ull;
+        hc[j] = s0 + j < nsteps ? bvp[3 * (s0 + j) + 2] : 0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < EPF; ++j) {
+        if (s0 + j < nsteps)
+          e4_emit_step(vc[j], ((s0 + j) << 6) + lane < W32, bv[j], bv[j + 1], bv[j + 2], bv[j + 3],
+                       bv[j + 4], mem[j], hc[j], lane, lut, ring, out, rpos, fl, obase);
+      }
+#pragma unroll
+      for (int j = 0; j < EPF; ++j) vc[j] = vl[j];
+    }
+    wave_lds_order();
+    e4_flush(out, ring, fl, rpos >> 4, obase, lane);
+    // the piece's last, partial line
+    if (rpos > fl * 16) {
+      const int j0 = (int)((obase > fl * 16 ? obase : fl * 16) - fl * 16);
+      e4_store_bytes(out, ring, fl, j0, (int)(rpos - fl * 16), lane);
+    }
   }
 }
 

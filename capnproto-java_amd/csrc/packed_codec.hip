@@ -1602,7 +1602,6 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
 #undef CPK_SP_HCALL
 #undef CPK_SP_RING
 #include "encode_sp3.hip"
-#include "encode_fused.hip"
 #include "decode_v2.hip"
 #include "stream_split.hip"
 
@@ -1700,9 +1699,6 @@ struct cpk_ctx_s {
   uint64_t rm_mw_max;     // cpk_read_message[_host]: streams under it by one workgroup (<= kRmMwMax)
   int e4_order;           // cpk_encode_messages' two passes, segments largest first: 1 both passes,
                           // 2 the emit pass only, 0 neither (CPK_E4_ORDER)
-  int e4_fused;           // cpk_encode_batch's two passes as one launch (encode_fused.hip, CPK_E4_FUSED)
-  int e4f_wg;             //   its workgroups per CU (CPK_E4F_WG) and pending pieces per wave (CPK_E4F_DEPTH)
-  int e4f_depth;
   bool trace;
   double tr_us[8];
   uint64_t tr_n[8];
@@ -1871,14 +1867,6 @@ int cpk_ctx_create(int device, cpk_ctx *out) {
     c->rm_mw_max = m ? (uint64_t)atoll(m) << 10 : 0;
     const char *o = getenv("CPK_E4_ORDER");
     c->e4_order = o ? atoi(o) : 1;
-    const char *fu = getenv("CPK_E4_FUSED");
-    c->e4_fused = fu ? atoi(fu) : 0;
-    const char *fw = getenv("CPK_E4F_WG");
-    c->e4f_wg = fw ? atoi(fw) : CPK_E4F_WPE;
-    if (c->e4f_wg < 1 || c->e4f_wg > CPK_E4F_WPE) c->e4f_wg = CPK_E4F_WPE;
-    const char *fd = getenv("CPK_E4F_DEPTH");
-    c->e4f_depth = fd ? atoi(fd) : 2;
-    if (c->e4f_depth < 1 || c->e4f_depth > cpk::kE4fMaxDepth) c->e4f_depth = 2;
   }
   if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     c->cus = 256;
@@ -1976,15 +1964,18 @@ static bool sp_takes(cpk_ctx ctx, uint32_t n, uint64_t max_seg_words) {
   return ctx->encoder != 4 && max_seg_words != 0 && sp_unit_bound(n, max_seg_words) <= (1ull << 25);
 }
 
-// `words` look-back words (ctx->sp_status) for a launch at a new epoch:
-// cleared only when the epoch wraps or the array grows
-static int sp_status_prep(cpk_ctx ctx, uint64_t words, hipStream_t s) {
+// `units`: a bound on the batch's units when its pieces may exceed one
+// chunk (0: every piece is one unit)
+int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64_t *pdesc,
+              const uint64_t *tin, uint32_t n, uint64_t hint, void *d_out, uint64_t *d_out_off,
+              hipStream_t s, bool gated = false, uint64_t units = 0, uint64_t out_cap = ~0ull) {
+  const uint64_t ucap = units ? units : n;  // look-back words (+ as many run-state words)
   bool fresh = false;
-  if (words > ctx->sp_cap) {
+  if (2 * ucap > ctx->sp_cap) {
     if (ctx->sp_status) hipFree(ctx->sp_status);
     ctx->sp_status = nullptr;
     ctx->sp_cap = 0;
-    const uint64_t cap = words < 8192 ? 8192 : words + words / 4;
+    const uint64_t cap = 2 * ucap < 8192 ? 8192 : 2 * ucap + ucap / 2;
     if (hipMalloc(&ctx->sp_status, cap * 8) != hipSuccess) return CPK_ENOMEM;
     ctx->sp_cap = cap;
     fresh = true;
@@ -1994,17 +1985,6 @@ static int sp_status_prep(cpk_ctx ctx, uint64_t words, hipStream_t s) {
     fresh = true;
   }
   if (fresh && hipMemsetAsync(ctx->sp_status, 0, ctx->sp_cap * 8, s) != hipSuccess) return CPK_EDEVICE;
-  return CPK_OK;
-}
-
-// `units`: a bound on the batch's units when its pieces may exceed one
-// chunk (0: every piece is one unit)
-int sp_launch(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, const uint64_t *pdesc,
-              const uint64_t *tin, uint32_t n, uint64_t hint, void *d_out, uint64_t *d_out_off,
-              hipStream_t s, bool gated = false, uint64_t units = 0, uint64_t out_cap = ~0ull) {
-  const uint64_t ucap = units ? units : n;  // look-back words (+ as many run-state words)
-  int rc = sp_status_prep(ctx, 2 * ucap, s);
-  if (rc) return rc;
   uint64_t *ustate = ctx->sp_status + ucap;
   const uint64_t *utab = nullptr, *nunits = nullptr;
   if (units) {
@@ -2125,20 +2105,6 @@ int e4_encode(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, uint32_t n, 
     hipLaunchKernelGGL(cpk::e4_minmax_kernel, dim3(mg), dim3(256), 0, s, d_swo, n, mm, (const uint64_t *)d_in);
     hipLaunchKernelGGL(cpk::e4_gate_kernel, dim3(1), dim3(64), 0, s, ctx->tickets, mg * 256u, (uint32_t)ctx->sp_form,
                        d_swo, n);
-  }
-  if (ctx->e4_fused) {
-    // one launch: each wave sizes a piece, publishes it for the look-back and
-    // emits its oldest pending piece whose offset is known (encode_fused.hip)
-    rc = sp_status_prep(ctx, n, s);
-    if (rc) return rc;
-    unsigned fg = (unsigned)(ctx->e4f_wg * ctx->cus);
-    if (fg > (n + cpk::kE4Waves - 1) / cpk::kE4Waves) fg = (n + cpk::kE4Waves - 1) / cpk::kE4Waves;
-    hipLaunchKernelGGL(cpk::e4_fused_kernel, dim3(fg), dim3(cpk::kE4Threads), cpk::kE4Lds, s,
-                       (const uint64_t *)d_in, d_swo, n, (uint8_t *)d_out, d_out_off, ctx->sp_status,
-                       ctx->sp_epoch, ctx->tickets + cpk::kTkEnc, ctx->e4_bv, stride,
-                       gate ? (const uint32_t *)(ctx->tickets + cpk::kTkGate + 2) : (const uint32_t *)nullptr,
-                       hint, out_cap, ctx->tickets + cpk::kTkErr, (uint32_t)ctx->e4f_depth);
-    return hip_ok(hipGetLastError());
   }
   unsigned grid = (unsigned)(8 * ctx->cus);
   if (grid > (n + cpk::kE4Waves - 1) / cpk::kE4Waves) grid = (n + cpk::kE4Waves - 1) / cpk::kE4Waves;
