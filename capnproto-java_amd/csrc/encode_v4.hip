@@ -12,16 +12,25 @@
 //                    bytes, count) is OR-ed into a 2 KiB LDS ring at its byte
 //                    position and complete 16-byte lines stream to memory.
 //                    A head's count needs the end of its run, at most 256
-//                    words on: the emit walk classifies 4 steps ahead.
+//                    words on: the emit walk reads the size pass's boundary
+//                    rows 4 steps ahead (rows and words one group of steps
+//                    ahead of their use; the strings and their placement in
+//                    encode_sp.hip's form: round 6, config-3 density -0.9 %)
 // Traffic: U + (U + P) instead of U + P, in exchange for no barriers, no
 // look-back and every wave independent (both passes are pure streams).
 
 constexpr int kE4Waves = 4;
 constexpr int kE4Threads = 64 * kE4Waves;
 constexpr uint32_t kE4RingBytes = 2048;  // output ring per wave (<= 41 live lines)
+// Each string is OR-ed from its first ring dword on without a wrap per
+// dword: a string's last three dwords past the ring's end go to one overhang
+// line, OR-ed into line 0 when that is stored (the ring holds at most 104
+// unstored lines, so line 0's previous bytes are out by then).
+constexpr uint32_t kE4Ov = 1u;                                    // overhang lines
+constexpr uint32_t kE4RingStride = kE4RingBytes + 16 * kE4Ov;
 constexpr uint32_t kE4oLut = 0;                                   // u64[256]
-constexpr uint32_t kE4oRing = 2048;                               // u32[waves][512]
-constexpr uint32_t kE4Lds = kE4oRing + kE4Waves * kE4RingBytes;   // 10 KiB
+constexpr uint32_t kE4oRing = 2048;                               // u32[waves][512 (+ 164)]
+constexpr uint32_t kE4Lds = kE4oRing + kE4Waves * kE4RingStride;  // 10 KiB (12.6 KiB with overhang)
 
 // the size pass's row per 64-word step for the emit pass: run boundaries,
 // literal-run members, heads (3 u64); at most 4 GiB of rows
@@ -38,6 +47,12 @@ constexpr uint32_t kE4RingDw = kE4RingBytes / 4;
 // long after; config-3 encode -2 %, r4AT_e4_size_nt_ab.log)
 #define E4_SLD(p) ld_stream(p)
 
+// lane l's 64-bit value, wave-uniform
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+}
+
 __device__ __forceinline__ uint32_t e4_tag(uint64_t v) {
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
   // bit 7 of each byte: the byte is nonzero (no carry crosses a byte); the
@@ -49,17 +64,36 @@ __device__ __forceinline__ uint32_t e4_tag(uint64_t v) {
   return __builtin_amdgcn_udot4(th, 0x80402010u, __builtin_amdgcn_udot4(tl, 0x08040201u, 0u, false), false) >> 7;
 }
 
+// ring line r (OR its overhang line) / cleared
+__device__ __forceinline__ uint4 e4_line(const uint32_t *ring, uint32_t r) {
+  const uint4 *rl = reinterpret_cast<const uint4 *>(ring);
+  uint4 v = rl[r];
+  if (r < kE4Ov) {
+    const uint4 o = rl[kE4RingLines + r];
+    v.x |= o.x;
+    v.y |= o.y;
+    v.z |= o.z;
+    v.w |= o.w;
+  }
+  return v;
+}
+__device__ __forceinline__ void e4_line_clear(uint32_t *ring, uint32_t r) {
+  uint4 *rl = reinterpret_cast<uint4 *>(ring);
+  rl[r] = make_uint4(0u, 0u, 0u, 0u);
+  if (r < kE4Ov) rl[kE4RingLines + r] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 // bytes [j0, j1) of global line L from the ring, then clears the ring line
 __device__ __forceinline__ void e4_store_bytes(uint8_t *out, uint32_t *ring, uint64_t L, int j0,
                                                int j1, int lane) {
-  uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kE4RingLines - 1));
-  const uint4 val = *rl;
+  const uint32_t r = (uint32_t)L & (kE4RingLines - 1);
+  const uint4 val = e4_line(ring, r);
   if (lane >= j0 && lane < j1) {
     const uint32_t d = (lane & 8) ? ((lane & 4) ? val.w : val.z) : ((lane & 4) ? val.y : val.x);
     out[L * 16 + lane] = (uint8_t)(d >> (8 * (lane & 3)));
   }
   wave_lds_order();
-  if (lane == 0) *rl = make_uint4(0u, 0u, 0u, 0u);
+  if (lane == 0) e4_line_clear(ring, r);
 }
 
 // stores the complete lines [fl, upto) of the ring; bytes below `lo` belong
@@ -74,9 +108,9 @@ __device__ __forceinline__ void e4_flush(uint8_t *out, uint32_t *ring, uint64_t 
   for (uint64_t L0 = fl; L0 < upto; L0 += 64) {
     const uint64_t L = L0 + lane;
     if (L < upto) {
-      uint4 *rl = reinterpret_cast<uint4 *>(ring) + (L & (kE4RingLines - 1));
-      const uint4 val = *rl;
-      *rl = make_uint4(0u, 0u, 0u, 0u);
+      const uint32_t r = (uint32_t)L & (kE4RingLines - 1);
+      const uint4 val = e4_line(ring, r);
+      e4_line_clear(ring, r);
       *reinterpret_cast<uint4 *>(out + L * 16) = val;
     }
   }
@@ -85,10 +119,6 @@ __device__ __forceinline__ void e4_flush(uint8_t *out, uint32_t *ring, uint64_t 
 
 constexpr int kE4Wpe = 8;
 
-// word group: 0 zero word, 1 D/L (<= 1 zero byte), 2 M, 3 past the piece's end
-__device__ __forceinline__ int e4_group(uint32_t m, bool valid) {
-  return !valid ? 3 : (m == 0 ? 0 : (__builtin_popcount(m) >= 7 ? 1 : 2));
-}
 
 #include "sp_roles.hip"  // SpSt, sp_roles: the run roles as mask algebra (shared with encode_sp.hip)
 
@@ -452,56 +482,60 @@ __device__ __forceinline__ void e4_emit_step(uint64_t word, bool valid, uint64_t
                                              uint64_t bv4, uint64_t mem, uint64_t hc, int lane,
                                              const uint64_t *lut, uint32_t *ring, uint8_t *out,
                                              uint64_t &rpos, uint64_t &fl, uint64_t obase) {
-  const uint32_t m = e4_tag(word);
-  const int g = e4_group(m, valid);
-  const uint32_t memb = (uint32_t)(mem >> lane) & 1u, head = (uint32_t)(hc >> lane) & 1u;
-  // a head's count: words to its run's end, at most 255 (:123-131, :143-164)
-  uint32_t cnt = 0;
-  if (hc) {
-    const uint64_t gtm = lane == 63 ? 0ull : (~0ull << (lane + 1));
-    const uint64_t bb = bv0 & gtm;
-    const int nbr = bv1 ? 64 + __builtin_ctzll(bv1)
-                        : bv2 ? 128 + __builtin_ctzll(bv2)
-                              : bv3 ? 192 + __builtin_ctzll(bv3)
-                                    : bv4 ? 256 + __builtin_ctzll(bv4) : 320;
-    const int re = bb ? __builtin_ctzll(bb) : nbr;
-    cnt = head ? (uint32_t)min(255, re - lane - 1) : 0u;
-  }
-  // bytes: M 1 + popcount, D/L 8 (a member verbatim, an L head tag + 7),
-  // + 2 for a head's count byte and (Z) tag / (D) extra byte
-  const uint32_t nb = (g == 2 ? 1u + __builtin_popcount(m) : 0u) + (g == 1 ? 8u : 0u) + 2u * head;
-  // the string: tag, the nonzero bytes (v_perm with the compaction LUT), the
-  // count after a 0x00 / 0xFF tag; a literal-run member is its 8 bytes (:163-171)
+  // (encode_sp.hip's string form: per-lane selects on the rows' scalar
+  // masks instead of per-lane mask bits and word classes)
+  const uint32_t m = valid ? e4_tag(word) : 0u;  // (a word past the piece: no bytes)
+  const uint64_t ZW = __ballot(m == 0);
   const uint32_t lo = (uint32_t)word, hi = (uint32_t)(word >> 32);
   const uint64_t sel = lut[m];
   const uint32_t c0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
   const uint32_t c1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
-  const uint32_t c0p = m == 0 ? cnt : c0;
+  uint32_t cz = 0, cd = 0;
+  if (hc) {
+    // a head's count: words to its run's end, at most 255 (:123-131,
+    // :143-164) -- the next boundary after the lane in this step, else X
+    // words past the step's end (v_ffbl: 0xffffffff for none)
+    const uint32_t X = bv1 ? (uint32_t)__builtin_ctzll(bv1)
+                           : bv2 ? 64u + (uint32_t)__builtin_ctzll(bv2)
+                                 : bv3 ? 128u + (uint32_t)__builtin_ctzll(bv3)
+                                       : bv4 ? 192u + (uint32_t)__builtin_ctzll(bv4) : 256u;
+    const uint64_t e = (bv0 >> lane) >> 1;
+    const uint32_t z_lo = sp_ffbl((uint32_t)e);
+    const uint32_t z_hi = sp_ffbl((uint32_t)(e >> 32)) | 32u;
+    const uint32_t tt = min(min(z_lo, z_hi), min((uint32_t)(63 - lane) + X, 255u));
+    cz = sp_sel(0u, tt, hc & ZW);   // zero-run heads: the count after the 0x00 tag
+    cd = sp_sel(0u, tt, hc & ~ZW);  // 0xFF heads: the count after the 8 bytes
+  }
+  const uint32_t c0p = c0 | cz;
   uint32_t s0 = m | (c0p << 8);
   uint32_t s1 = __builtin_amdgcn_alignbyte(c1, c0p, 3);
-  uint32_t s2 = __builtin_amdgcn_alignbyte(m == 0xffu ? cnt : 0u, c1, 3);
-  if (memb) {
-    s0 = lo;
-    s1 = hi;
-    s2 = 0;
-  }
+  uint32_t s2 = __builtin_amdgcn_alignbyte(cd, c1, 3);
+  s0 = sp_sel(s0, lo, mem);
+  s1 = sp_sel(s1, hi, mem);
+  s2 = sp_sel(s2, 0u, mem);
+  uint32_t nb = (uint32_t)__builtin_popcount(m) + sp_sel(1u, 2u, hc);
+  nb = sp_sel(nb, 8u, mem);
+  nb = sp_sel(nb, 0u, ZW & ~hc);  // a zero word that is no head, or past the piece
   const int incl = wave_incl_add((int)nb);
   const uint32_t o = (uint32_t)incl - nb;
   const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
   if (stot) {
     // OR the string into the ring at its output position (the ring's lines
     // are zero until written; bytes past a string are zero)
+    // (the string shifted onto its byte by one v_perm per dword, selector
+    // bytes [4 - b, 8 - b) of (s_k : s_k-1); from its first ring dword on,
+    // past the ring's end into the overhang line)
     const uint32_t p = (uint32_t)rpos + o;
-    const uint32_t sh = (p & 3) * 8;
-    const uint64_t a01 = (((uint64_t)s1 << 32) | s0) << sh;
-    const uint64_t a12 = (((uint64_t)s2 << 32) | s1) << sh;
-    const uint32_t w3 = (uint32_t)(((uint64_t)s2 << sh) >> 32);
-    const uint32_t d0 = (p >> 2) & (kE4RingDw - 1);
+    const uint32_t b = p & 3;
+    const uint32_t psel = 0x07060504u - __builtin_amdgcn_perm(0u, b, 0u);  // (b in every byte)
+    const uint32_t d0 = __builtin_amdgcn_perm(s0, 0u, psel), d1 = __builtin_amdgcn_perm(s1, s0, psel);
+    const uint32_t d2 = __builtin_amdgcn_perm(s2, s1, psel), d3 = __builtin_amdgcn_perm(0u, s2, psel);
+    uint32_t *rp = ring + ((p >> 2) & (kE4RingDw - 1));
     if (nb) {
-      atomicOr(&ring[d0], (uint32_t)a01);
-      atomicOr(&ring[(d0 + 1) & (kE4RingDw - 1)], (uint32_t)(a01 >> 32));
-      atomicOr(&ring[(d0 + 2) & (kE4RingDw - 1)], (uint32_t)(a12 >> 32));
-      atomicOr(&ring[(d0 + 3) & (kE4RingDw - 1)], w3);
+      atomicOr(rp, d0);
+      atomicOr(rp + 1, d1);
+      atomicOr(rp + 2, d2);
+      atomicOr(rp + 3, d3);
     }
     rpos += stot;
     // complete lines go out 64 at a time (one full-wave store: flushing
@@ -524,9 +558,9 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
   const uint64_t *lut = reinterpret_cast<const uint64_t *>(smem + kE4oLut);
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
-  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kE4oRing + w * kE4RingBytes);
+  uint32_t *ring = reinterpret_cast<uint32_t *>(smem + kE4oRing + w * kE4RingStride);
   fill_luts(reinterpret_cast<uint64_t *>(smem + kE4oLut), false);
-  for (uint32_t i = lane; i < kE4RingLines; i += 64)
+  for (uint32_t i = lane; i < kE4RingLines + kE4Ov; i += 64)
     reinterpret_cast<uint4 *>(ring)[i] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
   int xq = xcc_id(), dry = 0;
@@ -559,16 +593,28 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
     const uint32_t kl = W32 - 1;  // loads clamped, not predicated
 #pragma unroll
     for (int j = 0; j < EPF; ++j) vc[j] = E4_LD2(src + min(((uint32_t)j << 6) + lane, kl));
+    // the rows of a group's steps and the next four (3 x (EPF + 4) u64, one
+    // per lane) by one vector load a group ahead, like the words: the
+    // scalar loads of them at the group's start left their HBM latency
+    // exposed once per group
+    static_assert(3 * (EPF + 4) <= 64, "a group's rows fit the lanes");
+    auto ldrows = [&](uint32_t g0) __attribute__((always_inline)) -> uint64_t {
+      const uint32_t k = (uint32_t)lane / 3u, f = (uint32_t)lane - 3u * k;
+      if (lane >= 3 * (EPF + 4)) return 0ull;
+      return g0 + k < nsteps ? bvp[3 * g0 + (uint32_t)lane] : (f == 0 ? ~0ull : 0ull);
+    };
+    uint64_t rw = ldrows(0), rwn;
     for (uint32_t s0 = 0; s0 < nsteps; s0 += EPF) {
 #pragma unroll
       for (int j = 0; j < EPF; ++j) vl[j] = E4_LD2(src + min(((s0 + EPF + j) << 6) + lane, kl));
       uint64_t bv[EPF + 4], mem[EPF], hc[EPF];
+      rwn = ldrows(s0 + EPF);
 #pragma unroll
-      for (int j = 0; j < EPF + 4; ++j) bv[j] = s0 + j < nsteps ? bvp[3 * (s0 + j)] : ~0ull;
+      for (int j = 0; j < EPF + 4; ++j) bv[j] = rl64(rw, 3 * j);
 #pragma unroll
       for (int j = 0; j < EPF; ++j) {
-        mem[j] = s0 + j < nsteps ? bvp[3 * (s0 + j) + 1] : 0ull;
-        hc[j] = s0 + j < nsteps ? bvp[3 * (s0 + j) + 2] : 0ull;
+        mem[j] = rl64(rw, 3 * j + 1);
+        hc[j] = rl64(rw, 3 * j + 2);
       }
 #pragma unroll
       for (int j = 0; j < EPF; ++j) {
@@ -578,6 +624,7 @@ __global__ __launch_bounds__(kE4Threads, kE4Wpe) void e4_emit_kernel(
       }
 #pragma unroll
       for (int j = 0; j < EPF; ++j) vc[j] = vl[j];
+      rw = rwn;
     }
     wave_lds_order();
     e4_flush(out, ring, fl, rpos >> 4, obase, lane);
