@@ -584,10 +584,26 @@ __device__ __forceinline__ void sp_b(SpRegs &R, int cnt, const uint64_t *lut, ui
     ldw(j + 2 * 2);
     ldw(j + 2 * 2 + 1);
 #endif
+#if CPK_SP_SKIP
+    // (the sparse form: a step of zero words and no head -- inside a zero
+    // run -- has no bytes: its strings are not built, and a pair of them is
+    // skipped whole)
+    auto empty = [&](const int k) __attribute__((always_inline)) {
+      const uint32_t m = (R.mp[k >> 2] >> (8 * (k & 3))) & 0xffu;
+      return k >= cnt || (__ballot(m != 0u) == 0ull && sp_rl(R.ohl, R.ohh, k) == 0ull);
+    };
+    const bool ea = empty(j), eb = empty(j + 1);
+    if (!(ea && eb))
+#endif
     {
-      uint32_t a0, a1, a2, na, b0 = 0, b1 = 0, b2 = 0, nb2 = 0;
+      uint32_t a0 = 0, a1 = 0, a2 = 0, na = 0, b0 = 0, b1 = 0, b2 = 0, nb2 = 0;
+#if CPK_SP_SKIP
+      if (!ea) strings(j, a0, a1, a2, na);
+      if (!eb) strings(j + 1, b0, b1, b2, nb2);
+#else
       strings(j, a0, a1, a2, na);
       if (j + 1 < cnt) strings(j + 1, b0, b1, b2, nb2);
+#endif
       const uint32_t pk = na | (nb2 << 16);
       const uint32_t incl = (uint32_t)wave_incl_add((int)pk);
       const uint32_t stot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
