@@ -1692,6 +1692,7 @@ struct cpk_ctx_s {
   uint64_t ss_cap;        //   u64 entries
   uint64_t *rm_buf;       // cpk_read_message: piece word offsets | piece ends | statuses (lazy)
   uint64_t *fl_buf;       // cpk_decode_batch of a few large pieces: boundaries found [33] (lazy)
+  uint64_t *probe_pin;    //   and their extent, read back through pinned host memory [4] (lazy)
   uint8_t *rm_copy;       // cpk_read_message_host, one-wave path: the packed bytes on the device (lazy)
   uint64_t small_seq;     // the one-launch host paths' completion flag values (small_wait)
   uint64_t small_fallbacks;  // small_wait calls whose flag was unset even after a stream sync (lost flags)
@@ -1931,6 +1932,7 @@ void cpk_ctx_destroy(cpk_ctx ctx) {
   if (ctx->ss_buf) hipFree(ctx->ss_buf);
   if (ctx->rm_buf) hipFree(ctx->rm_buf);
   if (ctx->fl_buf) hipFree(ctx->fl_buf);
+  if (ctx->probe_pin) hipHostFree(ctx->probe_pin);
   if (ctx->rm_copy) hipFree(ctx->rm_copy);
   if (ctx->sp_units) hipFree(ctx->sp_units);
   pipe_destroy(ctx->pipe);
@@ -2363,13 +2365,16 @@ static int decode_batch_impl(cpk_ctx ctx, const void *d_packed, const uint64_t *
     // blocks in parallel, and let the batch decoders skip when every piece
     // ended exactly at its packed range's end (dec_stream_check_kernel);
     // otherwise they run after it and report the batch form's statuses.
-    uint64_t e[4];
-    if (hipMemcpyAsync(&e[0], d_in_off, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&e[1], d_in_off + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&e[2], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&e[3], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return CPK_EDEVICE;
+    // (one small kernel writes the four words to pinned host memory: four
+    // copies into pageable memory cost ~75 us per call, ADVICE r5,
+    // profiles/r6b_small_decode_launch_overhead.txt)
+    if (!ctx->probe_pin && hipHostMalloc((void **)&ctx->probe_pin, 4 * 8, hipHostMallocDefault) != hipSuccess) {
+      ctx->probe_pin = nullptr;
+      return CPK_ENOMEM;
+    }
+    hipLaunchKernelGGL(cpk::dec_probe_kernel, dim3(1), dim3(64), 0, s, d_in_off, d_swo, n, ctx->probe_pin);
+    if (hipStreamSynchronize(s) != hipSuccess) return CPK_EDEVICE;
+    const uint64_t *e = ctx->probe_pin;
     if (e[3] - e[2] >= ((uint64_t)n << 20) && (e[0] & 15) == 0 && e[1] >= e[0]) {
       if (!ctx->fl_buf && hipMalloc(&ctx->fl_buf, 33 * 8) != hipSuccess) return CPK_ENOMEM;
       int rc = cpk_decode_stream(ctx, (const uint8_t *)d_packed + e[0], e[1] - e[0], d_swo, n, d_out, ctx->fl_buf,
