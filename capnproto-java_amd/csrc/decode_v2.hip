@@ -407,18 +407,6 @@ __global__ __launch_bounds__(kD2Threads, kD2Wpe) void decode2_kernel(
   WPH_FLUSH(16)
 }
 
-// the extent of a batch -- in_off[0], in_off[n], swo[0], swo[n] -- into
-// pinned host memory (decode_batch_impl's probe of a few pieces)
-__global__ void dec_probe_kernel(const uint64_t *__restrict__ in_off, const uint64_t *__restrict__ swo, uint32_t n,
-                                 uint64_t *out) {
-  if (threadIdx.x == 0) {
-    out[0] = in_off[0];
-    out[1] = in_off[n];
-    out[2] = swo[0];
-    out[3] = swo[n];
-  }
-}
-
 // ---- decoder choice on the device (cpk_decode_batch, no host sync) --------
 // Sparse batches (packed bytes under 15 % of the words' bytes: long zero
 // runs) go to the record-index decoder, which measured 2.75 against 3.46 ms

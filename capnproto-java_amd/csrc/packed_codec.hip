@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "../../include/capnp_packed.h"
+#include <initializer_list>
 
 namespace cpk {
 
@@ -1588,6 +1589,16 @@ __global__ void mismatch_kernel(const uint64_t *__restrict__ a, const uint64_t *
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
 }
 
+// up to 8 device words gathered into pinned host memory, for the host's
+// read-backs of a few sizes (read_words): one launch and one sync instead
+// of a copy into pageable memory per word (~15-20 us each)
+struct Gather8 {
+  const uint64_t *p[8];
+};
+__global__ void gather8_kernel(Gather8 g, uint32_t k, uint64_t *out) {
+  if (threadIdx.x < k) out[threadIdx.x] = *g.p[threadIdx.x];
+}
+
 #include "encode_v4.hip"
 // the dense form's ring: 11 KiB per wave, the most three workgroups per CU
 // leave room for (round 4: config 2's ~7.7 KiB of output per wave overflowed
@@ -1692,7 +1703,7 @@ struct cpk_ctx_s {
   uint64_t ss_cap;        //   u64 entries
   uint64_t *rm_buf;       // cpk_read_message: piece word offsets | piece ends | statuses (lazy)
   uint64_t *fl_buf;       // cpk_decode_batch of a few large pieces: boundaries found [33] (lazy)
-  uint64_t *probe_pin;    //   and their extent, read back through pinned host memory [4] (lazy)
+  uint64_t *probe_pin;    // host read-backs of a few device words (read_words): pinned [8] (lazy)
   uint8_t *rm_copy;       // cpk_read_message_host, one-wave path: the packed bytes on the device (lazy)
   uint64_t small_seq;     // the one-launch host paths' completion flag values (small_wait)
   uint64_t small_fallbacks;  // small_wait calls whose flag was unset even after a stream sync (lost flags)
@@ -1955,6 +1966,22 @@ int cpk_ctx_dense_windows(cpk_ctx ctx, void *stream, uint64_t *serial, uint64_t 
   return CPK_OK;
 }
 
+// The device words at src[0..k) (k <= 8) on the host, after the work already
+// on stream s: one small kernel writes them to the context's pinned words.
+static int read_words(cpk_ctx ctx, hipStream_t s, std::initializer_list<const uint64_t *> src, uint64_t *dst) {
+  if (!ctx->probe_pin && hipHostMalloc((void **)&ctx->probe_pin, 8 * 8, hipHostMallocDefault) != hipSuccess) {
+    ctx->probe_pin = nullptr;
+    return CPK_ENOMEM;
+  }
+  cpk::Gather8 g = {};
+  uint32_t k = 0;
+  for (const uint64_t *p : src) g.p[k++] = p;
+  hipLaunchKernelGGL(cpk::gather8_kernel, dim3(1), dim3(64), 0, s, g, k, ctx->probe_pin);
+  if (hipStreamSynchronize(s) != hipSuccess) return CPK_EDEVICE;
+  for (uint32_t i = 0; i < k; ++i) dst[i] = ctx->probe_pin[i];
+  return CPK_OK;
+}
+
 // Single-pass encoder (encode_sp.hip): one launch, the look-back words
 // epoch-tagged (cleared only when the epoch wraps or the array grows).  Work
 // is ticketed per 8192-word chunk of a piece (a unit); a batch whose pieces
@@ -2067,10 +2094,8 @@ static int e4_rows(cpk_ctx ctx, const uint64_t *d_swo, uint32_t n, uint64_t hint
     rows = (uint64_t)(n ? n : 1) * stride;
   } else {
     uint64_t ends[2];
-    if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return CPK_EDEVICE;
+    int rc = read_words(ctx, s, {d_swo, d_swo + n}, ends);
+    if (rc) return rc;
     rows = (ends[1] - ends[0]) / 64 + n + 1;
   }
   if (rows > ctx->e4_bv_cap) {
@@ -2242,10 +2267,8 @@ int cpk_encode_batch_cap(cpk_ctx ctx, const void *d_in, const uint64_t *d_swo, u
     uint64_t hint = max_seg_words;
     if (!hint) {  // (no bound given: the batch's words bound every piece)
       uint64_t ends[2];
-      if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-          hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess)
-        return CPK_EDEVICE;
+      int rc = read_words(ctx, s, {d_swo, d_swo + n}, ends);
+      if (rc) return rc;
       hint = ends[1] - ends[0];
     }
     uint64_t ub = sp_unit_bound(n, hint);
@@ -2365,16 +2388,11 @@ static int decode_batch_impl(cpk_ctx ctx, const void *d_packed, const uint64_t *
     // blocks in parallel, and let the batch decoders skip when every piece
     // ended exactly at its packed range's end (dec_stream_check_kernel);
     // otherwise they run after it and report the batch form's statuses.
-    // (one small kernel writes the four words to pinned host memory: four
-    // copies into pageable memory cost ~75 us per call, ADVICE r5,
-    // profiles/r6b_small_decode_launch_overhead.txt)
-    if (!ctx->probe_pin && hipHostMalloc((void **)&ctx->probe_pin, 4 * 8, hipHostMallocDefault) != hipSuccess) {
-      ctx->probe_pin = nullptr;
-      return CPK_ENOMEM;
-    }
-    hipLaunchKernelGGL(cpk::dec_probe_kernel, dim3(1), dim3(64), 0, s, d_in_off, d_swo, n, ctx->probe_pin);
-    if (hipStreamSynchronize(s) != hipSuccess) return CPK_EDEVICE;
-    const uint64_t *e = ctx->probe_pin;
+    // (through pinned memory: four copies into pageable memory cost ~75 us
+    // per call, ADVICE r5, profiles/r6b_small_decode_launch_overhead.txt)
+    uint64_t e[4];
+    int rc0 = read_words(ctx, s, {d_in_off, d_in_off + n, d_swo, d_swo + n}, e);
+    if (rc0) return rc0;
     if (e[3] - e[2] >= ((uint64_t)n << 20) && (e[0] & 15) == 0 && e[1] >= e[0]) {
       if (!ctx->fl_buf && hipMalloc(&ctx->fl_buf, 33 * 8) != hipSuccess) return CPK_ENOMEM;
       int rc = cpk_decode_stream(ctx, (const uint8_t *)d_packed + e[0], e[1] - e[0], d_swo, n, d_out, ctx->fl_buf,
@@ -2512,10 +2530,8 @@ int cpk_decode_stream(cpk_ctx ctx, const void *d_packed, uint64_t avail,
     // the stream's word count bounds the bytes worth cutting into blocks
     // (the rest of `avail` may be later messages): read it back
     uint64_t ends[2];
-    if (hipMemcpyAsync(&ends[0], d_swo, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&ends[1], d_swo + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return CPK_EDEVICE;
+    int rc = read_words(ctx, s, {d_swo, d_swo + n}, ends);
+    if (rc) return rc;
     const uint64_t reach = ss_reach(avail, ends[1] - ends[0]);
     if (reach >= kSsMin)
       return ss_decode(ctx, (const uint8_t *)d_packed, avail, reach, d_swo, n, (uint64_t *)d_out, d_in_off,
@@ -2661,13 +2677,16 @@ int cpk_decode_messages(cpk_ctx ctx, const void *d_packed, const uint64_t *d_msg
   hipLaunchKernelGGL(cpk::e4_scan_down, dim3(nb), dim3(cpk::kE4ScanThreads), 0, s,
                      (const uint64_t *)d_msg_seg_off, nm, (const uint64_t *)bs1, d_msg_seg_off);
   uint64_t pk[2] = {0, 0};  // the messages' packed range (the decoder's density choice)
-  if (hipGetLastError() != hipSuccess ||
-      hipMemcpyAsync(&h_totals[0], mwoff + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(&h_totals[1], d_msg_seg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(&pk[0], d_msg_off, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(&pk[1], d_msg_off + nm, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess)
-    return CPK_EDEVICE;
+  if (hipGetLastError() != hipSuccess) return CPK_EDEVICE;
+  {
+    uint64_t w[4];
+    const int rcw = read_words(ctx, s, {mwoff + nm, d_msg_seg_off + nm, d_msg_off, d_msg_off + nm}, w);
+    if (rcw) return rcw;
+    h_totals[0] = w[0];
+    h_totals[1] = w[1];
+    pk[0] = w[2];
+    pk[1] = w[3];
+  }
   if (h_totals[0] > out_cap_words || h_totals[1] > seg_cap) return CPK_ENOMEM;
   if (h_totals[1] && (!d_seg_word_off || !d_seg_in_off || !d_seg_status)) return CPK_EINVAL;
   if (!d_seg_word_off) return CPK_OK;  // (no segments: every table failed)
